@@ -1,0 +1,220 @@
+#!/usr/bin/env python3
+"""Benchmark: env-steps/s of the batched Drone2dEnv step at 65 536 envs per MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+A "step" = one ``d2d_step`` (libdrone2d_hip.so) over all envs of a GPU: thrust -> Chipmunk-
+equivalent 3-body/6-joint solve -> collision -> 3-nearest sensing -> Brent closest point ->
+27-dim obs -> reward/termination -> in-kernel auto-reset.  Workload (BASELINE.json configs[2]):
+65 536 envs per GPU on the ``corridor`` test scenario (18 circles), U(-1,1) float32 actions
+pre-generated on the device (a bank of 16, cycled), inputs resident in HBM before timing.
+Multi-GPU: one process per GPU, each with its own 65 536 envs (weak scaling, global env ids), no
+collective in the step; the episode statistics are all-reduced once per timed interval (RCCL).
+
+Prints ONE JSON line (rank 0).  ``roofline.achieved`` = 650 algorithmic bytes per env-step x envs
+per launch / mean step-kernel duration (HIP events on the launch stream); ``cpu_baseline`` = the C
+oracle (a scalar port of the same algorithm) timed on this host's cores on a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "env-steps/sec at 65 536 parallel envs; 1/2/4/8 MI355X scaling"
+ENVS_PER_GPU = 65536
+SCENARIO = "corridor"
+BYTES_PER_ENV_STEP = 650   # DESIGN.md "Algorithmic bytes": 272 read + 378 written, info off
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec)
+ACTION_BANK = 16
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=1000)
+    p.add_argument("--warmup", type=int, default=50)
+    p.add_argument("--envs", type=int, default=ENVS_PER_GPU)
+    p.add_argument("--scenario", default=SCENARIO)
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--graph", action="store_true", help="replay the step loop as a hipGraph")
+    return p.parse_args()
+
+
+def setup_dist(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return rank, world, local
+
+
+def barrier_sync(world):
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+
+def cpu_baseline(args, kwargs):
+    """Time the C oracle on a bounded sample of the same workload (test infrastructure)."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+
+    import drone2d_amd as d2  # noqa: F401
+    from drone2d_amd.config import make_cfg
+    from drone2d_amd.env import build_scenarios
+
+    oracle.build()
+    threads = min(len(os.sched_getaffinity(0)), 16)
+    n = args.envs
+    scn = [s.to_c() for s in build_scenarios(kwargs, args.scenario)]
+    b = oracle.OracleBatch(make_cfg(dict(kwargs)), scn, n)
+    b.reset(0)
+    rng = np.random.default_rng(0)
+    act = rng.uniform(-1, 1, (n, 2)).astype(np.float32)
+    t0 = time.perf_counter()
+    b.step(act, nthreads=threads)  # one step to size the sample
+    one = time.perf_counter() - t0
+    steps = max(1, min(200, int(args.cpu_seconds / max(one, 1e-6))))
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        b.step(act, nthreads=threads)
+    dt = time.perf_counter() - t0
+    b.close()
+    return {"value": n * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "sample": f"C oracle (oracle/d2d_oracle.c, scalar fp64 port of the reference step), "
+                      f"{n} envs x {steps} steps of {args.scenario} with auto-reset, {threads} threads, "
+                      f"{dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    rank, world, local = setup_dist(args)
+    import drone2d_amd as d2
+    from drone2d_amd.config import ENV_TRAIN_CONFIG
+
+    kwargs = dict(ENV_TRAIN_CONFIG, scenario=args.scenario)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    n = args.envs
+    venv = d2.Drone2dVecEnv(n, device=dev, seed=12345, env_id_offset=rank * n, with_info=False, **kwargs)
+    g = torch.Generator(device=dev).manual_seed(1000 + rank)
+    bank = [(torch.rand(n, 2, device=dev, generator=g) * 2 - 1).contiguous() for _ in range(ACTION_BANK)]
+    venv.reset()
+    stream = torch.cuda.current_stream(dev)
+
+    for k in range(args.warmup):
+        venv.step(bank[k % ACTION_BANK])
+    venv.episode_stats(clear=True)
+
+    graph = None
+    if args.graph:
+        # capture ACTION_BANK steps (even count: the output double-buffer returns to its start)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            for k in range(ACTION_BANK):
+                venv.step(bank[k])
+        torch.cuda.synchronize()
+
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    barrier_sync(world)
+    t0 = time.perf_counter()
+    if graph is not None:
+        reps = (args.steps + ACTION_BANK - 1) // ACTION_BANK
+        for r in range(reps):
+            starts[r].record(stream)
+            graph.replay()
+            ends[r].record(stream)
+        n_timed = reps * ACTION_BANK
+    else:
+        for k in range(args.steps):
+            starts[k].record(stream)
+            venv.step(bank[k % ACTION_BANK])
+            ends[k].record(stream)
+        n_timed = args.steps
+    barrier_sync(world)
+    wall = time.perf_counter() - t0
+
+    # episode statistics of the interval: the one RCCL all-reduce (timed separately)
+    stats = venv.episode_stats(clear=True)
+    torch.cuda.synchronize()
+    t_ar = 0.0
+    if world > 1:
+        t1 = time.perf_counter()
+        dist.all_reduce(stats)
+        torch.cuda.synchronize()
+        t_ar = time.perf_counter() - t1
+    if graph is not None:
+        kern_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts[:reps], ends[:reps])])) / ACTION_BANK
+    else:
+        kern_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
+
+    wall_t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    kern_t = torch.tensor([kern_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(kern_t, op=dist.ReduceOp.MAX)
+    wall = float(wall_t.item())
+    kern_ms = float(kern_t.item())
+
+    if rank == 0:
+        total_steps = n * world * n_timed
+        value = total_steps / wall
+        achieved = BYTES_PER_ENV_STEP * n / (kern_ms * 1e-3) / 1e9
+        st = stats.cpu().numpy()
+        traffic = None
+        tf = os.path.join(REPO, "profiles", f"traffic_{args.scenario}_{n}.json")
+        if os.path.exists(tf):
+            traffic = json.load(open(tf)).get("bytes_per_launch")
+        line = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "env-steps/s",
+            "n_gpus": world,
+            "steps": n_timed,
+            "warmup": args.warmup,
+            "ms_per_step": wall * 1e3 / n_timed,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic",
+            "config": {"workload": f"{args.scenario}, {n} envs per GPU, U(-1,1) f32 actions, in-kernel auto-reset",
+                       "envs_per_gpu": n, "total_envs": n * world, "scenario": args.scenario,
+                       "parallelism": f"env-shard x{world}", "hipgraph": bool(graph is not None),
+                       "outputs": "obs f32[N,27], reward f32, terminated/truncated u8 (info rows off)"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "d2d_step_kernel", "kernel_ms": kern_ms,
+                         "bytes_per_env_step": BYTES_PER_ENV_STEP},
+            "episodes": {"finished": float(st[1]), "mean_return": float(st[0] / max(st[1], 1)),
+                         "success": float(st[2]), "collisions": float(st[4]),
+                         "allreduce_ms": t_ar * 1e3},
+        }
+        if not args.no_cpu_baseline and world == 1:
+            line["cpu_baseline"] = cpu_baseline(args, kwargs)
+        print(json.dumps(line), flush=True)
+    venv.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

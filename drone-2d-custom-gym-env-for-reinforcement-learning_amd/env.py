@@ -1,0 +1,298 @@
+"""Python facade over the HIP library: the reference's ``Drone2dEnv`` surface, batched.
+
+``Drone2dVecEnv``  N envs on one GPU; tensor fast path (torch-ROCm tensors in, out).
+``Drone2dEnv``     one env with the reference's gym-0.21 API (drone_2d_env.py:22-1023):
+                   ``reset() -> obs``, ``step(a) -> (obs, reward, done, info)``.
+
+Both take the reference's kwargs dict (rl_config.py:10-44, read at drone_2d_env.py:34-66).
+Every step runs ``d2d_step`` (libdrone2d_hip.so) on the caller's current HIP stream; there is no
+CPU or PyTorch fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Sequence
+
+import numpy as np
+import torch
+
+from . import abi
+from ._native import check, load
+from .config import CURRICULUM_STAGES, TEST_SCENARIOS, make_cfg
+from .scenarios import Scenario, create_test_scenario, free_flight
+
+INFO_KEYS = ("reward", "collision_avoidance_reward", "path_adherence", "path_progression", "collision_reward",
+             "reach_end_reward", "agressive_alpha_reward", "dist_closest_obs", "env_steps")
+
+
+class Box:
+    """Duck-typed ``gym.spaces.Box`` (gym/gymnasium are used when importable)."""
+
+    def __init__(self, low, high, dtype=np.float32):
+        self.low = np.asarray(low, dtype=dtype)
+        self.high = np.asarray(high, dtype=dtype)
+        self.shape = self.low.shape
+        self.dtype = np.dtype(dtype)
+
+    def sample(self):
+        return np.random.uniform(self.low, self.high).astype(self.dtype)
+
+    def contains(self, x):
+        x = np.asarray(x)
+        return x.shape == self.shape and bool(np.all(x >= self.low) and np.all(x <= self.high))
+
+
+def _make_box(low, high):
+    for mod in ("gymnasium", "gym"):
+        try:
+            spaces = __import__(mod + ".spaces", fromlist=["Box"])
+            return spaces.Box(low=np.asarray(low, np.float32), high=np.asarray(high, np.float32), dtype=np.float32)
+        except Exception:  # noqa: BLE001 -- optional dependency
+            continue
+    return Box(low, high)
+
+
+def build_scenarios(kwargs: dict, scenario=None) -> list[Scenario]:
+    """Scenario list for ``mode='test'``: one name, a list of names, or Scenario objects."""
+    W, H = kwargs["screensize_x"], kwargs["screensize_y"]
+    spec = kwargs["scenario"] if scenario is None else scenario
+    if isinstance(spec, (str, Scenario)):
+        spec = [spec]
+    out = []
+    for s in spec:
+        if isinstance(s, Scenario):
+            out.append(s)
+        elif s in TEST_SCENARIOS:
+            out.append(create_test_scenario(s, W, H))
+        elif isinstance(s, str) and s.endswith("_free") and s[:-5] in TEST_SCENARIOS:
+            out.append(free_flight(create_test_scenario(s[:-5], W, H)))
+        elif s in CURRICULUM_STAGES or kwargs["mode"] == "curriculum":
+            raise NotImplementedError("curriculum stages are not implemented in this build (SURVEY.md §8f row 2)")
+        else:
+            raise ValueError(f"unknown scenario {s!r}")
+    return out
+
+
+class Drone2dVecEnv:
+    """``num_envs`` independent Drone2dEnv copies stepping together on one GPU.
+
+    Parameters mirror the reference kwargs; extra knobs:
+      scenario        override kwargs['scenario'] (name, list of names, or Scenario objects)
+      env_scenario    int array [num_envs] mapping env -> scenario index (default: i % n_scenarios)
+      env_id_offset   global id of env 0 (multi-GPU shards keep per-env RNG streams global)
+      auto_reset      SB3 VecEnv semantics (done envs are reset inside the step kernel)
+      timeup_truncates  report time-up as truncation instead of termination (reference: False)
+    """
+
+    def __init__(self, num_envs: int, device=None, seed: int = 0, *, scenario=None,
+                 env_scenario: Sequence[int] | None = None, auto_reset: bool = True,
+                 timeup_truncates: bool = False, with_info: bool = True, env_id_offset: int = 0, **kwargs):
+        self.kwargs = dict(kwargs)
+        self._lib = load()
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise ValueError("Drone2dVecEnv runs on a HIP device only (device='cuda[:k]')")
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        self.num_envs = int(num_envs)
+        self.cfg = make_cfg(self.kwargs, auto_reset=auto_reset, timeup_truncates=timeup_truncates,
+                            env_id_base=env_id_offset)
+        self.scenarios = build_scenarios(self.kwargs, scenario)
+        self.seed_value = int(seed)
+        self.with_info = with_info
+        self.action_space = _make_box(-np.ones(2), np.ones(2))
+        self.observation_space = _make_box(-np.ones(27), np.ones(27))
+
+        h = C.c_void_p()
+        check(self._lib.d2d_create(C.byref(self.cfg), self.num_envs, self.device.index, C.byref(h)), "d2d_create")
+        self._h = h
+        n_scn = len(self.scenarios)
+        arr = (abi.D2DScn * n_scn)(*[s.to_c() for s in self.scenarios])
+        if env_scenario is None:
+            env_scenario = np.arange(self.num_envs) % n_scn
+        es = np.ascontiguousarray(np.asarray(env_scenario, dtype=np.int32))
+        if es.shape != (self.num_envs,):
+            raise ValueError("env_scenario must have shape [num_envs]")
+        self.env_scenario = es
+        check(self._lib.d2d_set_scenarios(h, arr, n_scn, es.ctypes.data_as(C.POINTER(C.c_int32))), "d2d_set_scenarios")
+
+        N, dev = self.num_envs, self.device
+        # double-buffered outputs: the tensors returned by step k stay valid during step k+1
+        self._bufs = [dict(obs=torch.empty(N, abi.OBS_DIM, dtype=torch.float32, device=dev),
+                           rew=torch.empty(N, dtype=torch.float32, device=dev),
+                           term=torch.empty(N, dtype=torch.uint8, device=dev),
+                           trunc=torch.empty(N, dtype=torch.uint8, device=dev),
+                           info=torch.empty(N, abi.INFO_DIM, dtype=torch.float32, device=dev),
+                           tobs=torch.zeros(N, abi.OBS_DIM, dtype=torch.float32, device=dev))
+                      for _ in range(2)]
+        self._k = 0
+        self._stats = torch.zeros(abi.NSTATS, dtype=torch.float64, device=dev)
+
+    # ------------------------------------------------------------------ plumbing
+    def _stream(self):
+        return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    @staticmethod
+    def _ptr(t):
+        return C.c_void_p(t.data_ptr()) if t is not None else None
+
+    def close(self):
+        if getattr(self, "_h", None):
+            torch.cuda.synchronize(self.device)
+            self._lib.d2d_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+    # ------------------------------------------------------------------ API
+    def reset(self, seed: int | None = None, mask: torch.Tensor | None = None) -> torch.Tensor:
+        """Reset all envs (or those with ``mask`` set); returns obs [N, 27] float32."""
+        if seed is not None:
+            self.seed_value = int(seed)
+        b = self._bufs[self._k]
+        m = None
+        if mask is not None:
+            m = mask.to(device=self.device, dtype=torch.uint8).contiguous()
+        check(self._lib.d2d_reset(self._h, self._ptr(m), C.c_uint64(self.seed_value & (2 ** 64 - 1)),
+                                  self._ptr(b["obs"]), self._stream()), "d2d_reset")
+        return b["obs"]
+
+    def _prep_actions(self, actions) -> torch.Tensor:
+        if not isinstance(actions, torch.Tensor):
+            actions = torch.as_tensor(np.asarray(actions, dtype=np.float32))
+        a = actions.to(device=self.device, dtype=torch.float32).reshape(self.num_envs, abi.ACT_DIM).contiguous()
+        return a
+
+    def step(self, actions):
+        """Tensor fast path: returns (obs, reward, terminated, truncated, info) device tensors.
+
+        ``obs`` rows of finished envs already hold the reset observation (auto-reset); their
+        pre-reset observation is in ``self.terminal_obs``.  ``info`` is the float32 [N, 12] table
+        of include/drone2d.h (D2D_INFO_*), or None when ``with_info=False``.
+        """
+        a = self._prep_actions(actions)
+        self._k ^= 1
+        b = self._bufs[self._k]
+        check(self._lib.d2d_step(self._h, self._ptr(a), self._ptr(b["obs"]), self._ptr(b["rew"]),
+                                 self._ptr(b["term"]), self._ptr(b["trunc"]),
+                                 self._ptr(b["info"]) if self.with_info else None,
+                                 self._ptr(b["tobs"]), self._stream()), "d2d_step")
+        self._last_actions = a  # keep alive until the kernel has consumed it
+        return b["obs"], b["rew"], b["term"].bool(), b["trunc"].bool(), (b["info"] if self.with_info else None)
+
+    @property
+    def terminal_obs(self) -> torch.Tensor:
+        return self._bufs[self._k]["tobs"]
+
+    def get_state(self):
+        st = torch.empty(abi.NSTATE, self.num_envs, dtype=torch.float64, device=self.device)
+        ist = torch.empty(abi.NISTATE, self.num_envs, dtype=torch.int32, device=self.device)
+        check(self._lib.d2d_get_state(self._h, self._ptr(st), self._ptr(ist), self._stream()), "d2d_get_state")
+        return st, ist
+
+    def set_state(self, state: torch.Tensor | None, istate: torch.Tensor | None = None):
+        st = None if state is None else state.to(self.device, torch.float64).contiguous()
+        ist = None if istate is None else istate.to(self.device, torch.int32).contiguous()
+        check(self._lib.d2d_set_state(self._h, self._ptr(st), self._ptr(ist), self._stream()), "d2d_set_state")
+        self._keep = (st, ist)
+
+    def episode_stats(self, clear: bool = True) -> torch.Tensor:
+        """float64 [8]: (sum return, episodes, successes, fails, collisions, sum APE, sum len, 0)."""
+        check(self._lib.d2d_episode_stats(self._h, self._ptr(self._stats), 1 if clear else 0, self._stream()),
+              "d2d_episode_stats")
+        return self._stats
+
+
+def info_dicts(info_row: np.ndarray, n_obstacles: int) -> dict:
+    """Rebuild the reference's ``info`` dict (drone_2d_env.py:575-613) from one info row."""
+    cause = int(info_row[abi.INFO_CAUSE])
+    d = {
+        "reward": float(info_row[abi.INFO_REWARD]),
+        "collision_avoidance_reward": float(info_row[abi.INFO_CA]),
+        "path_adherence": float(info_row[abi.INFO_PA]),
+        "path_progression": float(info_row[abi.INFO_PP]),
+        "collision_reward": float(info_row[abi.INFO_COLL]),
+        "reach_end_reward": float(info_row[abi.INFO_REACH]),
+        "agressive_alpha_reward": float(info_row[abi.INFO_AA]),
+        "env_steps": int(info_row[abi.INFO_STEPS]),
+        "dist_closest_obs": float(info_row[abi.INFO_DCLOSE]) if n_obstacles else float("inf"),
+        "APE": 0, "total_reward": 0, "n_collisions": 0, "n_successful_runs": 0, "n_failed_runs": 0,
+        "flight_path": 0,
+    }
+    if cause:
+        c1, c2 = bool(cause & abi.END_COLLISION), bool(cause & abi.END_REACH)
+        c4, c5 = bool(cause & abi.END_TIMEUP), bool(cause & abi.END_AA)
+        # the same overwrite order as drone_2d_env.py:595-610
+        if c1:
+            d["n_collisions"], d["n_failed_runs"] = 1, 1
+        if c2:
+            d["n_collisions"], d["n_successful_runs"] = 0, 1
+        if c4:
+            d["n_collisions"], d["n_failed_runs"] = 0, 1
+        if c5:
+            d["n_collisions"], d["n_failed_runs"] = 0, 1
+        d["APE"] = float(info_row[abi.INFO_APE])
+        d["total_reward"] = float(info_row[abi.INFO_TOTREW])
+    return d
+
+
+class Drone2dEnv:
+    """Single environment with the reference's gym-0.21 API (``reset() -> obs``,
+    ``step(a) -> (obs, reward, done, info)``), backed by a 1-env HIP batch.
+
+    Differences, all deliberate: observations are float32 values returned as a float64 array
+    (the reference builds float64 from the same expressions); the spawn draw comes from the
+    library's Philox stream instead of Python's unseeded ``random``; render keys are ignored.
+    """
+
+    metadata = {"render.modes": []}
+
+    def __init__(self, **kwargs):
+        self.kwargs = dict(kwargs)
+        self._venv = Drone2dVecEnv(1, seed=int(kwargs.get("seed", 0)), auto_reset=False,
+                                   **{k: v for k, v in kwargs.items() if k != "seed"})
+        self.action_space = self._venv.action_space
+        self.observation_space = self._venv.observation_space
+        self._n_obs = len(self._venv.scenarios[0].circles)
+        self.flight_path = []
+        self._done = False
+        self.reset()  # the reference spawns in __init__ (drone_2d_env.py:144)
+
+    def seed(self, seed=None):
+        if seed is not None:
+            self._venv.seed_value = int(seed)
+        return [self._venv.seed_value]
+
+    def reset(self):
+        obs = self._venv.reset()
+        self._done = False
+        self.flight_path = []
+        return obs[0].double().cpu().numpy()
+
+    def step(self, action):
+        a = torch.as_tensor(np.asarray(action, dtype=np.float32)).reshape(1, 2)
+        obs, rew, term, trunc, info = self._venv.step(a)
+        o = obs[0].double().cpu().numpy()
+        r = float(rew[0].item())
+        done = bool(term[0].item() or trunc[0].item()) or self._done  # self.done is sticky (:594)
+        d = info_dicts(info[0].cpu().numpy(), self._n_obs)
+        if self.kwargs.get("render_path"):
+            st, _ = self._venv.get_state()
+            x, y = float(st[0, 0]), float(st[1, 0])
+            self.flight_path.append((x, float(self.kwargs["screensize_y"]) - y))
+            if done:
+                d["flight_path"] = list(self.flight_path)
+        self._done = done
+        return o, r, done, d
+
+    def render(self, mode="human", close=False):
+        return None
+
+    def close(self):
+        self._venv.close()

@@ -1,0 +1,752 @@
+/*
+ * d2d_oracle.c -- CPU restatement of the reference's hot path, used as the PARITY ORACLE.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+ * leg load this library; the product (libdrone2d_hip.so + the Python package) never does.
+ *
+ * What it restates (reference = /root/reference/drone_2d_custom_gym_env, snapshot 2025-01-12):
+ *   - Drone2dEnv.step            drone_2d_env.py:394-615   -> o_step_env()
+ *   - Drone2dEnv.get_observation drone_2d_env.py:631-773   -> o_observe()
+ *   - get_obstacle_distances     drone_2d_env.py:617-629, distance_between_shapes :948-961
+ *   - m1to1 / invm1to1           drone_2d_env.py:972-978
+ *   - ssa / R_w_b                transformations.py:6-11
+ *   - QPMI2D.__call__            predef_path.py:88-142 (+ get_u_index :53-63, mu_r/mu_f :66-86)
+ *   - get_closest_u              predef_path.py:226-248 -> scipy.optimize.fminbound
+ *                                (scipy 1.15.3 _optimize.py:2251-2398, restated in o_fminbound)
+ *   - lookahead / LA lock        predef_path.py:257-266, drone_2d_env.py:737-749
+ *   - test-mode reset            drone_2d_env.py:218-311, Drone.py:9-95
+ *   - Chipmunk2D 7 cpSpaceStep for the Drone.py configuration (third-party C, absent here):
+ *     SURVEY.md Appendix A.  PARITY UNPINNED for this part (no Chipmunk source / pymunk offline);
+ *     pinned only by physics known-answer tests and by the independent Python restatement in
+ *     tests/golden/ref_shims.py.  Everything else is pinned by the tests/golden npz fixtures, recorded from
+ *     the reference's own Python.
+ *
+ * Floating point follows the reference's NumPy evaluation order exactly.  Compiled with
+ * -ffp-contract=off; the two places where NumPy itself fuses (np.linalg.norm of a 2-vector and a
+ * 2x2 np.matmul, both through OpenBLAS) use explicit fma() in the same order NumPy does.
+ */
+#include "d2d_oracle.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------------------------------ */
+/* Python / NumPy scalar helpers                                                               */
+/* ------------------------------------------------------------------------------------------ */
+static const double PI = 3.141592653589793;      /* np.pi */
+static const double TWO_PI = 6.283185307179586;  /* 2*np.pi */
+
+/* Python/NumPy float modulo (npy_remainder / float_rem): fmod, then shift into divisor's sign */
+static double pymod(double a, double b) {
+    double m = fmod(a, b);
+    if (m != 0.0) {
+        if ((b < 0.0) != (m < 0.0)) m += b;
+    } else {
+        m = copysign(0.0, b);
+    }
+    return m;
+}
+/* transformations.py:6-7 */
+static double ssa(double a) { return pymod(a + PI, TWO_PI) - PI; }
+/* drone_2d_env.py:972-978 */
+static double m1to1(double v, double lo, double hi) { return 2.0 * (v - lo) / (hi - lo) - 1.0; }
+static double invm1to1(double v, double lo, double hi) { return (v + 1.0) * (hi - lo) / 2.0 + lo; }
+/* np.clip on scalars (NaN propagates) */
+static double clip(double x, double lo, double hi) { return x < lo ? lo : (x > hi ? hi : x); }
+/* np.linalg.norm([dx, dy]) = sqrt(ddot) ; OpenBLAS ddot here = fma(dy, dy, dx*dx) */
+static double norm2(double dx, double dy) { return sqrt(fma(dy, dy, dx * dx)); }
+/* np.sign(x) + (x == 0) as used by fminbound */
+static double sgn_nz(double x) {
+    double s = (x > 0.0) ? 1.0 : ((x < 0.0) ? -1.0 : (x == 0.0 ? 0.0 : x));
+    return s + (x == 0.0 ? 1.0 : 0.0);
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Philox4x32-10 counter RNG: the build's own spawn RNG (the reference uses Python's unseeded    */
+/* `random`, drone_2d_env.py:229-232, which cannot be reproduced; see DESIGN.md "Reset").        */
+/* ------------------------------------------------------------------------------------------ */
+static void philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1,
+                   uint32_t out[4]) {
+    for (int r = 0; r < 10; ++r) {
+        uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+        uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+        uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+        uint32_t n1 = (uint32_t)p1;
+        uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        uint32_t n3 = (uint32_t)p0;
+        c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+/* Python random.random(): (a>>5 * 2^26 + b>>6) / 2^53 */
+static double u53(uint32_t a, uint32_t b) {
+    return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * (1.0 / 9007199254740992.0);
+}
+void d2dcpu_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+    philox(ctr[0], ctr[1], ctr[2], ctr[3], key[0], key[1], out);
+}
+void d2dcpu_spawn_uniforms(uint64_t seed, uint32_t env_id, uint32_t episode, double u[3]) {
+    uint32_t o[4];
+    philox(env_id, episode, 0u, 0u, (uint32_t)seed, (uint32_t)(seed >> 32), o);
+    u[0] = u53(o[0], o[1]);
+    u[1] = u53(o[2], o[3]);
+    philox(env_id, episode, 1u, 0u, (uint32_t)seed, (uint32_t)(seed >> 32), o);
+    u[2] = u53(o[0], o[1]);
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* QPMI2D path (predef_path.py)                                                                */
+/* ------------------------------------------------------------------------------------------ */
+/* get_u_index, predef_path.py:53-63 */
+static int o_get_u_index(const d2d_scn* s, double u) {
+    int n = 0;
+    while (n < s->n_wps - 1) {
+        if (u <= s->us[n + 1]) break;
+        n += 1;
+    }
+    return n;
+}
+static void quad(const d2d_scn* s, int k, double u, double* x, double* y) {
+    /* ax*u**2 + bx*u + cx */
+    *x = s->xa[k] * (u * u) + s->xb[k] * u + s->xc[k];
+    *y = s->ya[k] * (u * u) + s->yb[k] * u + s->yc[k];
+}
+/* QPMI2D.__call__, predef_path.py:88-142 */
+void d2dcpu_path_eval(const d2d_scn* s, double u, double* x, double* y) {
+    const int nw = s->n_wps, nseg = nw - 2;
+    const double* us = s->us;
+    if (u >= us[0] && u <= us[1]) {
+        quad(s, 0, u, x, y);
+    } else if ((u >= us[nw - 2] - 0.001 && u <= us[nw - 1]) || o_get_u_index(s, u) == nw - 1) {
+        quad(s, nseg - 1, u, x, y);
+    } else {
+        int n = o_get_u_index(s, u);
+        double mu_r = (u - us[n]) / (us[n + 1] - us[n]);
+        double mu_f = (us[n + 1] - u) / (us[n + 1] - us[n]);
+        int k1 = (n - 1 < 0) ? n - 1 + nseg : n - 1; /* python x_params[n-1], n=0 -> [-1] */
+        double x1, y1, x2, y2;
+        quad(s, k1, u, &x1, &y1);
+        quad(s, n, u, &x2, &y2);
+        *x = mu_r * x2 + mu_f * x1;
+        *y = mu_r * y2 + mu_f * y1;
+    }
+}
+/* lambda u: np.linalg.norm(self(u) - position), predef_path.py:246 */
+static double path_dist(const d2d_scn* s, double u, double px, double py) {
+    double x, y;
+    d2dcpu_path_eval(s, u, &x, &y);
+    return norm2(x - px, y - py);
+}
+/* scipy.optimize.fminbound -> _minimize_scalar_bounded (scipy 1.15.3 _optimize.py:2251-2398) */
+double d2dcpu_fminbound(const d2d_scn* s, double px, double py, double x1, double x2, double xatol,
+                        int maxfun, int* nfev) {
+    const double sqrt_eps = sqrt(2.2e-16);
+    const double golden_mean = 0.5 * (3.0 - sqrt(5.0));
+    double a = x1, b = x2;
+    double fulc = a + golden_mean * (b - a);
+    double nfc = fulc, xf = fulc;
+    double rat = 0.0, e = 0.0;
+    double x = xf;
+    double fx = path_dist(s, x, px, py);
+    int num = 1;
+    double fu = INFINITY;
+    double ffulc = fx, fnfc = fx;
+    double xm = 0.5 * (a + b);
+    double tol1 = sqrt_eps * fabs(xf) + xatol / 3.0;
+    double tol2 = 2.0 * tol1;
+    (void)fu;
+    while (fabs(xf - xm) > (tol2 - 0.5 * (b - a))) {
+        int golden = 1;
+        if (fabs(e) > tol1) {
+            golden = 0;
+            double r = (xf - nfc) * (fx - ffulc);
+            double q = (xf - fulc) * (fx - fnfc);
+            double p = (xf - fulc) * q - (xf - nfc) * r;
+            q = 2.0 * (q - r);
+            if (q > 0.0) p = -p;
+            q = fabs(q);
+            r = e;
+            e = rat;
+            if ((fabs(p) < fabs(0.5 * q * r)) && (p > q * (a - xf)) && (p < q * (b - xf))) {
+                rat = (p + 0.0) / q;
+                x = xf + rat;
+                if (((x - a) < tol2) || ((b - x) < tol2)) {
+                    double si = sgn_nz(xm - xf);
+                    rat = tol1 * si;
+                }
+            } else {
+                golden = 1;
+            }
+        }
+        if (golden) {
+            if (xf >= xm) e = a - xf;
+            else e = b - xf;
+            rat = golden_mean * e;
+        }
+        double si = sgn_nz(rat);
+        double ar = fabs(rat);
+        double mx = (ar != ar) ? ar : (ar > tol1 ? ar : tol1); /* np.maximum propagates NaN */
+        x = xf + si * mx;
+        fu = path_dist(s, x, px, py);
+        num += 1;
+        if (fu <= fx) {
+            if (x >= xf) a = xf;
+            else b = xf;
+            fulc = nfc; ffulc = fnfc;
+            nfc = xf; fnfc = fx;
+            xf = x; fx = fu;
+        } else {
+            if (x < xf) a = x;
+            else b = x;
+            if ((fu <= fnfc) || (nfc == xf)) {
+                fulc = nfc; ffulc = fnfc;
+                nfc = x; fnfc = fu;
+            } else if ((fu <= ffulc) || (fulc == xf) || (fulc == nfc)) {
+                fulc = x; ffulc = fu;
+            }
+        }
+        xm = 0.5 * (a + b);
+        tol1 = sqrt_eps * fabs(xf) + xatol / 3.0;
+        tol2 = 2.0 * tol1;
+        if (num >= maxfun) break;
+    }
+    if (nfev) *nfev = num;
+    return xf;
+}
+/* get_closest_u, predef_path.py:226-248 (margin 10, xtol 1e-6, maxfun 500) */
+double d2dcpu_closest_u(const d2d_scn* s, double px, double py, int* nfev) {
+    const double L = s->us[s->n_wps - 1];
+    return d2dcpu_fminbound(s, px, py, 0.0 - 10.0, L + 10.0, 1e-6, 500, nfev);
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* Chipmunk2D 7 step restated for the Drone.py configuration             */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct { double px, py, a, vx, vy, w, c, s, fx, fy, t, m_inv, i_inv; } obody;
+
+/* cpMomentForPoly(m, box verts in cpBoxShapeNew2 order, offset 0, r 0) */
+static double moment_box(double m, double w, double h) {
+    const double hw = w / 2.0, hh = h / 2.0;
+    const double vx[4] = {hw, hw, -hw, -hw}, vy[4] = {-hh, hh, hh, -hh};
+    double s1 = 0.0, s2 = 0.0;
+    for (int i = 0; i < 4; ++i) {
+        double v1x = vx[i] + 0.0, v1y = vy[i] + 0.0;
+        double v2x = vx[(i + 1) % 4] + 0.0, v2y = vy[(i + 1) % 4] + 0.0;
+        double a = v2x * v1y - v2y * v1x;
+        double b = (v1x * v1x + v1y * v1y) + (v1x * v2x + v1y * v2y) + (v2x * v2x + v2y * v2y);
+        s1 += a * b;
+        s2 += a;
+    }
+    return (m * s1) / (6.0 * s2);
+}
+/* Drone.py:9-95 with height=20, width=100, masses 0.2/0.4/0.4 (drone_2d_env.py:233) */
+static const double FRAME_W = 100.0, FRAME_H = 10.0, MOTOR_S = 20.0;
+static const double M_F = 0.2, M_M = 0.4;
+static const double DRONE_R = 40.0; /* width/2 - height/2 */
+static const double JA[6] = {-7.0, 0.0, 7.0, -7.0, 0.0, 7.0};   /* anchor on motor */
+static const double JB[6] = {-47.0, -40.0, -33.0, 33.0, 40.0, 47.0}; /* anchor on frame */
+
+static void body_load(obody* b, const double* st, int base, double m, double I) {
+    b->px = st[base + 0]; b->py = st[base + 1]; b->a = st[base + 2];
+    b->vx = st[base + 3]; b->vy = st[base + 4]; b->w = st[base + 5];
+    b->c = cos(b->a); b->s = sin(b->a);
+    b->fx = b->fy = b->t = 0.0;
+    b->m_inv = 1.0 / m;
+    b->i_inv = 1.0 / I;
+}
+static void body_store(const obody* b, double* st, int base) {
+    st[base + 0] = b->px; st[base + 1] = b->py; st[base + 2] = b->a;
+    st[base + 3] = b->vx; st[base + 4] = b->vy; st[base + 5] = b->w;
+}
+/* cpBodyApplyForceAtLocalPoint(body, (0, F), (lx, 0)) */
+static void apply_force_local(obody* b, double F, double lx) {
+    double fwx = b->c * 0.0 + (-b->s) * F;
+    double fwy = b->s * 0.0 + b->c * F;
+    double tx = b->px - (0.0 * b->c - 0.0 * b->s);
+    double ty = b->py - (0.0 * b->s + 0.0 * b->c);
+    double wpx = b->c * lx + (-b->s) * 0.0 + tx;
+    double wpy = b->s * lx + b->c * 0.0 + ty;
+    double cgx = b->c * 0.0 + (-b->s) * 0.0 + tx;
+    double cgy = b->s * 0.0 + b->c * 0.0 + ty;
+    b->fx = b->fx + fwx;
+    b->fy = b->fy + fwy;
+    double rx = wpx - cgx, ry = wpy - cgy;
+    b->t += rx * fwy - ry * fwx;
+}
+/* frame OBB (+-50, +-5) vs circle: CircleToPoly contact iff dist <= r (cpCollision.c) */
+static int box_circle_touch(const obody* f, double cx, double cy, double r) {
+    double dx = cx - f->px, dy = cy - f->py;
+    double lx = dx * f->c + dy * f->s;
+    double ly = -dx * f->s + dy * f->c;
+    double qx = clip(lx, -FRAME_W / 2.0, FRAME_W / 2.0);
+    double qy = clip(ly, -FRAME_H / 2.0, FRAME_H / 2.0);
+    double ex = lx - qx, ey = ly - qy;
+    return ex * ex + ey * ey <= r * r;
+}
+
+typedef struct { double r1x, r1y, r2x, r2y, ka, kb, kc, kd, bx, by; } ojoint;
+
+static void apply_imp(obody* b, double jx, double jy, double rx, double ry) {
+    b->vx = b->vx + jx * b->m_inv;
+    b->vy = b->vy + jy * b->m_inv;
+    b->w += b->i_inv * (rx * jy - ry * jx);
+}
+
+/* cpSpaceStep(dt) on (frame, left, right) + 6 pivots; st is the D2D_S_* state vector */
+static int o_space_step(const d2d_cfg* cfg, const d2d_scn* scn, double* st, double fL, double fR,
+                        int collided) {
+    const double dt = 1.0 / 60.0;
+    const double I_F = moment_box(M_F, FRAME_W, FRAME_H), I_M = moment_box(M_M, MOTOR_S, MOTOR_S);
+    obody B[3];
+    body_load(&B[0], st, D2D_S_F, M_F, I_F);
+    body_load(&B[1], st, D2D_S_L, M_M, I_M);
+    body_load(&B[2], st, D2D_S_R, M_M, I_M);
+    /* drone_2d_env.py:403-404: forces on the frame only, left then right */
+    apply_force_local(&B[0], fL, -DRONE_R);
+    apply_force_local(&B[0], fR, DRONE_R);
+    /* 1. cpBodyUpdatePosition (v_bias = 0) */
+    for (int i = 0; i < 3; ++i) {
+        B[i].px = B[i].px + (B[i].vx + 0.0) * dt;
+        B[i].py = B[i].py + (B[i].vy + 0.0) * dt;
+        B[i].a = B[i].a + (B[i].w + 0.0) * dt;
+        B[i].c = cos(B[i].a);
+        B[i].s = sin(B[i].a);
+    }
+    /* 2. collide: frame (type 1) vs circles (type 2) -> begin -> space.collison = True */
+    for (int k = 0; k < scn->n_circles; ++k)
+        if (box_circle_touch(&B[0], scn->cx[k], scn->cy[k], scn->cr[k])) collided = 1;
+    /* 3. PivotJoint preStep */
+    ojoint J[6];
+    for (int k = 0; k < 6; ++k) {
+        obody* a = &B[k < 3 ? 1 : 2];
+        obody* b = &B[0];
+        ojoint* j = &J[k];
+        j->r1x = a->c * JA[k] + (-a->s) * 0.0;
+        j->r1y = a->s * JA[k] + a->c * 0.0;
+        j->r2x = b->c * JB[k] + (-b->s) * 0.0;
+        j->r2y = b->s * JB[k] + b->c * 0.0;
+        double m_sum = a->m_inv + b->m_inv;
+        double k11 = m_sum, k12 = 0.0, k21 = 0.0, k22 = m_sum;
+        double r1xsq = j->r1x * j->r1x * a->i_inv, r1ysq = j->r1y * j->r1y * a->i_inv;
+        double r1nxy = -j->r1x * j->r1y * a->i_inv;
+        k11 += r1ysq; k12 += r1nxy; k21 += r1nxy; k22 += r1xsq;
+        double r2xsq = j->r2x * j->r2x * b->i_inv, r2ysq = j->r2y * j->r2y * b->i_inv;
+        double r2nxy = -j->r2x * j->r2y * b->i_inv;
+        k11 += r2ysq; k12 += r2nxy; k21 += r2nxy; k22 += r2xsq;
+        double det = k11 * k22 - k12 * k21;
+        double det_inv = 1.0 / det;
+        j->ka = k22 * det_inv; j->kb = -k12 * det_inv; j->kc = -k21 * det_inv; j->kd = k11 * det_inv;
+        double dx = (b->px + j->r2x) - (a->px + j->r1x);
+        double dy = (b->py + j->r2y) - (a->py + j->r1y);
+        double coef = -(1.0 - pow(0.0, dt)) / dt; /* error_bias = 0 (Drone.py:64 ...) */
+        j->bx = dx * coef;
+        j->by = dy * coef;
+    }
+    /* 4. cpBodyUpdateVelocity: gravity (0,-1000) (drone_2d_env.py:185), damping^dt */
+    const double damping = pow(cfg->damping, dt);
+    for (int i = 0; i < 3; ++i) {
+        obody* b = &B[i];
+        b->vx = b->vx * damping + (0.0 + b->fx * b->m_inv) * dt;
+        b->vy = b->vy * damping + (-1000.0 + b->fy * b->m_inv) * dt;
+        b->w = b->w * damping + b->t * b->i_inv * dt;
+        b->fx = b->fy = b->t = 0.0;
+    }
+    /* 5. applyCachedImpulse with dt_coef = dt/prev_dt = 1 (0 after reset, where jAcc = 0 anyway) */
+    for (int k = 0; k < 6; ++k) {
+        obody* a = &B[k < 3 ? 1 : 2];
+        double jx = st[D2D_S_J + 2 * k] * 1.0, jy = st[D2D_S_J + 2 * k + 1] * 1.0;
+        apply_imp(a, -jx, -jy, J[k].r1x, J[k].r1y);
+        apply_imp(&B[0], jx, jy, J[k].r2x, J[k].r2y);
+    }
+    /* 6. 10 sequential-impulse iterations (Space.iterations default) */
+    for (int it = 0; it < 10; ++it) {
+        for (int k = 0; k < 6; ++k) {
+            obody* a = &B[k < 3 ? 1 : 2];
+            obody* b = &B[0];
+            ojoint* j = &J[k];
+            double v1x = a->vx + (-j->r1y) * a->w, v1y = a->vy + j->r1x * a->w;
+            double v2x = b->vx + (-j->r2y) * b->w, v2y = b->vy + j->r2x * b->w;
+            double ux = j->bx - (v2x - v1x), uy = j->by - (v2y - v1y);
+            double jx = ux * j->ka + uy * j->kb;
+            double jy = ux * j->kc + uy * j->kd;
+            double ox = st[D2D_S_J + 2 * k], oy = st[D2D_S_J + 2 * k + 1];
+            double nx = ox + jx, ny = oy + jy;
+            st[D2D_S_J + 2 * k] = nx;
+            st[D2D_S_J + 2 * k + 1] = ny;
+            jx = nx - ox;
+            jy = ny - oy;
+            apply_imp(a, -jx, -jy, j->r1x, j->r1y);
+            apply_imp(b, jx, jy, j->r2x, j->r2y);
+        }
+    }
+    body_store(&B[0], st, D2D_S_F);
+    body_store(&B[1], st, D2D_S_L);
+    body_store(&B[2], st, D2D_S_R);
+    return collided;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* get_observation (drone_2d_env.py:631-773)                                                   */
+/* ------------------------------------------------------------------------------------------ */
+static void o_observe(const d2d_cfg* cfg, const d2d_scn* s, const double* st, uint32_t* flags,
+                      double obs[D2D_OBS_DIM]) {
+    const double W = cfg->screen_w, H = cfg->screen_h;
+    const double vx = st[D2D_S_F + 3], vy = st[D2D_S_F + 4], w = st[D2D_S_F + 5];
+    const double x = st[D2D_S_F + 0], y = st[D2D_S_F + 1], al = st[D2D_S_F + 2];
+    obs[0] = m1to1(vx, -1330.0, 1330.0);
+    obs[1] = m1to1(vy, -1330.0, 1330.0);
+    obs[2] = clip(w / 11.7, -1.0, 1.0);
+    obs[3] = al / PI;
+    obs[4] = m1to1(s->wp_last_x - x, 0.0, W);
+    obs[5] = m1to1(s->wp_last_y - y, 0.0, H);
+    obs[6] = m1to1(x, 0.0, W);
+    obs[7] = m1to1(y, 0.0, H);
+    for (int j = 0; j < 3; ++j) { obs[8 + 3 * j] = 1.0; obs[9 + 3 * j] = 0.0; obs[10 + 3 * j] = 0.0; }
+    if (s->n_circles > 0) {
+        /* get_obstacle_distances: min over the UNROTATED frame vertices (+-50, +-5) */
+        const double vxs[4] = {50.0, 50.0, -50.0, -50.0}, vys[4] = {-5.0, 5.0, 5.0, -5.0};
+        double best_d[3] = {INFINITY, INFINITY, INFINITY};
+        int best_i[3] = {-1, -1, -1};
+        int kk = s->n_circles < D2D_K_OBS ? s->n_circles : D2D_K_OBS;
+        for (int i = 0; i < s->n_circles; ++i) {
+            double dmin = INFINITY;
+            for (int v = 0; v < 4; ++v) {
+                double ex = (vxs[v] + x) - s->cx[i], ey = (vys[v] + y) - s->cy[i];
+                double d = sqrt(ex * ex + ey * ey) - s->cr[i];
+                if (d < dmin) dmin = d;
+            }
+            /* stable sort ascending, keep first k: insert after equal keys */
+            for (int q = 0; q < kk; ++q) {
+                if (best_i[q] < 0 || dmin < best_d[q]) {
+                    for (int z = kk - 1; z > q; --z) { best_d[z] = best_d[z - 1]; best_i[z] = best_i[z - 1]; }
+                    best_d[q] = dmin;
+                    best_i[q] = i;
+                    break;
+                }
+            }
+        }
+        const double diag = sqrt(W * W + H * H);
+        for (int j = 0; j < kk; ++j) {
+            int i = best_i[j];
+            obs[8 + 3 * j] = m1to1(best_d[j], 0.0, diag);
+            double ang = atan2(y - s->cy[i], x - s->cx[i]);
+            ang = ssa(ang - al - PI);
+            obs[9 + 3 * j] = sin(ang);
+            obs[10 + 3 * j] = cos(ang);
+        }
+    }
+    /* velocity angle */
+    double vab = ssa(atan2(vy, vx) - al);
+    obs[17] = sin(vab);
+    obs[18] = cos(vab);
+    /* closest point + lookahead (get_closest_u evaluated once; the reference calls it twice with
+       identical input, predef_path.py:255 and :261) */
+    double u = d2dcpu_closest_u(s, x, y, NULL);
+    double cpx, cpy;
+    d2dcpu_path_eval(s, u, &cpx, &cpy);
+    obs[19] = m1to1(cpx, 0.0, W);
+    obs[20] = m1to1(cpy, 0.0, H);
+    const double L = s->us[s->n_wps - 1];
+    double ula = (u + cfg->lookahead > L) ? L : u + cfg->lookahead;
+    double lax, lay;
+    d2dcpu_path_eval(s, ula, &lax, &lay);
+    if (fabs(lax - s->wp_last_x) < 10.0 && fabs(lay - s->wp_last_y) < 10.0) *flags |= D2D_FLAG_LA_LOCK;
+    if (*flags & D2D_FLAG_LA_LOCK) { lax = s->wp_last_x; lay = s->wp_last_y; }
+    obs[21] = m1to1(lax, 0.0, W);
+    obs[22] = m1to1(lay, 0.0, H);
+    /* np.matmul(R_w_b(alpha), p - [x, y]): row = fma(R[r][0], d0, R[r][1]*d1) */
+    const double ca = cos(al), sa = sin(al);
+    double dx = lax - x, dy = lay - y;
+    double bx = fma(ca, dx, (-sa) * dy), by = fma(sa, dx, ca * dy);
+    double laa = ssa(atan2(by, bx) - al);
+    obs[23] = sin(laa);
+    obs[24] = cos(laa);
+    dx = cpx - x; dy = cpy - y;
+    bx = fma(ca, dx, (-sa) * dy); by = fma(sa, dx, ca * dy);
+    double cpa = ssa(atan2(by, bx) - al);
+    obs[25] = sin(cpa);
+    obs[26] = cos(cpa);
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* reward + termination (drone_2d_env.py:423-615)                                              */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct { double reward, ca, pa, pp, coll, reach, aa, dclose, dist_path; int cause; } orew;
+
+static orew o_reward(const d2d_cfg* cfg, const d2d_scn* s, const double* obs, int collided, int t) {
+    const double W = cfg->screen_w, H = cfg->screen_h;
+    orew R;
+    memset(&R, 0, sizeof R);
+    double vxd = invm1to1(obs[0], -1330.0, 1330.0);
+    double vyd = invm1to1(obs[1], -1330.0, 1330.0);
+    double alpha = obs[3] * PI;
+    double tdx = invm1to1(obs[4], 0.0, W), tdy = invm1to1(obs[5], 0.0, H);
+    double pxd = invm1to1(obs[6], 0.0, W), pyd = invm1to1(obs[7], 0.0, H);
+    double vel_ang = pymod(atan2(obs[17] * PI, obs[18] * PI) + TWO_PI, TWO_PI);
+    double cpx = invm1to1(obs[19], 0.0, W), cpy = invm1to1(obs[20], 0.0, H);
+    double la_ang = pymod(atan2(obs[23], obs[24]) + TWO_PI, TWO_PI);
+    double lpa = 1.0, lca = 1.0, ca = 0.0;
+    R.dclose = INFINITY;
+    if (s->n_circles > 0) {
+        const double diag = sqrt(W * W + H * H);
+        double d = invm1to1(obs[8], 0.0, diag);
+        R.dclose = d;
+        double oa = pymod(atan2(obs[9], obs[10]) + TWO_PI, TWO_PI);
+        double adiff = fabs((pymod(oa - vel_ang + PI, TWO_PI) - PI) * (180.0 / PI));
+        const double Rr = cfg->danger_range, A = cfg->danger_angle, k = cfg->abs_inv_ca_min_rew;
+        if (d < Rr && cfg->use_lambda) {
+            lpa = (d / Rr) / 2.0;
+            if (lpa < 0.10) lpa = 0.10;
+            lca = 1.0 - lpa;
+        }
+        if (d < Rr) {
+            double rr = -(((Rr + k * Rr) / (d + k * Rr)) - 1.0);
+            double ar = -(((A + k * A) / (adiff + k * A)) - 1.0);
+            if (ar > 0.0) ar = 0.0;
+            if (rr > 0.0) rr = 0.0;
+            ca = rr + ar;
+        }
+    }
+    double dist = norm2(cpx - pxd, cpy - pyd);
+    R.dist_path = dist;
+    double pa = -(2.0 * (clip(dist, 0.0, cfg->pa_band_edge) / cfg->pa_band_edge) - 1.0) * cfg->pa_scale;
+    double vel = sqrt(vxd * vxd + vyd * vyd);
+    double sv = vel * cfg->pp_vel_scale;
+    double vla = fabs(pymod(la_ang - vel_ang + PI, TWO_PI) - PI);
+    double pp = clip(cos(vla) * sv, cfg->pp_rew_min, cfg->pp_rew_max);
+    double coll = 0.0;
+    int cause = 0;
+    if (collided) { coll = cfg->rew_collision; cause |= D2D_END_COLLISION; }
+    double reach = 0.0;
+    if (fabs(tdx) < cfg->reach_end_radius && fabs(tdy) < cfg->reach_end_radius) {
+        cause |= D2D_END_REACH;
+        reach = cfg->rew_reach_end;
+    }
+    double aa = 0.0;
+    if (alpha > cfg->aa_band) aa = -sin(alpha);
+    if (alpha < -cfg->aa_band) aa = sin(alpha);
+    if (fabs(alpha) >= cfg->aa_angle) { aa = cfg->rew_aa; cause |= D2D_END_AA; }
+    if (t == cfg->n_steps) cause |= D2D_END_TIMEUP;
+    R.reward = aa + pa * lpa + pp + coll + ca * lca + reach;
+    R.ca = ca * lca;
+    R.pa = pa * lpa;
+    R.pp = pp;
+    R.coll = coll;
+    R.reach = reach;
+    R.aa = aa;
+    R.cause = cause;
+    return R;
+}
+
+/* ------------------------------------------------------------------------------------------ */
+/* batched handle (same call shapes as libdrone2d_hip.so, host pointers)                       */
+/* ------------------------------------------------------------------------------------------ */
+struct d2dcpu {
+    d2d_cfg cfg;
+    int n;
+    d2d_scn* scn;
+    int n_scn;
+    int32_t* env_scn;
+    double* st;    /* [NSTATE][n] */
+    int32_t* ist;  /* [NISTATE][n] */
+    double* acc;   /* [NSTATS][n] */
+    uint64_t seed;
+};
+
+d2dcpu_t* d2dcpu_create(const d2d_cfg* cfg, int32_t n) {
+    d2dcpu_t* h = (d2dcpu_t*)calloc(1, sizeof(*h));
+    h->cfg = *cfg;
+    h->n = n;
+    h->st = (double*)calloc((size_t)D2D_NSTATE * n, sizeof(double));
+    h->ist = (int32_t*)calloc((size_t)D2D_NISTATE * n, sizeof(int32_t));
+    h->acc = (double*)calloc((size_t)D2D_NSTATS * n, sizeof(double));
+    h->env_scn = (int32_t*)calloc((size_t)n, sizeof(int32_t));
+    return h;
+}
+void d2dcpu_destroy(d2dcpu_t* h) {
+    if (!h) return;
+    free(h->st); free(h->ist); free(h->acc); free(h->env_scn); free(h->scn); free(h);
+}
+int32_t d2dcpu_set_scenarios(d2dcpu_t* h, const d2d_scn* s, int32_t n_scn, const int32_t* env_scn) {
+    free(h->scn);
+    h->scn = (d2d_scn*)malloc(sizeof(d2d_scn) * (size_t)n_scn);
+    memcpy(h->scn, s, sizeof(d2d_scn) * (size_t)n_scn);
+    h->n_scn = n_scn;
+    for (int i = 0; i < h->n; ++i) h->env_scn[i] = env_scn ? env_scn[i] : 0;
+    return 0;
+}
+
+static void gather(const d2dcpu_t* h, int i, double* st, uint32_t* fl, int* t) {
+    for (int f = 0; f < D2D_NSTATE; ++f) st[f] = h->st[(size_t)f * h->n + i];
+    *t = h->ist[(size_t)D2D_I_T * h->n + i];
+    *fl = (uint32_t)h->ist[(size_t)D2D_I_FLAGS * h->n + i];
+}
+static void scatter(d2dcpu_t* h, int i, const double* st, uint32_t fl, int t) {
+    for (int f = 0; f < D2D_NSTATE; ++f) h->st[(size_t)f * h->n + i] = st[f];
+    h->ist[(size_t)D2D_I_T * h->n + i] = t;
+    h->ist[(size_t)D2D_I_FLAGS * h->n + i] = (int32_t)fl;
+}
+static void write_obs(float* dst, const double* obs) {
+    for (int k = 0; k < D2D_OBS_DIM; ++k) dst[k] = (float)obs[k];
+}
+
+/* test-mode reset of env i (drone_2d_env.py:218-311 + Drone.py:20-52 + reset :908-912) */
+static void o_reset_env(d2dcpu_t* h, int i, float* obs_out) {
+    const d2d_scn* s = &h->scn[h->env_scn[i]];
+    uint32_t ep = (uint32_t)h->ist[(size_t)D2D_I_EPISODE * h->n + i];
+    double u[3];
+    d2dcpu_spawn_uniforms(h->seed, (uint32_t)h->cfg.env_id_base + (uint32_t)i, ep, u);
+    double x = s->spawn_xmin + (s->spawn_xmax - s->spawn_xmin) * u[0];
+    double y = s->spawn_ymin + (s->spawn_ymax - s->spawn_ymin) * u[1];
+    double th = s->spawn_amin + (s->spawn_amax - s->spawn_amin) * u[2];
+    double st[D2D_NSTATE];
+    memset(st, 0, sizeof st);
+    st[D2D_S_F + 0] = x; st[D2D_S_F + 1] = y; st[D2D_S_F + 2] = th;
+    st[D2D_S_L + 0] = cos(th + PI) * DRONE_R + x; st[D2D_S_L + 1] = sin(th + PI) * DRONE_R + y;
+    st[D2D_S_L + 2] = th;
+    st[D2D_S_R + 0] = cos(th) * DRONE_R + x; st[D2D_S_R + 1] = sin(th) * DRONE_R + y;
+    st[D2D_S_R + 2] = th;
+    uint32_t fl = 0;
+    double obs[D2D_OBS_DIM];
+    o_observe(&h->cfg, s, st, &fl, obs);
+    scatter(h, i, st, fl, 0);
+    h->ist[(size_t)D2D_I_EPISODE * h->n + i] = (int32_t)(ep + 1u);
+    if (obs_out) write_obs(obs_out + (size_t)i * D2D_OBS_DIM, obs);
+}
+
+int32_t d2dcpu_reset(d2dcpu_t* h, const uint8_t* mask, uint64_t seed, float* obs) {
+    h->seed = seed;
+    for (int i = 0; i < h->n; ++i)
+        if (!mask || mask[i]) o_reset_env(h, i, obs);
+    return 0;
+}
+
+static void o_step_env(d2dcpu_t* h, int i, const float* act, float* obs_o, float* rew_o,
+                       uint8_t* term_o, uint8_t* trunc_o, float* info_o, float* tobs_o) {
+    const d2d_cfg* cfg = &h->cfg;
+    const d2d_scn* s = &h->scn[h->env_scn[i]];
+    double st[D2D_NSTATE];
+    uint32_t fl;
+    int t;
+    gather(h, i, st, &fl, &t);
+    /* drone_2d_env.py:400-401 with SB3's float32 action: float32 arithmetic */
+    const float fs = (float)cfg->force_scale;
+    float a0 = act[2 * (size_t)i], a1 = act[2 * (size_t)i + 1];
+    volatile float lf = (a0 / 2.0f + 0.5f);
+    volatile float rf = (a1 / 2.0f + 0.5f);
+    float fL = lf * fs, fR = rf * fs;
+    int coll = o_space_step(cfg, s, st, (double)fL, (double)fR, (fl & D2D_FLAG_COLLIDED) != 0);
+    if (coll) fl |= D2D_FLAG_COLLIDED;
+    t += 1;
+    double obs[D2D_OBS_DIM];
+    o_observe(cfg, s, st, &fl, obs);
+    orew R = o_reward(cfg, s, obs, coll, t);
+    st[D2D_S_PATH_ERR] += R.dist_path;
+    double ape = st[D2D_S_PATH_ERR] / (double)t;
+    st[D2D_S_TOT_REW] += R.reward;
+    int done = R.cause != 0;
+    if (rew_o) rew_o[i] = (float)R.reward;
+    int trunc = 0, term = done;
+    if (cfg->timeup_truncates && done && R.cause == D2D_END_TIMEUP) { trunc = 1; term = 0; }
+    if (term_o) term_o[i] = (uint8_t)term;
+    if (trunc_o) trunc_o[i] = (uint8_t)trunc;
+    if (info_o) {
+        float* r = info_o + (size_t)i * D2D_INFO_DIM;
+        r[D2D_INFO_CA] = (float)R.ca; r[D2D_INFO_PA] = (float)R.pa; r[D2D_INFO_PP] = (float)R.pp;
+        r[D2D_INFO_COLL] = (float)R.coll; r[D2D_INFO_REACH] = (float)R.reach; r[D2D_INFO_AA] = (float)R.aa;
+        r[D2D_INFO_DCLOSE] = (float)R.dclose; r[D2D_INFO_STEPS] = (float)t;
+        r[D2D_INFO_CAUSE] = (float)R.cause;
+        r[D2D_INFO_APE] = done ? (float)ape : 0.0f;
+        r[D2D_INFO_TOTREW] = done ? (float)st[D2D_S_TOT_REW] : 0.0f;
+        r[D2D_INFO_REWARD] = (float)R.reward;
+    }
+    scatter(h, i, st, fl, t);
+    if (done) {
+        int c1 = (R.cause & D2D_END_COLLISION) != 0, c2 = (R.cause & D2D_END_REACH) != 0;
+        int c4 = (R.cause & D2D_END_TIMEUP) != 0, c5 = (R.cause & D2D_END_AA) != 0;
+        double* acc = h->acc;
+        size_t n = (size_t)h->n;
+        acc[D2D_ST_RETURN * n + i] += st[D2D_S_TOT_REW];
+        acc[D2D_ST_EPISODES * n + i] += 1.0;
+        acc[D2D_ST_SUCCESS * n + i] += c2 ? 1.0 : 0.0;
+        acc[D2D_ST_FAIL * n + i] += (c1 || c4 || c5) ? 1.0 : 0.0;
+        acc[D2D_ST_COLLISION * n + i] += (c1 && !c2 && !c4 && !c5) ? 1.0 : 0.0;
+        acc[D2D_ST_APE * n + i] += ape;
+        acc[D2D_ST_LEN * n + i] += (double)t;
+        if (tobs_o) write_obs(tobs_o + (size_t)i * D2D_OBS_DIM, obs);
+        if (cfg->auto_reset) {
+            o_reset_env(h, i, obs_o);
+            return;
+        }
+    }
+    if (obs_o) write_obs(obs_o + (size_t)i * D2D_OBS_DIM, obs);
+}
+
+typedef struct {
+    d2dcpu_t* h; int lo, hi; const float* act; float *obs, *rew; uint8_t *term, *trunc; float *info, *tobs;
+} ojob;
+static void* o_worker(void* p) {
+    ojob* j = (ojob*)p;
+    for (int i = j->lo; i < j->hi; ++i)
+        o_step_env(j->h, i, j->act, j->obs, j->rew, j->term, j->trunc, j->info, j->tobs);
+    return NULL;
+}
+int32_t d2dcpu_step_mt(d2dcpu_t* h, const float* act, float* obs, float* rew, uint8_t* term,
+                       uint8_t* trunc, float* info, float* tobs, int32_t nthreads) {
+    if (nthreads <= 1) {
+        for (int i = 0; i < h->n; ++i) o_step_env(h, i, act, obs, rew, term, trunc, info, tobs);
+        return 0;
+    }
+    if (nthreads > 256) nthreads = 256;
+    pthread_t th[256];
+    ojob jobs[256];
+    for (int k = 0; k < nthreads; ++k) {
+        jobs[k] = (ojob){h, (int)((long)h->n * k / nthreads), (int)((long)h->n * (k + 1) / nthreads),
+                         act, obs, rew, term, trunc, info, tobs};
+        pthread_create(&th[k], NULL, o_worker, &jobs[k]);
+    }
+    for (int k = 0; k < nthreads; ++k) pthread_join(th[k], NULL);
+    return 0;
+}
+int32_t d2dcpu_step(d2dcpu_t* h, const float* act, float* obs, float* rew, uint8_t* term,
+                    uint8_t* trunc, float* info, float* tobs) {
+    return d2dcpu_step_mt(h, act, obs, rew, term, trunc, info, tobs, 1);
+}
+
+int32_t d2dcpu_get_state(const d2dcpu_t* h, double* st, int32_t* ist) {
+    if (st) memcpy(st, h->st, sizeof(double) * D2D_NSTATE * (size_t)h->n);
+    if (ist) memcpy(ist, h->ist, sizeof(int32_t) * D2D_NISTATE * (size_t)h->n);
+    return 0;
+}
+int32_t d2dcpu_set_state(d2dcpu_t* h, const double* st, const int32_t* ist) {
+    if (st) memcpy(h->st, st, sizeof(double) * D2D_NSTATE * (size_t)h->n);
+    if (ist) memcpy(h->ist, ist, sizeof(int32_t) * D2D_NISTATE * (size_t)h->n);
+    return 0;
+}
+int32_t d2dcpu_episode_stats(d2dcpu_t* h, double* out, int32_t clear) {
+    for (int k = 0; k < D2D_NSTATS; ++k) {
+        double s = 0.0;
+        for (int i = 0; i < h->n; ++i) s += h->acc[(size_t)k * h->n + i];
+        out[k] = s;
+    }
+    if (clear) memset(h->acc, 0, sizeof(double) * D2D_NSTATS * (size_t)h->n);
+    return 0;
+}
+
+/* single-state probes for tests */
+void d2dcpu_observe_state(const d2d_cfg* cfg, const d2d_scn* s, const double* st, int32_t* flags,
+                          double* obs) {
+    uint32_t f = (uint32_t)*flags;
+    o_observe(cfg, s, st, &f, obs);
+    *flags = (int32_t)f;
+}
+int32_t d2dcpu_physics_step(const d2d_cfg* cfg, const d2d_scn* s, double* st, double fL, double fR,
+                            int32_t collided) {
+    return o_space_step(cfg, s, st, fL, fR, collided);
+}
+double d2dcpu_moment_box(double m, double w, double h) { return moment_box(m, w, h); }

@@ -1,0 +1,175 @@
+"""ctypes wrapper of the CPU parity oracle ``oracle/libd2d_oracle.so``.
+
+TEST INFRASTRUCTURE ONLY (tests/, __graft_entry__.smoke(), bench.py cpu_baseline).  The oracle
+is a plain C restatement of the reference's hot path; see d2d_oracle.c for the per-function
+reference citations and the parity-pinning status.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "libd2d_oracle.so")
+
+
+def build(force: bool = False) -> str:
+    src = [os.path.join(HERE, f) for f in ("d2d_oracle.c", "d2d_oracle.h", "Makefile")]
+    src.append(os.path.join(HERE, "..", "include", "drone2d.h"))
+    if force or not os.path.exists(LIB) or any(os.path.getmtime(s) > os.path.getmtime(LIB) for s in src):
+        subprocess.run(["make", "-s", "-C", HERE, "-B" if force else "all"], check=True)
+    return LIB
+
+
+def _abi():
+    import drone2d_amd.abi as abi  # ctypes structs only; does not load the HIP library
+
+    return abi
+
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        abi = _abi()
+        lib = C.CDLL(LIB)
+        P, VP, I32, D = C.POINTER, C.c_void_p, C.c_int32, C.c_double
+        sigs = {
+            "d2dcpu_create": (VP, [P(abi.D2DCfg), I32]),
+            "d2dcpu_destroy": (None, [VP]),
+            "d2dcpu_set_scenarios": (I32, [VP, P(abi.D2DScn), I32, VP]),
+            "d2dcpu_reset": (I32, [VP, VP, C.c_uint64, VP]),
+            "d2dcpu_step": (I32, [VP, VP, VP, VP, VP, VP, VP, VP]),
+            "d2dcpu_step_mt": (I32, [VP, VP, VP, VP, VP, VP, VP, VP, I32]),
+            "d2dcpu_get_state": (I32, [VP, VP, VP]),
+            "d2dcpu_set_state": (I32, [VP, VP, VP]),
+            "d2dcpu_episode_stats": (I32, [VP, VP, I32]),
+            "d2dcpu_path_eval": (None, [P(abi.D2DScn), D, P(D), P(D)]),
+            "d2dcpu_closest_u": (D, [P(abi.D2DScn), D, D, P(C.c_int)]),
+            "d2dcpu_observe_state": (None, [P(abi.D2DCfg), P(abi.D2DScn), VP, P(I32), VP]),
+            "d2dcpu_physics_step": (I32, [P(abi.D2DCfg), P(abi.D2DScn), VP, D, D, I32]),
+            "d2dcpu_moment_box": (D, [D, D, D]),
+            "d2dcpu_spawn_uniforms": (None, [C.c_uint64, C.c_uint32, C.c_uint32, P(D)]),
+            "d2dcpu_philox": (None, [P(C.c_uint32), P(C.c_uint32), P(C.c_uint32)]),
+        }
+        for name, (res, args) in sigs.items():
+            f = getattr(lib, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def _p(a):
+    return None if a is None else C.c_void_p(a.ctypes.data)
+
+
+class OracleBatch:
+    """Host-side batch with the same call shapes as the HIP library (numpy buffers)."""
+
+    def __init__(self, cfg, scenarios_c, n_envs: int, env_scenario=None):
+        self.lib = load()
+        abi = _abi()
+        self.abi = abi
+        self.n = int(n_envs)
+        self.cfg = cfg
+        self.h = self.lib.d2dcpu_create(C.byref(cfg), self.n)
+        arr = (abi.D2DScn * len(scenarios_c))(*scenarios_c)
+        self._scn = arr
+        es = None
+        if env_scenario is not None:
+            es = np.ascontiguousarray(np.asarray(env_scenario, dtype=np.int32))
+        self.lib.d2dcpu_set_scenarios(self.h, arr, len(scenarios_c), _p(es))
+        n = self.n
+        self.obs = np.zeros((n, abi.OBS_DIM), np.float32)
+        self.rew = np.zeros(n, np.float32)
+        self.term = np.zeros(n, np.uint8)
+        self.trunc = np.zeros(n, np.uint8)
+        self.info = np.zeros((n, abi.INFO_DIM), np.float32)
+        self.tobs = np.zeros((n, abi.OBS_DIM), np.float32)
+
+    def close(self):
+        if self.h:
+            self.lib.d2dcpu_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
+
+    def reset(self, seed: int, mask=None):
+        m = None if mask is None else np.ascontiguousarray(np.asarray(mask, dtype=np.uint8))
+        self.lib.d2dcpu_reset(self.h, _p(m), C.c_uint64(seed & (2 ** 64 - 1)), _p(self.obs))
+        return self.obs.copy()
+
+    def step(self, actions, nthreads: int = 1):
+        a = np.ascontiguousarray(np.asarray(actions, dtype=np.float32).reshape(self.n, 2))
+        self.lib.d2dcpu_step_mt(self.h, _p(a), _p(self.obs), _p(self.rew), _p(self.term), _p(self.trunc),
+                                _p(self.info), _p(self.tobs), nthreads)
+        return self.obs.copy(), self.rew.copy(), self.term.astype(bool), self.trunc.astype(bool), self.info.copy()
+
+    def get_state(self):
+        st = np.zeros((self.abi.NSTATE, self.n), np.float64)
+        ist = np.zeros((self.abi.NISTATE, self.n), np.int32)
+        self.lib.d2dcpu_get_state(self.h, _p(st), _p(ist))
+        return st, ist
+
+    def set_state(self, st, ist):
+        st = np.ascontiguousarray(st, dtype=np.float64)
+        ist = np.ascontiguousarray(ist, dtype=np.int32)
+        self.lib.d2dcpu_set_state(self.h, _p(st), _p(ist))
+
+    def episode_stats(self, clear=True):
+        out = np.zeros(self.abi.NSTATS, np.float64)
+        self.lib.d2dcpu_episode_stats(self.h, _p(out), 1 if clear else 0)
+        return out
+
+
+# ------------------------------------------------------------------------------ single probes
+def path_eval(scn_c, u: float):
+    x, y = C.c_double(), C.c_double()
+    load().d2dcpu_path_eval(C.byref(scn_c), float(u), C.byref(x), C.byref(y))
+    return x.value, y.value
+
+
+def closest_u(scn_c, px: float, py: float):
+    nf = C.c_int()
+    u = load().d2dcpu_closest_u(C.byref(scn_c), float(px), float(py), C.byref(nf))
+    return u, nf.value
+
+
+def observe_state(cfg, scn_c, state, flags: int = 0):
+    st = np.ascontiguousarray(state, dtype=np.float64)
+    obs = np.zeros(27, np.float64)
+    f = C.c_int32(flags)
+    load().d2dcpu_observe_state(C.byref(cfg), C.byref(scn_c), _p(st), C.byref(f), _p(obs))
+    return obs, f.value
+
+
+def physics_step(cfg, scn_c, state, fL: float, fR: float, collided: int = 0):
+    st = np.array(state, dtype=np.float64)
+    hit = load().d2dcpu_physics_step(C.byref(cfg), C.byref(scn_c), _p(st), float(fL), float(fR), int(collided))
+    return st, int(hit)
+
+
+def philox(ctr, key):
+    c = (C.c_uint32 * 4)(*ctr)
+    k = (C.c_uint32 * 2)(*key)
+    o = (C.c_uint32 * 4)()
+    load().d2dcpu_philox(c, k, o)
+    return list(o)
+
+
+def spawn_uniforms(seed: int, env_id: int, episode: int):
+    u = (C.c_double * 3)()
+    load().d2dcpu_spawn_uniforms(C.c_uint64(seed), env_id, episode, u)
+    return list(u)

@@ -1,0 +1,57 @@
+"""HIP-vs-oracle comparison helpers shared by tests/test_gpu_*.py and __graft_entry__.smoke().
+
+Test infrastructure: the oracle is the checker, never the thing measured."""
+from __future__ import annotations
+
+import numpy as np
+
+OBS_ATOL = 2e-5      # float32 outputs; HIP ocml vs glibc transcendental ulps
+REW_ATOL = 1e-4
+REW_RTOL = 1e-5
+STATE_RTOL = 1e-9
+
+
+def make_pair(d2, n_envs, scenarios, seed, kwargs, env_scenario=None, auto_reset=True):
+    import oracle
+    from drone2d_amd.config import make_cfg
+
+    venv = d2.Drone2dVecEnv(n_envs, seed=seed, scenario=scenarios, env_scenario=env_scenario,
+                            auto_reset=auto_reset, **kwargs)
+    cfg = make_cfg(dict(kwargs), auto_reset=auto_reset)
+    orc = oracle.OracleBatch(cfg, [s.to_c() for s in venv.scenarios], n_envs, env_scenario=venv.env_scenario)
+    obs_g = venv.reset().cpu().numpy()
+    obs_o = orc.reset(seed)
+    np.testing.assert_allclose(obs_g, obs_o, atol=OBS_ATOL)
+    sync_oracle(venv, orc)
+    return venv, orc
+
+
+def sync_oracle(venv, orc):
+    st, ist = venv.get_state()
+    orc.set_state(st.cpu().numpy(), ist.cpu().numpy())
+
+
+def compare_step(venv, orc, act, teacher_force=True, check_state=True):
+    """Step both with the same actions; assert parity; return max |obs diff|."""
+    import torch
+
+    if teacher_force:
+        sync_oracle(venv, orc)
+    obs, rew, term, trunc, info = venv.step(torch.as_tensor(act, device=venv.device))
+    tobs = venv.terminal_obs
+    obs, rew, term, trunc, info = (x.cpu().numpy() for x in (obs, rew, term, trunc, info))
+    tobs = tobs.cpu().numpy()
+    o_obs, o_rew, o_term, o_trunc, o_info = orc.step(act)
+    np.testing.assert_array_equal(term, o_term)
+    np.testing.assert_array_equal(trunc, o_trunc)
+    np.testing.assert_allclose(rew, o_rew, rtol=REW_RTOL, atol=REW_ATOL)
+    np.testing.assert_allclose(obs, o_obs, rtol=0, atol=OBS_ATOL)
+    np.testing.assert_allclose(info, o_info, rtol=REW_RTOL, atol=REW_ATOL)
+    if term.any():
+        np.testing.assert_allclose(tobs[term], orc.tobs[term], atol=OBS_ATOL)
+    if check_state:
+        st, ist = venv.get_state()
+        o_st, o_ist = orc.get_state()
+        np.testing.assert_array_equal(ist.cpu().numpy(), o_ist)
+        np.testing.assert_allclose(st.cpu().numpy(), o_st, rtol=STATE_RTOL, atol=1e-9)
+    return float(np.max(np.abs(obs - o_obs)))

@@ -1,0 +1,109 @@
+"""C-ABI checks that need no GPU: struct layout of include/drone2d.h vs the ctypes mirror, the
+HIP library loads and exports every entry point the header declares, Philox KAT."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import REPO
+
+HEADER = os.path.join(REPO, "include", "drone2d.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(d2d_[a-z_]+)\s*\(", src)))
+
+
+def test_header_declares_expected_api():
+    fns = header_functions()
+    for f in ("d2d_create", "d2d_destroy", "d2d_set_scenarios", "d2d_reset", "d2d_step", "d2d_get_state",
+              "d2d_set_state", "d2d_episode_stats", "d2d_last_error", "d2d_abi_version", "d2d_n_envs"):
+        assert f in fns
+
+
+def test_struct_layout_matches_ctypes(tmp_path, d2):
+    from drone2d_amd import abi
+
+    prog = ["#include <stdio.h>", "#include <stddef.h>", f'#include "{HEADER}"', "int main(void){"]
+    for cname, cls in (("d2d_cfg", abi.D2DCfg), ("d2d_scn", abi.D2DScn)):
+        prog.append(f'printf("{cname} %zu\\n", sizeof({cname}));')
+        for fname, _ in cls._fields_:
+            prog.append(f'printf("{cname}.{fname} %zu\\n", offsetof({cname}, {fname}));')
+    for k in ("D2D_NSTATE", "D2D_NISTATE", "D2D_INFO_DIM", "D2D_NSTATS", "D2D_OBS_DIM", "D2D_MAX_WPS",
+              "D2D_MAX_CIRCLES", "D2D_ABI_VERSION"):
+        prog.append(f'printf("{k} %d\\n", (int){k});')
+    prog.append("return 0;}")
+    c = tmp_path / "probe.c"
+    c.write_text("\n".join(prog))
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-o", str(exe), str(c)], check=True)
+    out = dict(line.rsplit(" ", 1) for line in subprocess.run([str(exe)], capture_output=True, text=True,
+                                                                check=True).stdout.splitlines())
+    assert int(out["d2d_cfg"]) == C.sizeof(abi.D2DCfg)
+    assert int(out["d2d_scn"]) == C.sizeof(abi.D2DScn)
+    for cname, cls in (("d2d_cfg", abi.D2DCfg), ("d2d_scn", abi.D2DScn)):
+        for fname, _ in cls._fields_:
+            assert int(out[f"{cname}.{fname}"]) == getattr(cls, fname).offset, (cname, fname)
+    assert int(out["D2D_NSTATE"]) == abi.NSTATE and int(out["D2D_NISTATE"]) == abi.NISTATE
+    assert int(out["D2D_INFO_DIM"]) == abi.INFO_DIM and int(out["D2D_NSTATS"]) == abi.NSTATS
+    assert int(out["D2D_OBS_DIM"]) == abi.OBS_DIM and int(out["D2D_MAX_WPS"]) == abi.MAX_WPS
+    assert int(out["D2D_MAX_CIRCLES"]) == abi.MAX_CIRCLES and int(out["D2D_ABI_VERSION"]) == abi.ABI_VERSION
+
+
+@pytest.fixture(scope="module")
+def hip_lib(d2):
+    from drone2d_amd import _build, _native
+
+    _build.build()
+    return _native.load()
+
+
+def test_hip_library_exports_every_header_symbol(hip_lib):
+    from drone2d_amd import _native
+
+    for f in header_functions():
+        assert hasattr(hip_lib, f), f
+        assert f in _native.SIGNATURES, f  # and the ctypes binding declares it
+    assert hip_lib.d2d_abi_version() == 1
+
+
+def test_hip_library_is_gfx950(d2):
+    from drone2d_amd import _build
+
+    data = open(_build.OUT, "rb").read()
+    assert b"hipv4-amdgcn-amd-amdhsa--gfx950" in data  # the embedded code-object bundle id
+
+
+def test_errors_without_device(hip_lib):
+    """Argument validation happens before any device call."""
+    from drone2d_amd import abi
+    from drone2d_amd.config import ENV_TRAIN_CONFIG, make_cfg
+
+    h = C.c_void_p()
+    cfg = make_cfg(dict(ENV_TRAIN_CONFIG))
+    assert hip_lib.d2d_create(C.byref(cfg), 0, 0, C.byref(h)) == abi.E_ARG
+    assert b"n_envs" in hip_lib.d2d_last_error()
+    assert hip_lib.d2d_step(None, None, None, None, None, None, None, None, None) == abi.E_ARG
+    assert hip_lib.d2d_reset(None, None, 0, None, None) == abi.E_ARG
+    assert hip_lib.d2d_n_envs(None) == -1
+
+
+def test_philox_known_answers(oracle_mod):
+    """Random123 Philox4x32-10 KAT vectors (the spawn RNG spec shared by kernel and oracle)."""
+    assert oracle_mod.philox([0, 0, 0, 0], [0, 0]) == [0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8]
+    m = 0xFFFFFFFF
+    assert oracle_mod.philox([m, m, m, m], [m, m]) == [0x408F276D, 0x41C83B0E, 0xA20BC7C6, 0x6D5451FD]
+    assert oracle_mod.philox([0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344], [0xA4093822, 0x299F31D0]) == \
+        [0xD16CFE09, 0x94FDCCEB, 0x5001E420, 0x24126EA1]
+
+
+def test_spawn_uniforms_range(oracle_mod):
+    import numpy as np
+
+    u = np.array([oracle_mod.spawn_uniforms(7, i, e) for i in range(200) for e in range(3)])
+    assert u.min() >= 0 and u.max() < 1
+    assert abs(u.mean() - 0.5) < 0.05

@@ -1,0 +1,218 @@
+"""HIP kernel parity (through the C ABI via the ctypes binding) -- needs an MI355X.
+
+1. teacher-forced one-step parity against the golden vectors recorded from the reference,
+2. HIP vs CPU oracle over natural trajectories with auto-reset (teacher-forced every step),
+3. free-running agreement over the first steps,
+4. full-size (65 536 envs) size-independent properties: determinism, shard invariance, finiteness,
+   mask-reset isolation, episode statistics = sum of per-episode info rows.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import SCENARIOS, load_golden
+from parity_util import OBS_ATOL, compare_step, make_pair
+
+pytestmark = pytest.mark.gpu
+
+
+def _cfgkw():
+    from drone2d_amd.config import ENV_TRAIN_CONFIG
+
+    return dict(ENV_TRAIN_CONFIG)
+
+
+@pytest.mark.parametrize("which", ["traj", "crafted"])
+def test_golden_teacher_forced(d2, which):
+    from drone2d_amd import abi
+
+    g = load_golden(which)
+    M = len(g["rew"])
+    venv = d2.Drone2dVecEnv(M, scenario=SCENARIOS, env_scenario=g["scn"], auto_reset=False, **_cfgkw())
+    venv.reset(seed=0)
+    st = torch.as_tensor(np.ascontiguousarray(g["pre"].T))
+    ist = torch.zeros(3, M, dtype=torch.int32)
+    ist[0] = torch.as_tensor(g["pre_i"][:, 0])
+    ist[1] = torch.as_tensor(g["pre_i"][:, 1] | (g["pre_i"][:, 2] << 1))
+    venv.set_state(st, ist)
+    obs, rew, term, trunc, info = venv.step(torch.as_tensor(g["act"]))
+    obs, rew, term, info = obs.cpu().numpy(), rew.cpu().numpy(), term.cpu().numpy(), info.cpu().numpy()
+    np.testing.assert_array_equal(term.astype(int), g["done"])
+    assert not trunc.any()
+    np.testing.assert_allclose(obs, g["obs"], rtol=0, atol=OBS_ATOL)
+    np.testing.assert_allclose(rew, g["rew"], rtol=1e-5, atol=1e-4)
+    st2, ist2 = venv.get_state()
+    np.testing.assert_allclose(st2.cpu().numpy().T, g["post"], rtol=1e-9, atol=1e-9)
+    np.testing.assert_array_equal(ist2[0].cpu().numpy(), g["post_i"][:, 0])
+    np.testing.assert_array_equal(ist2[1].cpu().numpy(), g["post_i"][:, 1] | (g["post_i"][:, 2] << 1))
+    gi = g["info"]
+    np.testing.assert_array_equal(info[:, abi.INFO_COLL], gi[:, 4])
+    np.testing.assert_array_equal(info[:, abi.INFO_REACH], gi[:, 5])
+    np.testing.assert_allclose(info[:, abi.INFO_PP], gi[:, 3], rtol=1e-5, atol=1e-4)
+    np.testing.assert_allclose(info[:, abi.INFO_CA], gi[:, 1], rtol=1e-5, atol=1e-4)
+    venv.close()
+
+
+@pytest.mark.parametrize("scn", ["corridor", "S_corridor", "large", "mixed"])
+def test_vs_oracle_teacher_forced(d2, scn):
+    scenarios = SCENARIOS if scn == "mixed" else [scn]
+    venv, orc = make_pair(d2, 2048, scenarios, seed=99, kwargs=_cfgkw())
+    rng = np.random.default_rng(1)
+    dones = 0
+    for t in range(150):
+        act = np.clip(rng.normal(0.0, 0.6, (venv.num_envs, 2)), -1, 1).astype(np.float32)
+        compare_step(venv, orc, act)
+        dones += int(orc.term.sum())
+    assert dones > 50  # auto-resets were exercised
+    venv.close()
+
+
+def test_free_running_agreement(d2):
+    """No teacher forcing: both batches evolve independently from the same reset."""
+    venv, orc = make_pair(d2, 1024, SCENARIOS, seed=5, kwargs=_cfgkw())
+    rng = np.random.default_rng(2)
+    for t in range(60):
+        act = rng.uniform(-1, 1, (venv.num_envs, 2)).astype(np.float32)
+        compare_step(venv, orc, act, teacher_force=False, check_state=False)
+    venv.close()
+
+
+def test_edge_actions(d2):
+    """Unclipped / extreme actions (the env does not clip, drone_2d_env.py:400-401)."""
+    venv, orc = make_pair(d2, 512, SCENARIOS, seed=3, kwargs=_cfgkw())
+    vals = np.array([-1, 1, 0, -3.5, 2.25, 1e-30, -0.0], np.float32)
+    rng = np.random.default_rng(3)
+    for t in range(20):
+        act = rng.choice(vals, (venv.num_envs, 2)).astype(np.float32)
+        compare_step(venv, orc, act)
+    venv.close()
+
+
+def test_timeup_and_truncation_option(d2):
+    from drone2d_amd.config import ENV_TRAIN_CONFIG
+
+    kw = dict(ENV_TRAIN_CONFIG, n_steps=5)
+    for trunc_mode in (False, True):
+        venv = d2.Drone2dVecEnv(64, scenario="large_free", timeup_truncates=trunc_mode, **kw)
+        venv.reset(seed=0)
+        hover = torch.zeros(64, 2, device=venv.device)
+        for t in range(5):
+            obs, rew, term, trunc, info = venv.step(hover)
+        # all hovering envs end at t == n_steps (end_cond_4)
+        if trunc_mode:
+            assert trunc.all() and not term.any()
+        else:
+            assert term.all() and not trunc.any()
+        assert torch.all(info[:, 7] == 5) and torch.all(info[:, 8] == 4)
+        venv.close()
+
+
+FULL = 65536
+
+
+def _rollout(d2, n, seed, steps, scn="corridor", offset=0, env_scenario=None):
+    venv = d2.Drone2dVecEnv(n, seed=seed, scenario=scn, env_id_offset=offset, env_scenario=env_scenario,
+                            **_cfgkw())
+    obs0 = venv.reset().clone()
+    g = torch.Generator(device="cpu").manual_seed(7)
+    acts = (torch.rand(steps, FULL, 2, generator=g) * 2 - 1)[:, offset:offset + n].contiguous()
+    outs = []
+    for t in range(steps):
+        obs, rew, term, trunc, info = venv.step(acts[t].to(venv.device))
+        outs.append((obs.clone(), rew.clone(), term.clone()))
+    st, ist = venv.get_state()
+    stats = venv.episode_stats().clone()
+    venv.close()
+    return obs0, outs, st, ist, stats
+
+
+def test_full_size_determinism_and_shard_invariance(d2):
+    a = _rollout(d2, FULL, 11, 30)
+    b = _rollout(d2, FULL, 11, 30)
+    for (oa, ra, ta), (ob, rb, tb) in zip(a[1], b[1]):
+        assert torch.equal(oa, ob) and torch.equal(ra, rb) and torch.equal(ta, tb)
+    assert torch.equal(a[2], b[2]) and torch.equal(a[4], b[4])
+    # two shards with global env ids reproduce the single batch bit for bit
+    h = FULL // 2
+    s0 = _rollout(d2, h, 11, 30, offset=0)
+    s1 = _rollout(d2, h, 11, 30, offset=h)
+    for t in range(30):
+        assert torch.equal(torch.cat([s0[1][t][0], s1[1][t][0]]), a[1][t][0])
+        assert torch.equal(torch.cat([s0[1][t][1], s1[1][t][1]]), a[1][t][1])
+    assert torch.equal(torch.cat([s0[2], s1[2]], 1), a[2])
+
+
+@pytest.mark.parametrize("scn", ["corridor", "large", "S_corridor"])
+def test_full_size_properties(d2, scn):
+    obs0, outs, st, ist, stats = _rollout(d2, FULL, 3, 60, scn=scn)
+    assert torch.isfinite(obs0).all()
+    n_done = 0
+    for obs, rew, term in outs:
+        assert torch.isfinite(obs).all() and torch.isfinite(rew).all()
+        # sin/cos slots are in [-1, 1]; distance slots are 2d/diag - 1 >= -1 - r/diag
+        sc = obs[:, [9, 10, 12, 13, 15, 16, 17, 18, 23, 24, 25, 26]]
+        assert (sc.abs() <= 1.0 + 1e-6).all()
+        n_done += int(term.sum())
+    assert torch.isfinite(st).all()
+    assert (ist[0] >= 0).all() and (ist[0] <= 1100).all()
+    assert stats[1].item() == n_done  # every finished episode is counted once
+    assert stats[2] + stats[3] >= stats[1]  # success or fail (both when reach + collide)
+
+
+def test_reset_mask_isolation(d2):
+    venv = d2.Drone2dVecEnv(4096, scenario=SCENARIOS, **_cfgkw())
+    venv.reset(seed=1)
+    for _ in range(5):
+        venv.step(torch.rand(4096, 2, device=venv.device) * 2 - 1)
+    st0, ist0 = venv.get_state()
+    mask = torch.zeros(4096, dtype=torch.bool, device=venv.device)
+    mask[::3] = True
+    venv.reset(mask=mask)
+    st1, ist1 = venv.get_state()
+    keep = ~mask
+    assert torch.equal(st0[:, keep], st1[:, keep]) and torch.equal(ist0[:, keep], ist1[:, keep])
+    assert (ist1[0, mask] == 0).all() and (ist1[2, mask] == ist0[2, mask] + 1).all()
+    venv.close()
+
+
+def test_episode_stats_match_info_rows(d2):
+    venv = d2.Drone2dVecEnv(8192, scenario=SCENARIOS, seed=4, **_cfgkw())
+    venv.reset()
+    ret = n = succ = ape = ln = 0.0
+    for t in range(200):
+        obs, rew, term, trunc, info = venv.step(torch.rand(8192, 2, device=venv.device) * 2 - 1)
+        d = term | trunc
+        if d.any():
+            i = info[d].double()
+            ret += i[:, 10].sum().item()
+            n += d.sum().item()
+            succ += ((i[:, 8].long() & 2) > 0).sum().item()
+            ape += i[:, 9].sum().item()
+            ln += i[:, 7].sum().item()
+    s = venv.episode_stats().cpu().numpy()
+    assert s[1] == n and s[2] == succ and s[6] == ln
+    np.testing.assert_allclose(s[0], ret, rtol=1e-5, atol=1e-2)
+    np.testing.assert_allclose(s[5], ape, rtol=1e-5)
+    assert venv.episode_stats()[1].item() == 0  # cleared
+    venv.close()
+
+
+def test_single_env_api(d2):
+    from drone2d_amd.config import ENV_TRAIN_CONFIG
+
+    env = d2.Drone2dEnv(**dict(ENV_TRAIN_CONFIG, scenario="corridor", render_path=True))
+    obs = env.reset()
+    assert obs.shape == (27,) and obs.dtype == np.float64
+    done, steps = False, 0
+    while not done and steps < 2000:
+        obs, r, done, info = env.step([1.0, -1.0])  # spin -> AA termination
+        steps += 1
+    assert done and isinstance(r, float)
+    for k in ("reward", "collision_avoidance_reward", "path_adherence", "path_progression", "collision_reward",
+              "reach_end_reward", "agressive_alpha_reward", "env_steps", "dist_closest_obs", "APE",
+              "n_collisions", "n_successful_runs", "n_failed_runs", "total_reward", "flight_path"):
+        assert k in info
+    assert info["n_failed_runs"] == 1 and len(info["flight_path"]) == steps
+    _, _, done2, _ = env.step([0.0, 0.0])
+    assert done2  # done is sticky until reset (drone_2d_env.py:594)
+    env.close()
