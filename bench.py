@@ -83,7 +83,7 @@ def cpu_baseline(args, kwargs):
     oracle.build()
     threads = min(len(os.sched_getaffinity(0)), 16)
     n = args.envs
-    scn = [s.to_c() for s in build_scenarios(kwargs, args.scenario)]
+    scn = [s.to_c() for s in build_scenarios(kwargs)]
     b = oracle.OracleBatch(make_cfg(dict(kwargs)), scn, n)
     b.reset(0)
     rng = np.random.default_rng(0)

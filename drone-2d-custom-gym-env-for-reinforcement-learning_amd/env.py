@@ -52,10 +52,10 @@ def _make_box(low, high):
     return Box(low, high)
 
 
-def build_scenarios(kwargs: dict, scenario=None) -> list[Scenario]:
+def build_scenarios(kwargs: dict) -> list[Scenario]:
     """Scenario list for ``mode='test'``: one name, a list of names, or Scenario objects."""
     W, H = kwargs["screensize_x"], kwargs["screensize_y"]
-    spec = kwargs["scenario"] if scenario is None else scenario
+    spec = kwargs["scenario"]
     if isinstance(spec, (str, Scenario)):
         spec = [spec]
     out = []
@@ -76,15 +76,16 @@ def build_scenarios(kwargs: dict, scenario=None) -> list[Scenario]:
 class Drone2dVecEnv:
     """``num_envs`` independent Drone2dEnv copies stepping together on one GPU.
 
-    Parameters mirror the reference kwargs; extra knobs:
-      scenario        override kwargs['scenario'] (name, list of names, or Scenario objects)
+    Parameters mirror the reference kwargs; ``kwargs['scenario']`` may also be a list of scenario
+    names / Scenario objects (mixed batches, BASELINE config 5) or '<name>_free' (no obstacles,
+    config 2).  Extra knobs:
       env_scenario    int array [num_envs] mapping env -> scenario index (default: i % n_scenarios)
       env_id_offset   global id of env 0 (multi-GPU shards keep per-env RNG streams global)
       auto_reset      SB3 VecEnv semantics (done envs are reset inside the step kernel)
       timeup_truncates  report time-up as truncation instead of termination (reference: False)
     """
 
-    def __init__(self, num_envs: int, device=None, seed: int = 0, *, scenario=None,
+    def __init__(self, num_envs: int, device=None, seed: int = 0, *,
                  env_scenario: Sequence[int] | None = None, auto_reset: bool = True,
                  timeup_truncates: bool = False, with_info: bool = True, env_id_offset: int = 0, **kwargs):
         self.kwargs = dict(kwargs)
@@ -99,7 +100,7 @@ class Drone2dVecEnv:
         self.num_envs = int(num_envs)
         self.cfg = make_cfg(self.kwargs, auto_reset=auto_reset, timeup_truncates=timeup_truncates,
                             env_id_base=env_id_offset)
-        self.scenarios = build_scenarios(self.kwargs, scenario)
+        self.scenarios = build_scenarios(self.kwargs)
         self.seed_value = int(seed)
         self.with_info = with_info
         self.action_space = _make_box(-np.ones(2), np.ones(2))

@@ -15,8 +15,8 @@ def make_pair(d2, n_envs, scenarios, seed, kwargs, env_scenario=None, auto_reset
     import oracle
     from drone2d_amd.config import make_cfg
 
-    venv = d2.Drone2dVecEnv(n_envs, seed=seed, scenario=scenarios, env_scenario=env_scenario,
-                            auto_reset=auto_reset, **kwargs)
+    kwargs = dict(kwargs, scenario=scenarios)
+    venv = d2.Drone2dVecEnv(n_envs, seed=seed, env_scenario=env_scenario, auto_reset=auto_reset, **kwargs)
     cfg = make_cfg(dict(kwargs), auto_reset=auto_reset)
     orc = oracle.OracleBatch(cfg, [s.to_c() for s in venv.scenarios], n_envs, env_scenario=venv.env_scenario)
     obs_g = venv.reset().cpu().numpy()

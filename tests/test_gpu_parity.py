@@ -16,10 +16,10 @@ from parity_util import OBS_ATOL, compare_step, make_pair
 pytestmark = pytest.mark.gpu
 
 
-def _cfgkw():
+def _cfgkw(scenario="corridor", **over):
     from drone2d_amd.config import ENV_TRAIN_CONFIG
 
-    return dict(ENV_TRAIN_CONFIG)
+    return dict(ENV_TRAIN_CONFIG, scenario=scenario, **over)
 
 
 @pytest.mark.parametrize("which", ["traj", "crafted"])
@@ -28,7 +28,7 @@ def test_golden_teacher_forced(d2, which):
 
     g = load_golden(which)
     M = len(g["rew"])
-    venv = d2.Drone2dVecEnv(M, scenario=SCENARIOS, env_scenario=g["scn"], auto_reset=False, **_cfgkw())
+    venv = d2.Drone2dVecEnv(M, env_scenario=g["scn"], auto_reset=False, **_cfgkw(SCENARIOS))
     venv.reset(seed=0)
     st = torch.as_tensor(np.ascontiguousarray(g["pre"].T))
     ist = torch.zeros(3, M, dtype=torch.int32)
@@ -91,9 +91,9 @@ def test_edge_actions(d2):
 def test_timeup_and_truncation_option(d2):
     from drone2d_amd.config import ENV_TRAIN_CONFIG
 
-    kw = dict(ENV_TRAIN_CONFIG, n_steps=5)
+    kw = dict(ENV_TRAIN_CONFIG, n_steps=5, scenario="large_free")
     for trunc_mode in (False, True):
-        venv = d2.Drone2dVecEnv(64, scenario="large_free", timeup_truncates=trunc_mode, **kw)
+        venv = d2.Drone2dVecEnv(64, timeup_truncates=trunc_mode, **kw)
         venv.reset(seed=0)
         hover = torch.zeros(64, 2, device=venv.device)
         for t in range(5):
@@ -111,8 +111,7 @@ FULL = 65536
 
 
 def _rollout(d2, n, seed, steps, scn="corridor", offset=0, env_scenario=None):
-    venv = d2.Drone2dVecEnv(n, seed=seed, scenario=scn, env_id_offset=offset, env_scenario=env_scenario,
-                            **_cfgkw())
+    venv = d2.Drone2dVecEnv(n, seed=seed, env_id_offset=offset, env_scenario=env_scenario, **_cfgkw(scn))
     obs0 = venv.reset().clone()
     g = torch.Generator(device="cpu").manual_seed(7)
     acts = (torch.rand(steps, FULL, 2, generator=g) * 2 - 1)[:, offset:offset + n].contiguous()
@@ -160,7 +159,7 @@ def test_full_size_properties(d2, scn):
 
 
 def test_reset_mask_isolation(d2):
-    venv = d2.Drone2dVecEnv(4096, scenario=SCENARIOS, **_cfgkw())
+    venv = d2.Drone2dVecEnv(4096, **_cfgkw(SCENARIOS))
     venv.reset(seed=1)
     for _ in range(5):
         venv.step(torch.rand(4096, 2, device=venv.device) * 2 - 1)
@@ -176,7 +175,7 @@ def test_reset_mask_isolation(d2):
 
 
 def test_episode_stats_match_info_rows(d2):
-    venv = d2.Drone2dVecEnv(8192, scenario=SCENARIOS, seed=4, **_cfgkw())
+    venv = d2.Drone2dVecEnv(8192, seed=4, **_cfgkw(SCENARIOS))
     venv.reset()
     ret = n = succ = ape = ln = 0.0
     for t in range(200):
