@@ -20,6 +20,13 @@
 
 #include "../../include/drone2d.h"
 
+// Diagnostic-only ablation mask (tools/ablate.py builds separate timing-only libraries with it;
+// the product is always built with 0): 1 skip Brent, 2 skip sensing, 4 skip joint iterations,
+// 8 skip collision test.
+#ifndef D2D_ABLATE
+#define D2D_ABLATE 0
+#endif
+
 namespace d2d {
 
 constexpr double PI = 3.141592653589793;      // np.pi
@@ -238,7 +245,7 @@ __device__ __forceinline__ bool space_step(const d2d_scn& s, double damping_dt, 
     }
     // ---- 2. collision: CircleToPoly(circle, frame box) contact iff dist(center, box) <= r
     bool hit = false;
-    for (int k = 0; k < s.n_circles; ++k) {
+    for (int k = 0; k < ((D2D_ABLATE & 8) ? 0 : s.n_circles); ++k) {
         const double dx = s.cx[k] - B[0].px, dy = s.cy[k] - B[0].py;
         const double lx = dx * cs[0] + dy * sn[0];
         const double ly = -dx * sn[0] + dy * cs[0];
@@ -297,7 +304,7 @@ __device__ __forceinline__ bool space_step(const d2d_scn& s, double damping_dt, 
         B[0].w += II_F * (r2x[k] * jy - r2y[k] * jx);
     }
     // ---- 6. 10 Gauss-Seidel iterations over the joints in space.add order
-    for (int it = 0; it < 10; ++it) {
+    for (int it = 0; it < ((D2D_ABLATE & 4) ? 0 : 10); ++it) {
 #pragma unroll
         for (int k = 0; k < 6; ++k) {
             const int m = k < 3 ? 1 : 2;
@@ -342,7 +349,7 @@ __device__ __forceinline__ void observe(const d2d_cfg& cfg, const d2d_scn& s, co
     double bd0 = 0.0, bd1 = 0.0, bd2 = 0.0;
     int bi0 = -1, bi1 = -1, bi2 = -1;
     const int nc = s.n_circles;
-    for (int i = 0; i < nc; ++i) {
+    for (int i = 0; i < ((D2D_ABLATE & 2) ? 0 : nc); ++i) {
         const double cx = s.cx[i], cy = s.cy[i];
         const double ax = (50.0 + x) - cx, bxx = (-50.0 + x) - cx;
         const double ay = (-5.0 + y) - cy, byy = (5.0 + y) - cy;
@@ -386,7 +393,7 @@ __device__ __forceinline__ void observe(const d2d_cfg& cfg, const d2d_scn& s, co
     obs[18] = cos(vab);
     // closest point and lookahead: get_closest_u is evaluated once (the reference calls it twice
     // with identical input, predef_path.py:255 and :261)
-    const double u = closest_u(s, x, y);
+    const double u = (D2D_ABLATE & 1) ? clipd(x - 100.0, -10.0, s.us[s.n_wps - 1]) : closest_u(s, x, y);
     double cpx, cpy;
     path_eval(s, u, cpx, cpy);
     obs[19] = m1to1(cpx, 0.0, W);

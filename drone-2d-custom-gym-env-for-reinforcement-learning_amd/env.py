@@ -87,9 +87,10 @@ class Drone2dVecEnv:
 
     def __init__(self, num_envs: int, device=None, seed: int = 0, *,
                  env_scenario: Sequence[int] | None = None, auto_reset: bool = True,
-                 timeup_truncates: bool = False, with_info: bool = True, env_id_offset: int = 0, **kwargs):
+                 timeup_truncates: bool = False, with_info: bool = True, env_id_offset: int = 0,
+                 native_lib: str | None = None, **kwargs):
         self.kwargs = dict(kwargs)
-        self._lib = load()
+        self._lib = load(native_lib)  # native_lib: alternative build (diagnostics only)
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device())
         self.device = torch.device(device)
