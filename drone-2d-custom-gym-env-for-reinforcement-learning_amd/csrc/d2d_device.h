@@ -1,10 +1,15 @@
-// d2d_device.h -- per-env device functions of the batched Drone2dEnv step (gfx950, fp64).
+// d2d_device.h -- device functions of the batched Drone2dEnv step (gfx950, fp64).
 //
-// One lane = one env.  Everything here is straight-line fp64 on VGPRs; the scenario (path
-// coefficients, knots, circles) is read from an LDS-staged copy shared by the workgroup.
-// Evaluation order follows the reference's NumPy order term by term (see oracle/d2d_oracle.c for
-// the plain restatement and tests/golden for the pinned vectors), compiled with
-// -ffp-contract=off; the only fused ops are where NumPy/OpenBLAS itself fuses (norm, matmul).
+// Evaluation order follows the reference's NumPy order term by term (oracle/d2d_oracle.c is the
+// plain restatement, tests/golden the pinned vectors); compiled with -ffp-contract=off, the only
+// fused ops are where NumPy/OpenBLAS itself fuses (np.linalg.norm, 2x2 np.matmul).
+//
+// The step is split into two "roles" that the cooperative kernel runs on different waves:
+//   path role    Brent closest point -> closest/lookahead point, LA lock, LA/CP angles (obs 19..26)
+//   sensor role  kinematics, 3-nearest circles, velocity angle (obs 0..18) + the reward's CA part
+// Their latency chains are independent, so running them on different waves of one workgroup turns
+// sum(latency) into max(latency).  All branches inside a role are written as selects so a wave's
+// lanes never serialise over divergent paths.
 //
 // Reference anchors (drone_2d_custom_gym_env/):
 //   thrust            drone_2d_env.py:400-404
@@ -35,19 +40,35 @@ constexpr double DT = 1.0 / 60.0;             // drone_2d_env.py:406
 constexpr double GRAV_Y = -1000.0;            // drone_2d_env.py:185
 constexpr double DRONE_R = 40.0;              // Drone.py:11 (100/2 - 20/2)
 constexpr double FRAME_HX = 50.0, FRAME_HY = 5.0;   // Drone.py:16 box (100, 10)
+constexpr double VEL_MAX = 1330.0;            // drone_2d_env.py:635
 
 // ------------------------------------------------------------------------------ scalar helpers
-// Python/NumPy float modulo (fmod, then move into the divisor's sign)
-__device__ __forceinline__ double pymod(double a, double b) {
-    double m = fmod(a, b);
-    if (m != 0.0) {
-        if ((b < 0.0) != (m < 0.0)) m += b;
+// fmod(a, 2*pi), bit-exact, without ocml's fmod loop (239 cycles dependent latency on gfx950 vs
+// ~50 here).  fmod's result a - q*b (q = trunc(a/b)) is exactly representable, so once q is the
+// true quotient fma(-q, b, a) is exact; the estimate from a * (1/b) is off by at most one, which the
+// sign / range test below detects and corrects.  |a| >= 2^40 (and NaN/inf) falls back to fmod.
+__device__ __forceinline__ double fmod_2pi(double a) {
+    constexpr double INV = 0.15915494309189535;  // 1/(2*pi), rounded
+    if (!(fabs(a) < 1099511627776.0)) return fmod(a, TWO_PI);
+    double q = trunc(a * INV);
+    double r = fma(-q, TWO_PI, a);
+    if (a >= 0.0) {
+        const double dq = (r < 0.0) ? -1.0 : ((r >= TWO_PI) ? 1.0 : 0.0);
+        if (dq != 0.0) r = fma(-(q + dq), TWO_PI, a);
     } else {
-        m = copysign(0.0, b);
+        const double dq = (r > 0.0) ? 1.0 : ((r <= -TWO_PI) ? -1.0 : 0.0);
+        if (dq != 0.0) r = fma(-(q + dq), TWO_PI, a);
     }
-    return m;
+    return r;
 }
-__device__ __forceinline__ double ssa(double a) { return pymod(a + PI, TWO_PI) - PI; }
+// Python/NumPy float modulo by 2*pi (npy_remainder: fmod, then move into the divisor's sign)
+__device__ __forceinline__ double pymod_2pi(double a) {
+    double m = fmod_2pi(a);
+    return (m != 0.0) ? ((m < 0.0) ? m + TWO_PI : m) : 0.0;
+}
+// transformations.py:6-7
+__device__ __forceinline__ double ssa(double a) { return pymod_2pi(a + PI) - PI; }
+// drone_2d_env.py:972-978
 __device__ __forceinline__ double m1to1(double v, double lo, double hi) { return 2.0 * (v - lo) / (hi - lo) - 1.0; }
 __device__ __forceinline__ double invm1to1(double v, double lo, double hi) { return (v + 1.0) * (hi - lo) / 2.0 + lo; }
 __device__ __forceinline__ double clipd(double x, double lo, double hi) { return x < lo ? lo : (x > hi ? hi : x); }
@@ -57,6 +78,7 @@ __device__ __forceinline__ double sgn_nz(double x) {
     double s = (x > 0.0) ? 1.0 : ((x < 0.0) ? -1.0 : (x == 0.0 ? 0.0 : x));
     return s + (x == 0.0 ? 1.0 : 0.0);
 }
+__device__ __forceinline__ void sincos_d(double x, double& s, double& c) { sincos(x, &s, &c); }
 
 // ------------------------------------------------------------------------------ Philox4x32-10
 __device__ __forceinline__ void philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
@@ -75,6 +97,19 @@ __device__ __forceinline__ void philox(uint32_t c0, uint32_t c1, uint32_t c2, ui
 __device__ __forceinline__ double u53(uint32_t a, uint32_t b) {
     return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * (1.0 / 9007199254740992.0);
 }
+// test-mode spawn draw (drone_2d_env.py:229-232): x, y, theta for (seed, global env id, episode)
+__device__ __forceinline__ void spawn_draw(const d2d_scn& s, uint64_t seed, uint32_t gid, uint32_t episode,
+                                           double& x, double& y, double& th) {
+    uint32_t o[4];
+    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    philox(gid, episode, 0u, 0u, k0, k1, o);
+    const double u0 = u53(o[0], o[1]), u1 = u53(o[2], o[3]);
+    philox(gid, episode, 1u, 0u, k0, k1, o);
+    const double u2 = u53(o[0], o[1]);
+    x = s.spawn_xmin + (s.spawn_xmax - s.spawn_xmin) * u0;
+    y = s.spawn_ymin + (s.spawn_ymax - s.spawn_ymin) * u1;
+    th = s.spawn_amin + (s.spawn_amax - s.spawn_amin) * u2;
+}
 
 // ------------------------------------------------------------------------------ QPMI2D path
 // get_u_index (predef_path.py:53-63): first n with u <= us[n+1]; for non-decreasing knots this is
@@ -85,39 +120,38 @@ __device__ __forceinline__ int u_index(const d2d_scn& s, double u) {
     for (int k = 1; k < D2D_MAX_WPS; ++k) n += (k < s.n_wps && !(u <= s.us[k])) ? 1 : 0;
     return n;
 }
-__device__ __forceinline__ void quad(const d2d_scn& s, int k, double u, double& x, double& y) {
-    const double uu = u * u;
-    x = s.xa[k] * uu + s.xb[k] * u + s.xc[k];
-    y = s.ya[k] * uu + s.yb[k] * u + s.yc[k];
-}
-// QPMI2D.__call__ (predef_path.py:88-142)
+// QPMI2D.__call__ (predef_path.py:88-142), branch-free: both candidate quadratics are evaluated
+// and the reference's case analysis picks the result with selects (same arithmetic per case).
 __device__ __forceinline__ void path_eval(const d2d_scn& s, double u, double& x, double& y) {
     const int nw = s.n_wps, nseg = nw - 2;
     const int n = u_index(s, u);
-    if (u >= s.us[0] && u <= s.us[1]) {
-        quad(s, 0, u, x, y);
-    } else if ((u >= s.us[nw - 2] - 0.001 && u <= s.us[nw - 1]) || n == nw - 1) {
-        quad(s, nseg - 1, u, x, y);
-    } else {
-        const double u0 = s.us[n], u1 = s.us[n + 1];
-        const double mu_r = (u - u0) / (u1 - u0);
-        const double mu_f = (u1 - u) / (u1 - u0);
-        const int k1 = (n == 0) ? nseg - 1 : n - 1;  // python x_params[n-1]
-        double x1, y1, x2, y2;
-        quad(s, k1, u, x1, y1);
-        quad(s, n, u, x2, y2);
-        x = mu_r * x2 + mu_f * x1;
-        y = mu_r * y2 + mu_f * y1;
-    }
+    const bool first = (u >= s.us[0] && u <= s.us[1]);
+    const bool last = !first && ((u >= s.us[nw - 2] - 0.001 && u <= s.us[nw - 1]) || n == nw - 1);
+    const bool blend = !first && !last;
+    const int kb = first ? 0 : (last ? nseg - 1 : n);
+    const int ka = (n == 0) ? nseg - 1 : n - 1;  // python x_params[n-1]
+    const int n1 = (n + 1 < D2D_MAX_WPS) ? n + 1 : D2D_MAX_WPS - 1;
+    const double u0 = s.us[n], u1 = s.us[n1];
+    const double uu = u * u;
+    const double xB = s.xa[kb] * uu + s.xb[kb] * u + s.xc[kb];
+    const double yB = s.ya[kb] * uu + s.yb[kb] * u + s.yc[kb];
+    const int kas = blend ? ka : kb;
+    const double xA = s.xa[kas] * uu + s.xb[kas] * u + s.xc[kas];
+    const double yA = s.ya[kas] * uu + s.yb[kas] * u + s.yc[kas];
+    const double mu_r = (u - u0) / (u1 - u0);
+    const double mu_f = (u1 - u) / (u1 - u0);
+    x = blend ? mu_r * xB + mu_f * xA : xB;
+    y = blend ? mu_r * yB + mu_f * yA : yB;
 }
 __device__ __forceinline__ double path_dist(const d2d_scn& s, double u, double px, double py) {
     double x, y;
     path_eval(s, u, x, y);
     return norm2(x - px, y - py);
 }
-// get_closest_u (predef_path.py:226-248) = scipy fminbound(x1=-10, x2=L+10, xtol=1e-6, maxfun=500)
-// restated from scipy 1.15.3 _minimize_scalar_bounded (_optimize.py:2251-2398), probe for probe.
-__device__ double closest_u(const d2d_scn& s, double px, double py) {
+// get_closest_u (predef_path.py:226-248) = scipy fminbound(x1=-10, x2=L+10, xtol=1e-6, maxfun=500),
+// restated from scipy 1.15.3 _minimize_scalar_bounded (_optimize.py:2251-2398) probe for probe; the
+// golden/parabolic case analysis is evaluated with selects (identical arithmetic per case).
+__device__ __forceinline__ double closest_u(const d2d_scn& s, double px, double py) {
     const double sqrt_eps = 1.4832396974191326e-08;   // sqrt(2.2e-16)
     const double golden_mean = 0.3819660112501051;    // 0.5*(3.0 - sqrt(5.0))
     const double xatol3 = 1e-6 / 3.0;
@@ -125,56 +159,47 @@ __device__ double closest_u(const d2d_scn& s, double px, double py) {
     double fulc = a + golden_mean * (b - a);
     double nfc = fulc, xf = fulc;
     double rat = 0.0, e = 0.0;
-    double x = xf;
-    double fx = path_dist(s, x, px, py);
+    double fx = path_dist(s, xf, px, py);
     int num = 1;
     double ffulc = fx, fnfc = fx;
     double xm = 0.5 * (a + b);
     double tol1 = sqrt_eps * fabs(xf) + xatol3;
     double tol2 = 2.0 * tol1;
     while (fabs(xf - xm) > (tol2 - 0.5 * (b - a))) {
-        bool golden = true;
-        if (fabs(e) > tol1) {
-            golden = false;
-            double r = (xf - nfc) * (fx - ffulc);
-            double q = (xf - fulc) * (fx - fnfc);
-            double p = (xf - fulc) * q - (xf - nfc) * r;
-            q = 2.0 * (q - r);
-            if (q > 0.0) p = -p;
-            q = fabs(q);
-            r = e;
-            e = rat;
-            if ((fabs(p) < fabs(0.5 * q * r)) && (p > q * (a - xf)) && (p < q * (b - xf))) {
-                rat = (p + 0.0) / q;
-                x = xf + rat;
-                if (((x - a) < tol2) || ((b - x) < tol2)) rat = tol1 * sgn_nz(xm - xf);
-            } else {
-                golden = true;
-            }
-        }
-        if (golden) {
-            e = (xf >= xm) ? a - xf : b - xf;
-            rat = golden_mean * e;
-        }
+        // parabolic candidate (used only when |e| > tol1 and it is acceptable)
+        const double r = (xf - nfc) * (fx - ffulc);
+        double q = (xf - fulc) * (fx - fnfc);
+        double p = (xf - fulc) * q - (xf - nfc) * r;
+        q = 2.0 * (q - r);
+        p = (q > 0.0) ? -p : p;
+        q = fabs(q);
+        const bool par = (fabs(e) > tol1) && (fabs(p) < fabs(0.5 * q * e)) && (p > q * (a - xf)) &&
+                         (p < q * (b - xf));
+        double rat_p = (p + 0.0) / q;
+        const double xp = xf + rat_p;
+        rat_p = (((xp - a) < tol2) || ((b - xp) < tol2)) ? tol1 * sgn_nz(xm - xf) : rat_p;
+        // golden-section candidate
+        const double e_g = (xf >= xm) ? a - xf : b - xf;
+        const double rat_g = golden_mean * e_g;
+        e = par ? rat : e_g;
+        rat = par ? rat_p : rat_g;
         const double ar = fabs(rat);
         const double mx = (ar != ar) ? ar : (ar > tol1 ? ar : tol1);
-        x = xf + sgn_nz(rat) * mx;
+        const double x = xf + sgn_nz(rat) * mx;
         const double fu = path_dist(s, x, px, py);
         num += 1;
-        if (fu <= fx) {
-            if (x >= xf) a = xf; else b = xf;
-            fulc = nfc; ffulc = fnfc;
-            nfc = xf; fnfc = fx;
-            xf = x; fx = fu;
-        } else {
-            if (x < xf) a = x; else b = x;
-            if ((fu <= fnfc) || (nfc == xf)) {
-                fulc = nfc; ffulc = fnfc;
-                nfc = x; fnfc = fu;
-            } else if ((fu <= ffulc) || (fulc == xf) || (fulc == nfc)) {
-                fulc = x; ffulc = fu;
-            }
-        }
+        const bool le = fu <= fx;
+        const bool c1 = !le && ((fu <= fnfc) || (nfc == xf));
+        const bool c2 = !le && !c1 && ((fu <= ffulc) || (fulc == xf) || (fulc == nfc));
+        const double na = le ? ((x >= xf) ? xf : a) : ((x < xf) ? x : a);
+        const double nb = le ? ((x >= xf) ? b : xf) : ((x < xf) ? b : x);
+        const double nfulc = (le || c1) ? nfc : (c2 ? x : fulc);
+        const double nffulc = (le || c1) ? fnfc : (c2 ? fu : ffulc);
+        const double nnfc = le ? xf : (c1 ? x : nfc);
+        const double nfnfc = le ? fx : (c1 ? fu : fnfc);
+        xf = le ? x : xf;
+        fx = le ? fu : fx;
+        a = na; b = nb; fulc = nfulc; ffulc = nffulc; nfc = nnfc; fnfc = nfnfc;
         xm = 0.5 * (a + b);
         tol1 = sqrt_eps * fabs(xf) + xatol3;
         tol2 = 2.0 * tol1;
@@ -184,11 +209,22 @@ __device__ double closest_u(const d2d_scn& s, double px, double py) {
 }
 
 // ------------------------------------------------------------------------------ bodies / physics
+// One cpSpaceStep(1/60) of the Drone.py body/joint configuration, split in
+// two stages so that a caller can retire the positions before the Gauss-Seidel sweep:
+//   phys_positions   forces on the frame (drone_2d_env.py:403-404), cpBodyUpdatePosition of the
+//                    3 bodies, frame-box vs circle contact (the sticky begin() flag, :17-19)
+//   phys_velocities  PivotJoint preStep (K^-1, bias = -delta/dt), cpBodyUpdateVelocity, cached
+//                    impulses (dt_coef = 1; after a reset jAcc = 0 so dt_coef = 0 is identical),
+//                    10 Gauss-Seidel sweeps over the joints in space.add order.
+// With JBUF = true the per-joint (K^-1, bias) live in a per-lane LDS buffer (`jb[f * stride]`,
+// 36 doubles) and are re-read every sweep (volatile): that keeps the sweep at ~90 VGPRs.
 struct Body {
     double px, py, a, vx, vy, w;
 };
 
-// cpMomentForPoly(m, cpBoxShapeNew2 verts) -- evaluated at compile time order, see oracle
+constexpr double M_F = 0.2, M_M = 0.4;   // drone_2d_env.py:233 -> Drone.py:19,36,50
+
+// cpMomentForPoly(m, cpBoxShapeNew2 verts) in Chipmunk's evaluation order
 __host__ __device__ constexpr double moment_box(double m, double w, double h) {
     double hw = w / 2.0, hh = h / 2.0;
     double vx[4] = {hw, hw, -hw, -hw}, vy[4] = {-hh, hh, hh, -hh};
@@ -203,20 +239,34 @@ __host__ __device__ constexpr double moment_box(double m, double w, double h) {
     }
     return (m * s1) / (6.0 * s2);
 }
+constexpr double MI_F = 1.0 / M_F, MI_M = 1.0 / M_M;
+constexpr double II_F = 1.0 / moment_box(M_F, 100.0, 10.0);
+constexpr double II_M = 1.0 / moment_box(M_M, 20.0, 20.0);
 
-// One cpSpaceStep(1/60) of the Drone.py body/joint configuration with the two thrusts already
-// mapped (drone_2d_env.py:400-406).  B[0] frame, B[1] left motor, B[2] right motor; j[12] the six
-// accumulated pivot impulses.  Returns true if the frame box touches any circle after the
-// position update (the sticky begin() flag, drone_2d_env.py:17-19).
-__device__ __forceinline__ bool space_step(const d2d_scn& s, double damping_dt, Body B[3], double j[12],
-                                           double fL, double fR) {
-    constexpr double M_F = 0.2, M_M = 0.4;
-    constexpr double MI_F = 1.0 / M_F, MI_M = 1.0 / M_M;
-    constexpr double II_F = 1.0 / moment_box(M_F, 100.0, 10.0);
-    constexpr double II_M = 1.0 / moment_box(M_M, 20.0, 20.0);
-    // ---- forces on the frame at local (-40,0) then (40,0): cpBodyApplyForceAtLocalPoint
-    double c0 = cos(B[0].a), s0 = sin(B[0].a);
-    double fx, fy, tq;
+// Joint anchors (Drone.py:61-95): motor side JA = (-7, 0, 7) for both motors, frame side JB.
+// r = R(theta) * (a, 0) = (c*a + (-s)*0, s*a + c*0) == (c*a, s*a) (adding a signed zero never
+// changes the value), and c*(-a) == -(c*a) bitwise, so each body needs only its c*|a|, s*|a|.
+struct Arms {
+    double m7c[2], m7s[2];          // motor (left, right): c*7, s*7
+    double f47c, f47s, f40c, f40s, f33c, f33s;  // frame: c*47, s*47, c*40, s*40, c*33, s*33
+};
+__device__ __forceinline__ void arm(const Arms& A, int k, double& r1x, double& r1y, double& r2x, double& r2y) {
+    const int m = k < 3 ? 0 : 1;
+    const int q = k % 3;  // JA = -7, 0, 7
+    r1x = (q == 0) ? -A.m7c[m] : ((q == 1) ? 0.0 : A.m7c[m]);
+    r1y = (q == 0) ? -A.m7s[m] : ((q == 1) ? 0.0 : A.m7s[m]);
+    // JB = -47, -40, -33, 33, 40, 47
+    const double c = (k == 0 || k == 5) ? A.f47c : ((k == 1 || k == 4) ? A.f40c : A.f33c);
+    const double s = (k == 0 || k == 5) ? A.f47s : ((k == 1 || k == 4) ? A.f40s : A.f33s);
+    r2x = (k < 3) ? -c : c;
+    r2y = (k < 3) ? -s : s;
+}
+
+__device__ __forceinline__ bool phys_positions(const d2d_scn& s, Body B[3], double fL, double fR, double cs[3],
+                                               double sn[3], double& fx, double& fy, double& tq) {
+    // forces on the frame at local (-40,0) then (40,0): cpBodyApplyForceAtLocalPoint
+    double c0, s0;
+    sincos_d(B[0].a, s0, c0);
     {
         const double tx = B[0].px - (0.0 * c0 - 0.0 * s0), ty = B[0].py - (0.0 * s0 + 0.0 * c0);
         const double cgx = c0 * 0.0 + (-s0) * 0.0 + tx, cgy = s0 * 0.0 + c0 * 0.0 + ty;
@@ -233,17 +283,15 @@ __device__ __forceinline__ bool space_step(const d2d_scn& s, double damping_dt, 
         fy = fy + fwy;
         tq += rx * fwy - ry * fwx;
     }
-    // ---- 1. cpBodyUpdatePosition
-    double cs[3], sn[3];
+    // 1. cpBodyUpdatePosition (v_bias = 0)
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
         B[i].px = B[i].px + (B[i].vx + 0.0) * DT;
         B[i].py = B[i].py + (B[i].vy + 0.0) * DT;
         B[i].a = B[i].a + (B[i].w + 0.0) * DT;
-        cs[i] = cos(B[i].a);
-        sn[i] = sin(B[i].a);
+        sincos_d(B[i].a, sn[i], cs[i]);
     }
-    // ---- 2. collision: CircleToPoly(circle, frame box) contact iff dist(center, box) <= r
+    // 2. collision: CircleToPoly(circle, frame box) contact iff dist(center, box) <= r
     bool hit = false;
     for (int k = 0; k < ((D2D_ABLATE & 8) ? 0 : s.n_circles); ++k) {
         const double dx = s.cx[k] - B[0].px, dy = s.cy[k] - B[0].py;
@@ -253,103 +301,156 @@ __device__ __forceinline__ bool space_step(const d2d_scn& s, double damping_dt, 
         const double r = s.cr[k];
         hit |= (ex * ex + ey * ey <= r * r);
     }
-    // ---- 3. PivotJoint preStep: r1 (motor), r2 (frame), K^-1, bias = -delta/dt
-    constexpr double JA[6] = {-7.0, 0.0, 7.0, -7.0, 0.0, 7.0};
-    constexpr double JB[6] = {-47.0, -40.0, -33.0, 33.0, 40.0, 47.0};
-    const double bias_coef = -(1.0 - 0.0) / DT;  // error_bias = 0 -> 1 - 0^dt = 1
-    double r1x[6], r1y[6], r2x[6], r2y[6], ka[6], kb[6], kc[6], kd[6], bx[6], by[6];
+    return hit;
+}
+
+__device__ __forceinline__ Arms make_arms(const double cs[3], const double sn[3]) {
+    Arms A;
+    A.m7c[0] = cs[1] * 7.0; A.m7s[0] = sn[1] * 7.0;
+    A.m7c[1] = cs[2] * 7.0; A.m7s[1] = sn[2] * 7.0;
+    A.f47c = cs[0] * 47.0; A.f47s = sn[0] * 47.0;
+    A.f40c = cs[0] * 40.0; A.f40s = sn[0] * 40.0;
+    A.f33c = cs[0] * 33.0; A.f33s = sn[0] * 33.0;
+    return A;
+}
+
+// stage 2.  pos = {frame px, py, left px, py, right px, py} (post position update); vel[9] =
+// (vx, vy, w) of frame, left, right; j[12] the accumulated pivot impulses.
+template <bool JBUF>
+__device__ __forceinline__ void phys_velocities(const Arms& A, const double pos[6], double damping_dt, double fx,
+                                                double fy, double tq, double vel[9], double j[12], double* jb,
+                                                int stride) {
+    const double bias_coef = -(1.0 - 0.0) / DT;  // error_bias = 0 -> bias_coef(0, dt) = 1 - 0^dt = 1
+    double kk[JBUF ? 1 : 6][6];
+    // preStep
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
         const int m = k < 3 ? 1 : 2;
-        r1x[k] = cs[m] * JA[k] + (-sn[m]) * 0.0;
-        r1y[k] = sn[m] * JA[k] + cs[m] * 0.0;
-        r2x[k] = cs[0] * JB[k] + (-sn[0]) * 0.0;
-        r2y[k] = sn[0] * JB[k] + cs[0] * 0.0;
+        double r1x, r1y, r2x, r2y;
+        arm(A, k, r1x, r1y, r2x, r2y);
         const double m_sum = MI_M + MI_F;
         double k11 = m_sum, k12 = 0.0, k21 = 0.0, k22 = m_sum;
-        const double r1xsq = r1x[k] * r1x[k] * II_M, r1ysq = r1y[k] * r1y[k] * II_M;
-        const double r1nxy = -r1x[k] * r1y[k] * II_M;
+        const double r1xsq = r1x * r1x * II_M, r1ysq = r1y * r1y * II_M;
+        const double r1nxy = -r1x * r1y * II_M;
         k11 += r1ysq; k12 += r1nxy; k21 += r1nxy; k22 += r1xsq;
-        const double r2xsq = r2x[k] * r2x[k] * II_F, r2ysq = r2y[k] * r2y[k] * II_F;
-        const double r2nxy = -r2x[k] * r2y[k] * II_F;
+        const double r2xsq = r2x * r2x * II_F, r2ysq = r2y * r2y * II_F;
+        const double r2nxy = -r2x * r2y * II_F;
         k11 += r2ysq; k12 += r2nxy; k21 += r2nxy; k22 += r2xsq;
         const double det = k11 * k22 - k12 * k21;
         const double det_inv = 1.0 / det;
-        ka[k] = k22 * det_inv; kb[k] = -k12 * det_inv; kc[k] = -k21 * det_inv; kd[k] = k11 * det_inv;
-        const double dx = (B[0].px + r2x[k]) - (B[m].px + r1x[k]);
-        const double dy = (B[0].py + r2y[k]) - (B[m].py + r1y[k]);
-        bx[k] = dx * bias_coef;
-        by[k] = dy * bias_coef;
-    }
-    // ---- 4. cpBodyUpdateVelocity (gravity, damping^dt, forces on the frame only)
-    B[0].vx = B[0].vx * damping_dt + (0.0 + fx * MI_F) * DT;
-    B[0].vy = B[0].vy * damping_dt + (GRAV_Y + fy * MI_F) * DT;
-    B[0].w = B[0].w * damping_dt + tq * II_F * DT;
+        const double dx = (pos[0] + r2x) - (pos[2 * m] + r1x);
+        const double dy = (pos[1] + r2y) - (pos[2 * m + 1] + r1y);
+        const double v[6] = {k22 * det_inv, -k12 * det_inv, -k21 * det_inv, k11 * det_inv, dx * bias_coef,
+                             dy * bias_coef};
 #pragma unroll
-    for (int i = 1; i < 3; ++i) {
-        B[i].vx = B[i].vx * damping_dt + (0.0 + 0.0 * MI_M) * DT;
-        B[i].vy = B[i].vy * damping_dt + (GRAV_Y + 0.0 * MI_M) * DT;
-        B[i].w = B[i].w * damping_dt + 0.0 * II_M * DT;
+        for (int q = 0; q < 6; ++q) {
+            if (JBUF) jb[(6 * k + q) * stride] = v[q];
+            else kk[JBUF ? 0 : k][q] = v[q];
+        }
     }
-    // ---- 5. applyCachedImpulse (dt_coef = 1; after a reset jAcc = 0 so dt_coef = 0 is identical)
+    // cpBodyUpdateVelocity: gravity (0, -1000), damping^dt, forces on the frame only
+    vel[0] = vel[0] * damping_dt + (0.0 + fx * MI_F) * DT;
+    vel[1] = vel[1] * damping_dt + (GRAV_Y + fy * MI_F) * DT;
+    vel[2] = vel[2] * damping_dt + tq * II_F * DT;
+#pragma unroll
+    for (int b = 1; b < 3; ++b) {
+        vel[3 * b + 0] = vel[3 * b + 0] * damping_dt + (0.0 + 0.0 * MI_M) * DT;
+        vel[3 * b + 1] = vel[3 * b + 1] * damping_dt + (GRAV_Y + 0.0 * MI_M) * DT;
+        vel[3 * b + 2] = vel[3 * b + 2] * damping_dt + 0.0 * II_M * DT;
+    }
+    // applyCachedImpulse with dt_coef = 1
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
         const int m = k < 3 ? 1 : 2;
+        double r1x, r1y, r2x, r2y;
+        arm(A, k, r1x, r1y, r2x, r2y);
         const double jx = j[2 * k] * 1.0, jy = j[2 * k + 1] * 1.0;
-        B[m].vx = B[m].vx + (-jx) * MI_M;
-        B[m].vy = B[m].vy + (-jy) * MI_M;
-        B[m].w += II_M * (r1x[k] * (-jy) - r1y[k] * (-jx));
-        B[0].vx = B[0].vx + jx * MI_F;
-        B[0].vy = B[0].vy + jy * MI_F;
-        B[0].w += II_F * (r2x[k] * jy - r2y[k] * jx);
+        vel[3 * m + 0] = vel[3 * m + 0] + (-jx) * MI_M;
+        vel[3 * m + 1] = vel[3 * m + 1] + (-jy) * MI_M;
+        vel[3 * m + 2] += II_M * (r1x * (-jy) - r1y * (-jx));
+        vel[0] = vel[0] + jx * MI_F;
+        vel[1] = vel[1] + jy * MI_F;
+        vel[2] += II_F * (r2x * jy - r2y * jx);
     }
-    // ---- 6. 10 Gauss-Seidel iterations over the joints in space.add order
+    // 10 sequential-impulse sweeps (Space.iterations default)
+#pragma unroll 1
     for (int it = 0; it < ((D2D_ABLATE & 4) ? 0 : 10); ++it) {
 #pragma unroll
         for (int k = 0; k < 6; ++k) {
             const int m = k < 3 ? 1 : 2;
-            const double v1x = B[m].vx + (-r1y[k]) * B[m].w, v1y = B[m].vy + r1x[k] * B[m].w;
-            const double v2x = B[0].vx + (-r2y[k]) * B[0].w, v2y = B[0].vy + r2x[k] * B[0].w;
-            const double ux = bx[k] - (v2x - v1x), uy = by[k] - (v2y - v1y);
-            double jx = ux * ka[k] + uy * kb[k];
-            double jy = ux * kc[k] + uy * kd[k];
+            double r1x, r1y, r2x, r2y;
+            arm(A, k, r1x, r1y, r2x, r2y);
+            double ka, kb, kc, kd, bx, by;
+            if (JBUF) {
+                // an explicit LDS (address_space 3) pointer: generic volatile loads would become flat
+                // loads with one 64-bit address per slot
+                using LdsD = __attribute__((address_space(3))) double;
+                const volatile LdsD* kv = (const volatile LdsD*)jb;
+                ka = kv[(6 * k + 0) * stride]; kb = kv[(6 * k + 1) * stride];
+                kc = kv[(6 * k + 2) * stride]; kd = kv[(6 * k + 3) * stride];
+                bx = kv[(6 * k + 4) * stride]; by = kv[(6 * k + 5) * stride];
+            } else {
+                const int kq = JBUF ? 0 : k;
+                ka = kk[kq][0]; kb = kk[kq][1]; kc = kk[kq][2]; kd = kk[kq][3]; bx = kk[kq][4]; by = kk[kq][5];
+            }
+            const double v1x = vel[3 * m + 0] + (-r1y) * vel[3 * m + 2], v1y = vel[3 * m + 1] + r1x * vel[3 * m + 2];
+            const double v2x = vel[0] + (-r2y) * vel[2], v2y = vel[1] + r2x * vel[2];
+            const double ux = bx - (v2x - v1x), uy = by - (v2y - v1y);
+            double jx = ux * ka + uy * kb;
+            double jy = ux * kc + uy * kd;
             const double ox = j[2 * k], oy = j[2 * k + 1];
             const double nx = ox + jx, ny = oy + jy;
             j[2 * k] = nx;
             j[2 * k + 1] = ny;
             jx = nx - ox;
             jy = ny - oy;
-            B[m].vx = B[m].vx + (-jx) * MI_M;
-            B[m].vy = B[m].vy + (-jy) * MI_M;
-            B[m].w += II_M * (r1x[k] * (-jy) - r1y[k] * (-jx));
-            B[0].vx = B[0].vx + jx * MI_F;
-            B[0].vy = B[0].vy + jy * MI_F;
-            B[0].w += II_F * (r2x[k] * jy - r2y[k] * jx);
+            vel[3 * m + 0] = vel[3 * m + 0] + (-jx) * MI_M;
+            vel[3 * m + 1] = vel[3 * m + 1] + (-jy) * MI_M;
+            vel[3 * m + 2] += II_M * (r1x * (-jy) - r1y * (-jx));
+            vel[0] = vel[0] + jx * MI_F;
+            vel[1] = vel[1] + jy * MI_F;
+            vel[2] += II_F * (r2x * jy - r2y * jx);
         }
+    }
+}
+
+// whole step, registers only (reference / diagnostics)
+__device__ __forceinline__ bool space_step(const d2d_scn& s, double damping_dt, Body B[3], double j[12], double fL,
+                                           double fR) {
+    double cs[3], sn[3], fx, fy, tq;
+    const bool hit = phys_positions(s, B, fL, fR, cs, sn, fx, fy, tq);
+    const Arms A = make_arms(cs, sn);
+    const double pos[6] = {B[0].px, B[0].py, B[1].px, B[1].py, B[2].px, B[2].py};
+    double vel[9] = {B[0].vx, B[0].vy, B[0].w, B[1].vx, B[1].vy, B[1].w, B[2].vx, B[2].vy, B[2].w};
+    phys_velocities<false>(A, pos, damping_dt, fx, fy, tq, vel, j, nullptr, 0);
+#pragma unroll
+    for (int b = 0; b < 3; ++b) {
+        B[b].vx = vel[3 * b];
+        B[b].vy = vel[3 * b + 1];
+        B[b].w = vel[3 * b + 2];
     }
     return hit;
 }
 
-// ------------------------------------------------------------------------------ observation
-// get_observation (drone_2d_env.py:631-773) for frame body F; may set the sticky LA lock.
-__device__ __forceinline__ void observe(const d2d_cfg& cfg, const d2d_scn& s, const Body& F, uint32_t& flags,
-                                        double obs[D2D_OBS_DIM]) {
+// ------------------------------------------------------------------------------ observation roles
+// sensor role: obs[0..18] of get_observation (drone_2d_env.py:633-727) for frame state F.
+// k = 3 nearest circles by min over the UNROTATED frame vertices (+-50, +-5) of |v+p-c| - r;
+// sqrt is monotone and correctly rounded, so sqrt(min d^2) - r == min(sqrt(d^2) - r) bitwise.
+__device__ __forceinline__ void sensor_obs(const d2d_cfg& cfg, const d2d_scn& s, const Body& F, double o[19]) {
     const double W = cfg.screen_w, H = cfg.screen_h;
     const double x = F.px, y = F.py, al = F.a;
-    obs[0] = m1to1(F.vx, -1330.0, 1330.0);
-    obs[1] = m1to1(F.vy, -1330.0, 1330.0);
-    obs[2] = clipd(F.w / 11.7, -1.0, 1.0);
-    obs[3] = al / PI;
-    obs[4] = m1to1(s.wp_last_x - x, 0.0, W);
-    obs[5] = m1to1(s.wp_last_y - y, 0.0, H);
-    obs[6] = m1to1(x, 0.0, W);
-    obs[7] = m1to1(y, 0.0, H);
-    // k = 3 nearest circles by min over the UNROTATED frame vertices (+-50, +-5) of |v+p-c| - r;
-    // sqrt is monotone and correctly rounded, so sqrt(min d^2) - r == min(sqrt(d^2) - r) bitwise.
-    double bd0 = 0.0, bd1 = 0.0, bd2 = 0.0;
+    o[0] = m1to1(F.vx, -VEL_MAX, VEL_MAX);
+    o[1] = m1to1(F.vy, -VEL_MAX, VEL_MAX);
+    o[2] = clipd(F.w / 11.7, -1.0, 1.0);
+    o[3] = al / PI;
+    o[4] = m1to1(s.wp_last_x - x, 0.0, W);
+    o[5] = m1to1(s.wp_last_y - y, 0.0, H);
+    o[6] = m1to1(x, 0.0, W);
+    o[7] = m1to1(y, 0.0, H);
+    double bd0 = __builtin_inf(), bd1 = __builtin_inf(), bd2 = __builtin_inf();
     int bi0 = -1, bi1 = -1, bi2 = -1;
-    const int nc = s.n_circles;
-    for (int i = 0; i < ((D2D_ABLATE & 2) ? 0 : nc); ++i) {
+    const int nc = (D2D_ABLATE & 2) ? 0 : s.n_circles;
+    for (int i = 0; i < nc; ++i) {
         const double cx = s.cx[i], cy = s.cy[i];
         const double ax = (50.0 + x) - cx, bxx = (-50.0 + x) - cx;
         const double ay = (-5.0 + y) - cy, byy = (5.0 + y) - cy;
@@ -361,145 +462,163 @@ __device__ __forceinline__ void observe(const d2d_cfg& cfg, const d2d_scn& s, co
         q = (q2 < q) ? q2 : q;
         q = (q3 < q) ? q3 : q;
         const double d = sqrt(q) - s.cr[i];
-        // stable ascending insertion into the top-3
-        if (bi0 < 0 || d < bd0) {
-            bd2 = bd1; bi2 = bi1; bd1 = bd0; bi1 = bi0; bd0 = d; bi0 = i;
-        } else if (bi1 < 0 || d < bd1) {
-            bd2 = bd1; bi2 = bi1; bd1 = d; bi1 = i;
-        } else if (bi2 < 0 || d < bd2) {
-            bd2 = d; bi2 = i;
-        }
+        // stable ascending insertion into the top-3 (equal keys keep index order)
+        const bool l0 = (bi0 < 0) || d < bd0, l1 = (bi1 < 0) || d < bd1, l2 = (bi2 < 0) || d < bd2;
+        bd2 = l1 ? bd1 : (l2 ? d : bd2);
+        bi2 = l1 ? bi1 : (l2 ? i : bi2);
+        bd1 = l0 ? bd0 : (l1 ? d : bd1);
+        bi1 = l0 ? bi0 : (l1 ? i : bi1);
+        bd0 = l0 ? d : bd0;
+        bi0 = l0 ? i : bi0;
     }
     const double diag = sqrt(W * W + H * H);
-    {
-        const double bd[3] = {bd0, bd1, bd2};
-        const int bi[3] = {bi0, bi1, bi2};
+    const double bd[3] = {bd0, bd1, bd2};
+    const int bi[3] = {bi0, bi1, bi2};
 #pragma unroll
-        for (int jj = 0; jj < 3; ++jj) {
-            if (bi[jj] >= 0) {
-                obs[8 + 3 * jj] = m1to1(bd[jj], 0.0, diag);
-                const double ang = ssa(atan2(y - s.cy[bi[jj]], x - s.cx[bi[jj]]) - al - PI);
-                obs[9 + 3 * jj] = sin(ang);
-                obs[10 + 3 * jj] = cos(ang);
-            } else {
-                obs[8 + 3 * jj] = 1.0;
-                obs[9 + 3 * jj] = 0.0;
-                obs[10 + 3 * jj] = 0.0;
-            }
-        }
+    for (int jj = 0; jj < 3; ++jj) {  // three independent atan2/sincos chains
+        const int idx = bi[jj] < 0 ? 0 : bi[jj];
+        const double ang = ssa(atan2(y - s.cy[idx], x - s.cx[idx]) - al - PI);
+        double sa, ca;
+        sincos_d(ang, sa, ca);
+        const bool have = bi[jj] >= 0;
+        o[8 + 3 * jj] = have ? m1to1(bd[jj], 0.0, diag) : 1.0;
+        o[9 + 3 * jj] = have ? sa : 0.0;
+        o[10 + 3 * jj] = have ? ca : 0.0;
     }
     const double vab = ssa(atan2(F.vy, F.vx) - al);
-    obs[17] = sin(vab);
-    obs[18] = cos(vab);
-    // closest point and lookahead: get_closest_u is evaluated once (the reference calls it twice
-    // with identical input, predef_path.py:255 and :261)
+    sincos_d(vab, o[17], o[18]);
+}
+
+// path role: obs[19..26] (drone_2d_env.py:729-763).  get_closest_u is evaluated once (the
+// reference calls it twice with identical input, predef_path.py:255 and :261).  Updates the
+// sticky LA lock in `flags`; returns the closest point (cpx, cpy) for the path-adherence reward.
+__device__ __forceinline__ void path_obs(const d2d_cfg& cfg, const d2d_scn& s, double x, double y, double al,
+                                         uint32_t& flags, double o[8]) {
+    const double W = cfg.screen_w, H = cfg.screen_h;
     const double u = (D2D_ABLATE & 1) ? clipd(x - 100.0, -10.0, s.us[s.n_wps - 1]) : closest_u(s, x, y);
     double cpx, cpy;
     path_eval(s, u, cpx, cpy);
-    obs[19] = m1to1(cpx, 0.0, W);
-    obs[20] = m1to1(cpy, 0.0, H);
     const double L = s.us[s.n_wps - 1];
     const double ula = (u + cfg.lookahead > L) ? L : u + cfg.lookahead;
     double lax, lay;
     path_eval(s, ula, lax, lay);
     if (fabs(lax - s.wp_last_x) < 10.0 && fabs(lay - s.wp_last_y) < 10.0) flags |= D2D_FLAG_LA_LOCK;
-    if (flags & D2D_FLAG_LA_LOCK) {
-        lax = s.wp_last_x;
-        lay = s.wp_last_y;
-    }
-    obs[21] = m1to1(lax, 0.0, W);
-    obs[22] = m1to1(lay, 0.0, H);
-    const double ca = cos(al), sa = sin(al);
+    const bool lock = (flags & D2D_FLAG_LA_LOCK) != 0;
+    lax = lock ? s.wp_last_x : lax;
+    lay = lock ? s.wp_last_y : lay;
+    o[0] = m1to1(cpx, 0.0, W);
+    o[1] = m1to1(cpy, 0.0, H);
+    o[2] = m1to1(lax, 0.0, W);
+    o[3] = m1to1(lay, 0.0, H);
+    double sa, ca;
+    sincos_d(al, sa, ca);
     // np.matmul(R_w_b(alpha), d): row r = fma(R[r][0], d0, R[r][1] * d1)
     double dx = lax - x, dy = lay - y;
-    double bxv = fma(ca, dx, (-sa) * dy), byv = fma(sa, dx, ca * dy);
-    const double laa = ssa(atan2(byv, bxv) - al);
-    obs[23] = sin(laa);
-    obs[24] = cos(laa);
+    const double bx1 = fma(ca, dx, (-sa) * dy), by1 = fma(sa, dx, ca * dy);
     dx = cpx - x;
     dy = cpy - y;
-    bxv = fma(ca, dx, (-sa) * dy);
-    byv = fma(sa, dx, ca * dy);
-    const double cpa = ssa(atan2(byv, bxv) - al);
-    obs[25] = sin(cpa);
-    obs[26] = cos(cpa);
+    const double bx2 = fma(ca, dx, (-sa) * dy), by2 = fma(sa, dx, ca * dy);
+    const double laa = ssa(atan2(by1, bx1) - al);  // two independent chains
+    const double cpa = ssa(atan2(by2, bx2) - al);
+    sincos_d(laa, o[4], o[5]);
+    sincos_d(cpa, o[6], o[7]);
 }
 
 // ------------------------------------------------------------------------------ reward
-struct Reward {
-    double reward, ca, pa, pp, coll, reach, aa, dclose, dist_path;
-    int cause;
+// The reward decodes from the fp64 observation exactly as the reference does (drone_2d_env.py:423-572).
+struct CAPart {  // computed by the sensor role (obs 0..18 only)
+    double vel_ang, ca, lpa, lca, dclose;
 };
-// drone_2d_env.py:423-572 -- decodes from the (fp64) observation exactly as the reference does
-__device__ __forceinline__ Reward reward_fn(const d2d_cfg& cfg, const d2d_scn& s, const double* obs,
-                                            bool collided, int t) {
+__device__ __forceinline__ CAPart reward_ca_part(const d2d_cfg& cfg, const d2d_scn& s, const double* o) {
     const double W = cfg.screen_w, H = cfg.screen_h;
-    Reward R;
-    const double vxd = invm1to1(obs[0], -1330.0, 1330.0);
-    const double vyd = invm1to1(obs[1], -1330.0, 1330.0);
-    const double alpha = obs[3] * PI;
-    const double tdx = invm1to1(obs[4], 0.0, W), tdy = invm1to1(obs[5], 0.0, H);
-    const double pxd = invm1to1(obs[6], 0.0, W), pyd = invm1to1(obs[7], 0.0, H);
-    const double vel_ang = pymod(atan2(obs[17] * PI, obs[18] * PI) + TWO_PI, TWO_PI);
-    const double cpx = invm1to1(obs[19], 0.0, W), cpy = invm1to1(obs[20], 0.0, H);
-    const double la_ang = pymod(atan2(obs[23], obs[24]) + TWO_PI, TWO_PI);
-    double lpa = 1.0, lca = 1.0, ca = 0.0;
-    R.dclose = __builtin_inf();
+    CAPart P;
+    P.vel_ang = pymod_2pi(atan2(o[17] * PI, o[18] * PI) + TWO_PI);
+    P.lpa = 1.0;
+    P.lca = 1.0;
+    P.ca = 0.0;
+    P.dclose = __builtin_inf();
     if (s.n_circles > 0) {
         const double diag = sqrt(W * W + H * H);
-        const double d = invm1to1(obs[8], 0.0, diag);
-        R.dclose = d;
-        const double oa = pymod(atan2(obs[9], obs[10]) + TWO_PI, TWO_PI);
-        const double adiff = fabs((pymod(oa - vel_ang + PI, TWO_PI) - PI) * (180.0 / PI));
+        const double d = invm1to1(o[8], 0.0, diag);
+        P.dclose = d;
+        const double oa = pymod_2pi(atan2(o[9], o[10]) + TWO_PI);
+        const double adiff = fabs((pymod_2pi(oa - P.vel_ang + PI) - PI) * (180.0 / PI));
         const double Rr = cfg.danger_range, A = cfg.danger_angle, k = cfg.abs_inv_ca_min_rew;
         if (d < Rr && cfg.use_lambda) {
-            lpa = (d / Rr) / 2.0;
-            if (lpa < 0.10) lpa = 0.10;
-            lca = 1.0 - lpa;
+            const double l = (d / Rr) / 2.0;
+            P.lpa = (l < 0.10) ? 0.10 : l;
+            P.lca = 1.0 - P.lpa;
         }
         if (d < Rr) {
             double rr = -(((Rr + k * Rr) / (d + k * Rr)) - 1.0);
             double ar = -(((A + k * A) / (adiff + k * A)) - 1.0);
-            if (ar > 0.0) ar = 0.0;
-            if (rr > 0.0) rr = 0.0;
-            ca = rr + ar;
+            ar = (ar > 0.0) ? 0.0 : ar;
+            rr = (rr > 0.0) ? 0.0 : rr;
+            P.ca = rr + ar;
         }
     }
+    return P;
+}
+// end conditions that need only the post-physics frame (drone_2d_env.py:543-571): collision,
+// reach-end (decoded target distance), AA (decoded alpha), time-up.  Known before the observation,
+// which lets the cooperative kernel start the auto-reset observation concurrently.
+__device__ __forceinline__ int end_cause(const d2d_cfg& cfg, const d2d_scn& s, const Body& F, bool collided, int t) {
+    const double W = cfg.screen_w, H = cfg.screen_h;
+    const double tdx = invm1to1(m1to1(s.wp_last_x - F.px, 0.0, W), 0.0, W);
+    const double tdy = invm1to1(m1to1(s.wp_last_y - F.py, 0.0, H), 0.0, H);
+    const double alpha = (F.a / PI) * PI;
+    int cause = 0;
+    if (collided) cause |= D2D_END_COLLISION;
+    if (fabs(tdx) < cfg.reach_end_radius && fabs(tdy) < cfg.reach_end_radius) cause |= D2D_END_REACH;
+    if (fabs(alpha) >= cfg.aa_angle) cause |= D2D_END_AA;
+    if (t == cfg.n_steps) cause |= D2D_END_TIMEUP;
+    return cause;
+}
+struct Reward {
+    double reward, ca, pa, pp, coll, reach, aa, dclose, dist_path;
+    int cause;
+};
+// final combination (path-role results o19..26 = po[0..7], CA part from the sensor role)
+__device__ __forceinline__ Reward reward_final(const d2d_cfg& cfg, const Body& F, const double* po,
+                                               const CAPart& P, int cause) {
+    const double W = cfg.screen_w, H = cfg.screen_h;
+    Reward R;
+    const double vxd = invm1to1(m1to1(F.vx, -VEL_MAX, VEL_MAX), -VEL_MAX, VEL_MAX);
+    const double vyd = invm1to1(m1to1(F.vy, -VEL_MAX, VEL_MAX), -VEL_MAX, VEL_MAX);
+    const double alpha = (F.a / PI) * PI;
+    const double pxd = invm1to1(m1to1(F.px, 0.0, W), 0.0, W), pyd = invm1to1(m1to1(F.py, 0.0, H), 0.0, H);
+    const double cpx = invm1to1(po[0], 0.0, W), cpy = invm1to1(po[1], 0.0, H);
+    const double la_ang = pymod_2pi(atan2(po[4], po[5]) + TWO_PI);
     const double dist = norm2(cpx - pxd, cpy - pyd);
     R.dist_path = dist;
     const double pa = -(2.0 * (clipd(dist, 0.0, cfg.pa_band_edge) / cfg.pa_band_edge) - 1.0) * cfg.pa_scale;
     const double vel = sqrt(vxd * vxd + vyd * vyd);
     const double sv = vel * cfg.pp_vel_scale;
-    const double vla = fabs(pymod(la_ang - vel_ang + PI, TWO_PI) - PI);
+    const double vla = fabs(pymod_2pi(la_ang - P.vel_ang + PI) - PI);
     const double pp = clipd(cos(vla) * sv, cfg.pp_rew_min, cfg.pp_rew_max);
-    int cause = 0;
-    double coll = 0.0;
-    if (collided) {
-        coll = cfg.rew_collision;
-        cause |= D2D_END_COLLISION;
-    }
-    double reach = 0.0;
-    if (fabs(tdx) < cfg.reach_end_radius && fabs(tdy) < cfg.reach_end_radius) {
-        cause |= D2D_END_REACH;
-        reach = cfg.rew_reach_end;
-    }
+    const double coll = (cause & D2D_END_COLLISION) ? cfg.rew_collision : 0.0;
+    const double reach = (cause & D2D_END_REACH) ? cfg.rew_reach_end : 0.0;
     double aa = 0.0;
     if (alpha > cfg.aa_band) aa = -sin(alpha);
     if (alpha < -cfg.aa_band) aa = sin(alpha);
-    if (fabs(alpha) >= cfg.aa_angle) {
-        aa = cfg.rew_aa;
-        cause |= D2D_END_AA;
-    }
-    if (t == cfg.n_steps) cause |= D2D_END_TIMEUP;
-    R.reward = aa + pa * lpa + pp + coll + ca * lca + reach;
-    R.ca = ca * lca;
-    R.pa = pa * lpa;
+    if (cause & D2D_END_AA) aa = cfg.rew_aa;
+    R.reward = aa + pa * P.lpa + pp + coll + P.ca * P.lca + reach;
+    R.ca = P.ca * P.lca;
+    R.pa = pa * P.lpa;
     R.pp = pp;
     R.coll = coll;
     R.reach = reach;
     R.aa = aa;
+    R.dclose = P.dclose;
     R.cause = cause;
     return R;
+}
+
+// full single-lane observation (reset kernel)
+__device__ __forceinline__ void observe(const d2d_cfg& cfg, const d2d_scn& s, const Body& F, uint32_t& flags,
+                                        double obs[D2D_OBS_DIM]) {
+    sensor_obs(cfg, s, F, obs);
+    path_obs(cfg, s, F.px, F.py, F.a, flags, obs + 19);
 }
 
 }  // namespace d2d
