@@ -38,6 +38,7 @@ struct d2d_handle {
     int32_t* env_scn = nullptr;
     uint64_t seed = 0;
     bool reset_done = false;
+    uint64_t* stamps = nullptr;  // diagnostic builds (D2D_STAMPS) only
 };
 
 namespace {
@@ -54,6 +55,7 @@ StepArgs make_args(const d2d_t* h) {
     a.cfg = h->cfg;
     a.damping_dt = std::pow(h->cfg.damping, 1.0 / 60.0);
     a.seed = h->seed;
+    a.stamps = h->stamps;
     return a;
 }
 
@@ -120,6 +122,15 @@ void d2d_destroy(d2d_t* h) {
 }
 
 int32_t d2d_n_envs(const d2d_t* h) { return h ? h->n : -1; }
+
+#ifdef D2D_STAMPS
+// diagnostic builds only: K1 writes 8 s_memtime stamps per wave into buf ([n_blocks*4][8] u64)
+int32_t d2d_debug_stamps(d2d_t* h, uint64_t* buf) {
+    if (!h) return fail(D2D_E_ARG, "d2d_debug_stamps: null handle");
+    h->stamps = buf;
+    return D2D_OK;
+}
+#endif
 
 int32_t d2d_set_scenarios(d2d_t* h, const d2d_scn* scns, int32_t n_scn, const int32_t* env_scn_host) {
     if (!h || !scns || n_scn <= 0) return fail(D2D_E_ARG, "d2d_set_scenarios: null handle/scenarios or n_scn <= 0");

@@ -47,7 +47,22 @@ struct StepArgs {
     float* info;
     float* tobs;
     const uint8_t* mask;     // reset kernel only
+    uint64_t* stamps;        // diagnostic builds only (D2D_STAMPS): [waves][8] s_memtime stamps
 };
+
+// Diagnostic phase stamps (separate timing-only build, never in the product): lane 0 of each wave
+// records s_memtime at the phase boundaries of K1.
+#ifdef D2D_STAMPS
+#define STAMP(k)                                                                                       \
+    do {                                                                                               \
+        if (a.stamps && (threadIdx.x & 63) == 0)                                                       \
+            a.stamps[(size_t)(blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define STAMP(k) \
+    do {         \
+    } while (0)
+#endif
 
 template <bool LDS, int NT>
 __device__ __forceinline__ const d2d_scn* stage_scenarios(const StepArgs& a, d2d_scn* lds) {
@@ -97,9 +112,11 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
     const int i = e0 + lane;
     const bool valid = i < a.n;
     const int n = a.n;
+    STAMP(0);
     const d2d_scn* scns = stage_scenarios<LDS, K1_THREADS>(a, s_scn);
     if (wave == 0) sh.scn[lane] = (valid && a.env_scn && a.n_scn > 1) ? a.env_scn[i] : 0;
     __syncthreads();
+    STAMP(1);
     const d2d_scn& S = scns[sh.scn[lane]];
 
     // ---------------------------------------------------------------- phase 1
@@ -180,7 +197,9 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
         sh.sp[6][lane] = sr * DRONE_R + y;
         sh.ep[lane] = ep;
     }
+    STAMP(2);
     __syncthreads();
+    STAMP(3);
 
     // ---------------------------------------------------------------- phase 2
     const int my_cause = sh.cause[lane];
@@ -239,7 +258,9 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
             }
         }
     }
+    STAMP(4);
     __syncthreads();
+    STAMP(5);
 
     // ---------------------------------------------------------------- phase 3
     // obs tile: rows [e0, e0+rows) are one contiguous span of global memory
@@ -311,6 +332,7 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
             fld(a.ist, D2D_I_FLAGS, n, i) = (int32_t)flags;
         }
     }
+    STAMP(6);
 }
 
 // ------------------------------------------------------------------------------------------ K2

@@ -25,3 +25,6 @@ step kt 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/kt"
 step pmc_sq 600 rocprofv3 $KR -T --output-format csv -d "$OUT/pmc_sq" -o sq --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_ANY -- $B --steps 20 --warmup 5
 step pmc_fetch 600 rocprofv3 $KR -T --output-format csv -d "$OUT/pmc_fetch" -o fetch --pmc FETCH_SIZE -- $B --steps 20 --warmup 5
 step pmc_write 600 rocprofv3 $KR -T --output-format csv -d "$OUT/pmc_write" -o write --pmc WRITE_SIZE -- $B --steps 20 --warmup 5
+rocprofv3 -L > "$OUT/counters.txt" 2>&1 || true
+step pmc_clk 600 rocprofv3 $KR -T --output-format csv -d "$OUT/pmc_clk" -o clk --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES -- $B --steps 20 --warmup 5
+step pmc_sq2 600 rocprofv3 $KR -T --output-format csv -d "$OUT/pmc_sq2" -o sq2 --pmc SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 -- $B --steps 20 --warmup 5
