@@ -8,7 +8,8 @@ import subprocess
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG_DIR)
 SRC = os.path.join(PKG_DIR, "csrc", "d2d_hip.hip")
-HDRS = [os.path.join(PKG_DIR, "csrc", "d2d_device.h"), os.path.join(REPO, "include", "drone2d.h")]
+HDRS = [os.path.join(PKG_DIR, "csrc", "d2d_device.h"), os.path.join(PKG_DIR, "csrc", "d2d_kernels.h"),
+        os.path.join(REPO, "include", "drone2d.h")]
 OUT = os.path.join(PKG_DIR, "_lib", "libdrone2d_hip.so")
 
 # -ffp-contract=off: the kernels follow the reference's NumPy evaluation order (explicit fma() only

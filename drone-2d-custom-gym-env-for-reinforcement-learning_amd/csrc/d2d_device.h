@@ -25,6 +25,9 @@
 
 #include "../../include/drone2d.h"
 
+// bool conditions are combined with & / | on purpose (selects instead of short-circuit branches)
+#pragma clang diagnostic ignored "-Wbitwise-instead-of-logical"
+
 // Diagnostic-only ablation mask (tools/ablate.py builds separate timing-only libraries with it;
 // the product is always built with 0): 1 skip Brent, 2 skip sensing, 4 skip joint iterations,
 // 8 skip collision test.
@@ -41,6 +44,29 @@ constexpr double GRAV_Y = -1000.0;            // drone_2d_env.py:185
 constexpr double DRONE_R = 40.0;              // Drone.py:11 (100/2 - 20/2)
 constexpr double FRAME_HX = 50.0, FRAME_HY = 5.0;   // Drone.py:16 box (100, 10)
 constexpr double VEL_MAX = 1330.0;            // drone_2d_env.py:635
+
+// Device-side scenario: the ABI table plus fields derived once in d2d_set_scenarios.
+// us[k >= n_wps] = +inf (unused knots never count in u_index);
+// inv_du[n] = RN(1 / (us[n+1] - us[n])) (only read where the blend case selects it).
+struct Scn : d2d_scn {
+    double inv_du[D2D_MAX_WPS];
+};
+static_assert(sizeof(Scn) == sizeof(d2d_scn) + 8 * D2D_MAX_WPS, "Scn layout");
+__host__ __device__ inline void scn_derive(Scn& s) {
+    for (int k = s.n_wps; k < D2D_MAX_WPS; ++k) s.us[k] = __builtin_inf();
+    for (int k = 0; k < D2D_MAX_WPS; ++k) {
+        const int k1 = (k + 1 < D2D_MAX_WPS) ? k + 1 : D2D_MAX_WPS - 1;
+        s.inv_du[k] = 1.0 / (s.us[k1] - s.us[k]);
+    }
+}
+// a / b correctly rounded from y = RN(1/b) (Markstein): q = RN(a*y) is within 1 ulp of a/b, the
+// residual a - q*b is exact under fma, and RN(q + r*y) == RN(a/b) for normal operands.  Three
+// dependent ops instead of the ~10 of the IEEE division sequence.
+__device__ __forceinline__ double div_by_recip(double a, double b, double y) {
+    const double q = a * y;
+    const double r = fma(-q, b, a);
+    return fma(r, y, q);
+}
 
 // ------------------------------------------------------------------------------ scalar helpers
 // fmod(a, 2*pi), bit-exact, without ocml's fmod loop (239 cycles dependent latency on gfx950 vs
@@ -74,9 +100,10 @@ __device__ __forceinline__ double invm1to1(double v, double lo, double hi) { ret
 __device__ __forceinline__ double clipd(double x, double lo, double hi) { return x < lo ? lo : (x > hi ? hi : x); }
 // np.linalg.norm of a 2-vector == sqrt(OpenBLAS ddot) == sqrt(fma(dy, dy, dx*dx))
 __device__ __forceinline__ double norm2(double dx, double dy) { return sqrt(fma(dy, dy, dx * dx)); }
+// np.sign(x) + (x == 0): 1 for x > 0 and +-0, -1 for x < 0, NaN for NaN (two selects)
 __device__ __forceinline__ double sgn_nz(double x) {
-    double s = (x > 0.0) ? 1.0 : ((x < 0.0) ? -1.0 : (x == 0.0 ? 0.0 : x));
-    return s + (x == 0.0 ? 1.0 : 0.0);
+    const double s = (x < 0.0) ? -1.0 : 1.0;
+    return (x != x) ? x : s;
 }
 __device__ __forceinline__ void sincos_d(double x, double& s, double& c) { sincos(x, &s, &c); }
 
@@ -98,7 +125,7 @@ __device__ __forceinline__ double u53(uint32_t a, uint32_t b) {
     return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * (1.0 / 9007199254740992.0);
 }
 // test-mode spawn draw (drone_2d_env.py:229-232): x, y, theta for (seed, global env id, episode)
-__device__ __forceinline__ void spawn_draw(const d2d_scn& s, uint64_t seed, uint32_t gid, uint32_t episode,
+__device__ __forceinline__ void spawn_draw(const Scn& s, uint64_t seed, uint32_t gid, uint32_t episode,
                                            double& x, double& y, double& th) {
     uint32_t o[4];
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
@@ -114,20 +141,42 @@ __device__ __forceinline__ void spawn_draw(const d2d_scn& s, uint64_t seed, uint
 // ------------------------------------------------------------------------------ QPMI2D path
 // get_u_index (predef_path.py:53-63): first n with u <= us[n+1]; for non-decreasing knots this is
 // the number of knots k >= 1 with !(u <= us[k]) (NaN -> n_wps-1, as the Python loop).
-__device__ __forceinline__ int u_index(const d2d_scn& s, double u) {
+// The device table pads us[k >= n_wps] with +inf (scn_derive), so those knots never count for a
+// non-NaN u; the min() maps NaN (every comparison false) to n_wps - 1 as the Python loop does.
+// `kmax` is a wave-uniform bound on n_wps (the loop stops early when all lanes share a scenario).
+__device__ __forceinline__ int u_index(const Scn& s, double u, int kmax) {
     int n = 0;
 #pragma unroll
-    for (int k = 1; k < D2D_MAX_WPS; ++k) n += (k < s.n_wps && !(u <= s.us[k])) ? 1 : 0;
-    return n;
+    for (int k = 1; k < D2D_MAX_WPS; ++k) {
+        if (k < kmax) n += !(u <= s.us[k]) ? 1 : 0;
+    }
+    return min(n, s.n_wps - 1);
+}
+__device__ __forceinline__ int u_index(const Scn& s, double u) { return u_index(s, u, D2D_MAX_WPS); }
+// wave-uniform upper bound on the knot count of the active lanes' scenarios
+__device__ __forceinline__ int wave_knots(const Scn& s) {
+    const int nw = s.n_wps;
+    const int f = __builtin_amdgcn_readfirstlane(nw);
+    return (__ballot(nw != f) == 0) ? f : D2D_MAX_WPS;
+}
+// loop invariants of path_eval (hoisted out of the Brent loop)
+struct PathK {
+    double us0, us1, last_lo, L;
+    int nw, kmax;
+};
+__device__ __forceinline__ PathK path_k(const Scn& s) {
+    const int nw = s.n_wps;
+    return PathK{s.us[0], s.us[1], s.us[nw - 2] - 0.001, s.us[nw - 1], nw, wave_knots(s)};
 }
 // QPMI2D.__call__ (predef_path.py:88-142), branch-free: both candidate quadratics are evaluated
 // and the reference's case analysis picks the result with selects (same arithmetic per case).
-__device__ __forceinline__ void path_eval(const d2d_scn& s, double u, double& x, double& y) {
-    const int nw = s.n_wps, nseg = nw - 2;
-    const int n = u_index(s, u);
-    const bool first = (u >= s.us[0] && u <= s.us[1]);
-    const bool last = !first && ((u >= s.us[nw - 2] - 0.001 && u <= s.us[nw - 1]) || n == nw - 1);
-    const bool blend = !first && !last;
+// Conditions combine with non-short-circuit & / | so the compiler emits selects, not branches.
+__device__ __forceinline__ void path_eval(const Scn& s, const PathK& K, double u, double& x, double& y) {
+    const int nw = K.nw, nseg = nw - 2;
+    const int n = u_index(s, u, K.kmax);
+    const bool first = (u >= K.us0) & (u <= K.us1);
+    const bool last = !first & (((u >= K.last_lo) & (u <= K.L)) | (n == nw - 1));
+    const bool blend = !first & !last;
     const int kb = first ? 0 : (last ? nseg - 1 : n);
     const int ka = (n == 0) ? nseg - 1 : n - 1;  // python x_params[n-1]
     const int n1 = (n + 1 < D2D_MAX_WPS) ? n + 1 : D2D_MAX_WPS - 1;
@@ -138,74 +187,101 @@ __device__ __forceinline__ void path_eval(const d2d_scn& s, double u, double& x,
     const int kas = blend ? ka : kb;
     const double xA = s.xa[kas] * uu + s.xb[kas] * u + s.xc[kas];
     const double yA = s.ya[kas] * uu + s.yb[kas] * u + s.yc[kas];
-    const double mu_r = (u - u0) / (u1 - u0);
-    const double mu_f = (u1 - u) / (u1 - u0);
+    const double du = u1 - u0, idu = s.inv_du[n];
+    const double mu_r = div_by_recip(u - u0, du, idu);   // (u - u0) / (u1 - u0)
+    const double mu_f = div_by_recip(u1 - u, du, idu);   // (u1 - u) / (u1 - u0)
     x = blend ? mu_r * xB + mu_f * xA : xB;
     y = blend ? mu_r * yB + mu_f * yA : yB;
 }
-__device__ __forceinline__ double path_dist(const d2d_scn& s, double u, double px, double py) {
+__device__ __forceinline__ void path_eval(const Scn& s, double u, double& x, double& y) {
+    path_eval(s, path_k(s), u, x, y);
+}
+__device__ __forceinline__ double path_dist(const Scn& s, const PathK& K, double u, double px, double py) {
     double x, y;
-    path_eval(s, u, x, y);
+    path_eval(s, K, u, x, y);
     return norm2(x - px, y - py);
 }
 // get_closest_u (predef_path.py:226-248) = scipy fminbound(x1=-10, x2=L+10, xtol=1e-6, maxfun=500),
 // restated from scipy 1.15.3 _minimize_scalar_bounded (_optimize.py:2251-2398) probe for probe; the
 // golden/parabolic case analysis is evaluated with selects (identical arithmetic per case).
-__device__ __forceinline__ double closest_u(const d2d_scn& s, double px, double py) {
-    const double sqrt_eps = 1.4832396974191326e-08;   // sqrt(2.2e-16)
-    const double golden_mean = 0.3819660112501051;    // 0.5*(3.0 - sqrt(5.0))
-    const double xatol3 = 1e-6 / 3.0;
-    double a = 0.0 - 10.0, b = s.us[s.n_wps - 1] + 10.0;
-    double fulc = a + golden_mean * (b - a);
-    double nfc = fulc, xf = fulc;
-    double rat = 0.0, e = 0.0;
-    double fx = path_dist(s, xf, px, py);
-    int num = 1;
-    double ffulc = fx, fnfc = fx;
-    double xm = 0.5 * (a + b);
-    double tol1 = sqrt_eps * fabs(xf) + xatol3;
-    double tol2 = 2.0 * tol1;
-    while (fabs(xf - xm) > (tol2 - 0.5 * (b - a))) {
-        // parabolic candidate (used only when |e| > tol1 and it is acceptable)
-        const double r = (xf - nfc) * (fx - ffulc);
-        double q = (xf - fulc) * (fx - fnfc);
-        double p = (xf - fulc) * q - (xf - nfc) * r;
-        q = 2.0 * (q - r);
-        p = (q > 0.0) ? -p : p;
-        q = fabs(q);
-        const bool par = (fabs(e) > tol1) && (fabs(p) < fabs(0.5 * q * e)) && (p > q * (a - xf)) &&
-                         (p < q * (b - xf));
-        double rat_p = (p + 0.0) / q;
-        const double xp = xf + rat_p;
-        rat_p = (((xp - a) < tol2) || ((b - xp) < tol2)) ? tol1 * sgn_nz(xm - xf) : rat_p;
-        // golden-section candidate
-        const double e_g = (xf >= xm) ? a - xf : b - xf;
-        const double rat_g = golden_mean * e_g;
-        e = par ? rat : e_g;
-        rat = par ? rat_p : rat_g;
-        const double ar = fabs(rat);
-        const double mx = (ar != ar) ? ar : (ar > tol1 ? ar : tol1);
-        const double x = xf + sgn_nz(rat) * mx;
-        const double fu = path_dist(s, x, px, py);
-        num += 1;
-        const bool le = fu <= fx;
-        const bool c1 = !le && ((fu <= fnfc) || (nfc == xf));
-        const bool c2 = !le && !c1 && ((fu <= ffulc) || (fulc == xf) || (fulc == nfc));
-        const double na = le ? ((x >= xf) ? xf : a) : ((x < xf) ? x : a);
-        const double nb = le ? ((x >= xf) ? b : xf) : ((x < xf) ? b : x);
-        const double nfulc = (le || c1) ? nfc : (c2 ? x : fulc);
-        const double nffulc = (le || c1) ? fnfc : (c2 ? fu : ffulc);
-        const double nnfc = le ? xf : (c1 ? x : nfc);
-        const double nfnfc = le ? fx : (c1 ? fu : fnfc);
-        xf = le ? x : xf;
-        fx = le ? fu : fx;
-        a = na; b = nb; fulc = nfulc; ffulc = nffulc; nfc = nnfc; fnfc = nfnfc;
-        xm = 0.5 * (a + b);
-        tol1 = sqrt_eps * fabs(xf) + xatol3;
-        tol2 = 2.0 * tol1;
-        if (num >= 500) break;
-    }
-    return xf;
+// The search state is explicit so that a search can be suspended and resumed bit-exactly (the
+// auto-reset observation cache runs it in slices across steps); xm / tol1 / tol2 are functions of
+// the state, recomputed exactly as scipy recomputes them at the end of each iteration.
+struct Brent {
+    double a, b, fulc, ffulc, nfc, fnfc, xf, fx, rat, e;
+    int num;
+};
+constexpr double BR_SQRT_EPS = 1.4832396974191326e-08;  // sqrt(2.2e-16)
+constexpr double BR_GOLDEN = 0.3819660112501051;        // 0.5*(3.0 - sqrt(5.0))
+constexpr double BR_XATOL3 = 1e-6 / 3.0;
+__device__ __forceinline__ void brent_init(const Scn& s, const PathK& K, double px, double py, Brent& B) {
+    B.a = 0.0 - 10.0;
+    B.b = K.L + 10.0;
+    B.fulc = B.a + BR_GOLDEN * (B.b - B.a);
+    B.nfc = B.fulc;
+    B.xf = B.fulc;
+    B.rat = 0.0;
+    B.e = 0.0;
+    B.fx = path_dist(s, K, B.xf, px, py);
+    B.num = 1;
+    B.ffulc = B.fx;
+    B.fnfc = B.fx;
+}
+__device__ __forceinline__ bool brent_active(const Brent& B) {
+    const double xm = 0.5 * (B.a + B.b);
+    const double tol1 = BR_SQRT_EPS * fabs(B.xf) + BR_XATOL3;
+    const double tol2 = 2.0 * tol1;
+    return (fabs(B.xf - xm) > (tol2 - 0.5 * (B.b - B.a))) & (B.num < 500);
+}
+__device__ __forceinline__ void brent_step(const Scn& s, const PathK& K, double px, double py, Brent& B) {
+    const double a = B.a, b = B.b, xf = B.xf, fx = B.fx, nfc = B.nfc, fulc = B.fulc;
+    const double xm = 0.5 * (a + b);
+    const double tol1 = BR_SQRT_EPS * fabs(xf) + BR_XATOL3;
+    const double tol2 = 2.0 * tol1;
+    // parabolic candidate (used only when |e| > tol1 and it is acceptable)
+    const double r = (xf - nfc) * (fx - B.ffulc);
+    double q = (xf - fulc) * (fx - B.fnfc);
+    double p = (xf - fulc) * q - (xf - nfc) * r;
+    q = 2.0 * (q - r);
+    p = (q > 0.0) ? -p : p;
+    q = fabs(q);
+    const bool par = (fabs(B.e) > tol1) & (fabs(p) < fabs(0.5 * q * B.e)) & (p > q * (a - xf)) & (p < q * (b - xf));
+    double rat_p = (p + 0.0) / q;
+    const double xp = xf + rat_p;
+    rat_p = (((xp - a) < tol2) | ((b - xp) < tol2)) ? tol1 * sgn_nz(xm - xf) : rat_p;
+    // golden-section candidate
+    const double e_g = (xf >= xm) ? a - xf : b - xf;
+    const double rat_g = BR_GOLDEN * e_g;
+    B.e = par ? B.rat : e_g;
+    const double rat = par ? rat_p : rat_g;
+    B.rat = rat;
+    const double ar = fabs(rat);
+    const double mx = (ar != ar) ? ar : (ar > tol1 ? ar : tol1);
+    const double x = xf + sgn_nz(rat) * mx;
+    const double fu = path_dist(s, K, x, px, py);
+    B.num += 1;
+    const bool le = fu <= fx;
+    const bool c1 = !le & ((fu <= B.fnfc) | (nfc == xf));
+    const bool c2 = !le & !c1 & ((fu <= B.ffulc) | (fulc == xf) | (fulc == nfc));
+    B.a = le ? ((x >= xf) ? xf : a) : ((x < xf) ? x : a);
+    B.b = le ? ((x >= xf) ? b : xf) : ((x < xf) ? b : x);
+    const double nfulc = (le | c1) ? nfc : (c2 ? x : fulc);
+    const double nffulc = (le | c1) ? B.fnfc : (c2 ? fu : B.ffulc);
+    const double nnfc = le ? xf : (c1 ? x : nfc);
+    const double nfnfc = le ? fx : (c1 ? fu : B.fnfc);
+    B.fulc = nfulc;
+    B.ffulc = nffulc;
+    B.nfc = nnfc;
+    B.fnfc = nfnfc;
+    B.xf = le ? x : xf;
+    B.fx = le ? fu : fx;
+}
+__device__ __forceinline__ double closest_u(const Scn& s, double px, double py) {
+    const PathK K = path_k(s);
+    Brent B;
+    brent_init(s, K, px, py, B);
+    while (brent_active(B)) brent_step(s, K, px, py, B);
+    return B.xf;
 }
 
 // ------------------------------------------------------------------------------ bodies / physics
@@ -217,7 +293,7 @@ __device__ __forceinline__ double closest_u(const d2d_scn& s, double px, double 
 //                    impulses (dt_coef = 1; after a reset jAcc = 0 so dt_coef = 0 is identical),
 //                    10 Gauss-Seidel sweeps over the joints in space.add order.
 // With JBUF = true the per-joint (K^-1, bias) live in a per-lane LDS buffer (`jb[f * stride]`,
-// 36 doubles) and are re-read every sweep (volatile): that keeps the sweep at ~90 VGPRs.
+// 6 x JB_PER_JOINT doubles) and are re-read every sweep (volatile): that keeps the sweep at ~90 VGPRs.
 struct Body {
     double px, py, a, vx, vy, w;
 };
@@ -262,7 +338,24 @@ __device__ __forceinline__ void arm(const Arms& A, int k, double& r1x, double& r
     r2y = (k < 3) ? -s : s;
 }
 
-__device__ __forceinline__ bool phys_positions(const d2d_scn& s, Body B[3], double fL, double fR, double cs[3],
+__device__ __forceinline__ void advance_position(Body& b) {
+    b.px = b.px + (b.vx + 0.0) * DT;
+    b.py = b.py + (b.vy + 0.0) * DT;
+    b.a = b.a + (b.w + 0.0) * DT;
+}
+__device__ __forceinline__ bool frame_hits(const Scn& s, const Body& F, double cs, double sn) {
+    bool hit = false;
+    for (int k = 0; k < ((D2D_ABLATE & 8) ? 0 : s.n_circles); ++k) {
+        const double dx = s.cx[k] - F.px, dy = s.cy[k] - F.py;
+        const double lx = dx * cs + dy * sn;
+        const double ly = -dx * sn + dy * cs;
+        const double ex = lx - clipd(lx, -FRAME_HX, FRAME_HX), ey = ly - clipd(ly, -FRAME_HY, FRAME_HY);
+        const double r = s.cr[k];
+        hit |= (ex * ex + ey * ey <= r * r);
+    }
+    return hit;
+}
+__device__ __forceinline__ bool phys_positions(const Scn& s, Body B[3], double fL, double fR, double cs[3],
                                                double sn[3], double& fx, double& fy, double& tq) {
     // forces on the frame at local (-40,0) then (40,0): cpBodyApplyForceAtLocalPoint
     double c0, s0;
@@ -286,22 +379,19 @@ __device__ __forceinline__ bool phys_positions(const d2d_scn& s, Body B[3], doub
     // 1. cpBodyUpdatePosition (v_bias = 0)
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-        B[i].px = B[i].px + (B[i].vx + 0.0) * DT;
-        B[i].py = B[i].py + (B[i].vy + 0.0) * DT;
-        B[i].a = B[i].a + (B[i].w + 0.0) * DT;
+        advance_position(B[i]);
         sincos_d(B[i].a, sn[i], cs[i]);
     }
     // 2. collision: CircleToPoly(circle, frame box) contact iff dist(center, box) <= r
-    bool hit = false;
-    for (int k = 0; k < ((D2D_ABLATE & 8) ? 0 : s.n_circles); ++k) {
-        const double dx = s.cx[k] - B[0].px, dy = s.cy[k] - B[0].py;
-        const double lx = dx * cs[0] + dy * sn[0];
-        const double ly = -dx * sn[0] + dy * cs[0];
-        const double ex = lx - clipd(lx, -FRAME_HX, FRAME_HX), ey = ly - clipd(ly, -FRAME_HY, FRAME_HY);
-        const double r = s.cr[k];
-        hit |= (ex * ex + ey * ey <= r * r);
-    }
-    return hit;
+    return frame_hits(s, B[0], cs[0], sn[0]);
+}
+// The frame's post-step position and contact flag from its pre-step state alone (forces only act
+// on velocities): lets the observation waves start without waiting for the physics wave.
+__device__ __forceinline__ bool frame_advance(const Scn& s, Body& F) {
+    advance_position(F);
+    double sn, cs;
+    sincos_d(F.a, sn, cs);
+    return frame_hits(s, F, cs, sn);
 }
 
 __device__ __forceinline__ Arms make_arms(const double cs[3], const double sn[3]) {
@@ -316,12 +406,13 @@ __device__ __forceinline__ Arms make_arms(const double cs[3], const double sn[3]
 
 // stage 2.  pos = {frame px, py, left px, py, right px, py} (post position update); vel[9] =
 // (vx, vy, w) of frame, left, right; j[12] the accumulated pivot impulses.
+constexpr int JB_PER_JOINT = 5;  // K^-1 (a, b = c, d) + bias (x, y)
 template <bool JBUF>
 __device__ __forceinline__ void phys_velocities(const Arms& A, const double pos[6], double damping_dt, double fx,
                                                 double fy, double tq, double vel[9], double j[12], double* jb,
                                                 int stride) {
     const double bias_coef = -(1.0 - 0.0) / DT;  // error_bias = 0 -> bias_coef(0, dt) = 1 - 0^dt = 1
-    double kk[JBUF ? 1 : 6][6];
+    double kk[JBUF ? 1 : 6][5];
     // preStep
 #pragma unroll
     for (int k = 0; k < 6; ++k) {
@@ -340,11 +431,12 @@ __device__ __forceinline__ void phys_velocities(const Arms& A, const double pos[
         const double det_inv = 1.0 / det;
         const double dx = (pos[0] + r2x) - (pos[2 * m] + r1x);
         const double dy = (pos[1] + r2y) - (pos[2 * m + 1] + r1y);
-        const double v[6] = {k22 * det_inv, -k12 * det_inv, -k21 * det_inv, k11 * det_inv, dx * bias_coef,
-                             dy * bias_coef};
+        // K^-1 = [[k22, -k12], [-k21, k11]] * det_inv; k12 and k21 are the same sums, so the two
+        // off-diagonal entries are bitwise equal and one is kept
+        const double v[5] = {k22 * det_inv, -k12 * det_inv, k11 * det_inv, dx * bias_coef, dy * bias_coef};
 #pragma unroll
-        for (int q = 0; q < 6; ++q) {
-            if (JBUF) jb[(6 * k + q) * stride] = v[q];
+        for (int q = 0; q < 5; ++q) {
+            if (JBUF) jb[(JB_PER_JOINT * k + q) * stride] = v[q];
             else kk[JBUF ? 0 : k][q] = v[q];
         }
     }
@@ -380,19 +472,20 @@ __device__ __forceinline__ void phys_velocities(const Arms& A, const double pos[
             const int m = k < 3 ? 1 : 2;
             double r1x, r1y, r2x, r2y;
             arm(A, k, r1x, r1y, r2x, r2y);
-            double ka, kb, kc, kd, bx, by;
+            double ka, kb, kd, bx, by;
             if (JBUF) {
                 // an explicit LDS (address_space 3) pointer: generic volatile loads would become flat
                 // loads with one 64-bit address per slot
                 using LdsD = __attribute__((address_space(3))) double;
                 const volatile LdsD* kv = (const volatile LdsD*)jb;
-                ka = kv[(6 * k + 0) * stride]; kb = kv[(6 * k + 1) * stride];
-                kc = kv[(6 * k + 2) * stride]; kd = kv[(6 * k + 3) * stride];
-                bx = kv[(6 * k + 4) * stride]; by = kv[(6 * k + 5) * stride];
+                ka = kv[(JB_PER_JOINT * k + 0) * stride]; kb = kv[(JB_PER_JOINT * k + 1) * stride];
+                kd = kv[(JB_PER_JOINT * k + 2) * stride];
+                bx = kv[(JB_PER_JOINT * k + 3) * stride]; by = kv[(JB_PER_JOINT * k + 4) * stride];
             } else {
                 const int kq = JBUF ? 0 : k;
-                ka = kk[kq][0]; kb = kk[kq][1]; kc = kk[kq][2]; kd = kk[kq][3]; bx = kk[kq][4]; by = kk[kq][5];
+                ka = kk[kq][0]; kb = kk[kq][1]; kd = kk[kq][2]; bx = kk[kq][3]; by = kk[kq][4];
             }
+            const double kc = kb;
             const double v1x = vel[3 * m + 0] + (-r1y) * vel[3 * m + 2], v1y = vel[3 * m + 1] + r1x * vel[3 * m + 2];
             const double v2x = vel[0] + (-r2y) * vel[2], v2y = vel[1] + r2x * vel[2];
             const double ux = bx - (v2x - v1x), uy = by - (v2y - v1y);
@@ -415,7 +508,7 @@ __device__ __forceinline__ void phys_velocities(const Arms& A, const double pos[
 }
 
 // whole step, registers only (reference / diagnostics)
-__device__ __forceinline__ bool space_step(const d2d_scn& s, double damping_dt, Body B[3], double j[12], double fL,
+__device__ __forceinline__ bool space_step(const Scn& s, double damping_dt, Body B[3], double j[12], double fL,
                                            double fR) {
     double cs[3], sn[3], fx, fy, tq;
     const bool hit = phys_positions(s, B, fL, fR, cs, sn, fx, fy, tq);
@@ -436,12 +529,18 @@ __device__ __forceinline__ bool space_step(const d2d_scn& s, double damping_dt, 
 // sensor role: obs[0..18] of get_observation (drone_2d_env.py:633-727) for frame state F.
 // k = 3 nearest circles by min over the UNROTATED frame vertices (+-50, +-5) of |v+p-c| - r;
 // sqrt is monotone and correctly rounded, so sqrt(min d^2) - r == min(sqrt(d^2) - r) bitwise.
-__device__ __forceinline__ void sensor_obs(const d2d_cfg& cfg, const d2d_scn& s, const Body& F, double o[19]) {
-    const double W = cfg.screen_w, H = cfg.screen_h;
-    const double x = F.px, y = F.py, al = F.a;
+// Split in the velocity-dependent entries (0, 1, 2, 17, 18: need the joint sweep's output) and the
+// position-dependent ones (3..16: known right after the position update).
+__device__ __forceinline__ void sensor_vel(const Body& F, double o[19]) {
     o[0] = m1to1(F.vx, -VEL_MAX, VEL_MAX);
     o[1] = m1to1(F.vy, -VEL_MAX, VEL_MAX);
     o[2] = clipd(F.w / 11.7, -1.0, 1.0);
+    const double vab = ssa(atan2(F.vy, F.vx) - F.a);
+    sincos_d(vab, o[17], o[18]);
+}
+__device__ __forceinline__ void sensor_pos(const d2d_cfg& cfg, const Scn& s, double x, double y, double al,
+                                           double o[19]) {
+    const double W = cfg.screen_w, H = cfg.screen_h;
     o[3] = al / PI;
     o[4] = m1to1(s.wp_last_x - x, 0.0, W);
     o[5] = m1to1(s.wp_last_y - y, 0.0, H);
@@ -485,17 +584,19 @@ __device__ __forceinline__ void sensor_obs(const d2d_cfg& cfg, const d2d_scn& s,
         o[9 + 3 * jj] = have ? sa : 0.0;
         o[10 + 3 * jj] = have ? ca : 0.0;
     }
-    const double vab = ssa(atan2(F.vy, F.vx) - al);
-    sincos_d(vab, o[17], o[18]);
+}
+__device__ __forceinline__ void sensor_obs(const d2d_cfg& cfg, const Scn& s, const Body& F, double o[19]) {
+    sensor_vel(F, o);
+    sensor_pos(cfg, s, F.px, F.py, F.a, o);
 }
 
 // path role: obs[19..26] (drone_2d_env.py:729-763).  get_closest_u is evaluated once (the
 // reference calls it twice with identical input, predef_path.py:255 and :261).  Updates the
 // sticky LA lock in `flags`; returns the closest point (cpx, cpy) for the path-adherence reward.
-__device__ __forceinline__ void path_obs(const d2d_cfg& cfg, const d2d_scn& s, double x, double y, double al,
-                                         uint32_t& flags, double o[8]) {
+// the part after the closest-point search, for a given u
+__device__ __forceinline__ void path_obs_u(const d2d_cfg& cfg, const Scn& s, double x, double y, double al,
+                                           double u, uint32_t& flags, double o[8]) {
     const double W = cfg.screen_w, H = cfg.screen_h;
-    const double u = (D2D_ABLATE & 1) ? clipd(x - 100.0, -10.0, s.us[s.n_wps - 1]) : closest_u(s, x, y);
     double cpx, cpy;
     path_eval(s, u, cpx, cpy);
     const double L = s.us[s.n_wps - 1];
@@ -523,13 +624,18 @@ __device__ __forceinline__ void path_obs(const d2d_cfg& cfg, const d2d_scn& s, d
     sincos_d(laa, o[4], o[5]);
     sincos_d(cpa, o[6], o[7]);
 }
+__device__ __forceinline__ void path_obs(const d2d_cfg& cfg, const Scn& s, double x, double y, double al,
+                                         uint32_t& flags, double o[8]) {
+    const double u = (D2D_ABLATE & 1) ? clipd(x - 100.0, -10.0, s.us[s.n_wps - 1]) : closest_u(s, x, y);
+    path_obs_u(cfg, s, x, y, al, u, flags, o);
+}
 
 // ------------------------------------------------------------------------------ reward
 // The reward decodes from the fp64 observation exactly as the reference does (drone_2d_env.py:423-572).
 struct CAPart {  // computed by the sensor role (obs 0..18 only)
     double vel_ang, ca, lpa, lca, dclose;
 };
-__device__ __forceinline__ CAPart reward_ca_part(const d2d_cfg& cfg, const d2d_scn& s, const double* o) {
+__device__ __forceinline__ CAPart reward_ca_part(const d2d_cfg& cfg, const Scn& s, const double* o) {
     const double W = cfg.screen_w, H = cfg.screen_h;
     CAPart P;
     P.vel_ang = pymod_2pi(atan2(o[17] * PI, o[18] * PI) + TWO_PI);
@@ -562,7 +668,7 @@ __device__ __forceinline__ CAPart reward_ca_part(const d2d_cfg& cfg, const d2d_s
 // end conditions that need only the post-physics frame (drone_2d_env.py:543-571): collision,
 // reach-end (decoded target distance), AA (decoded alpha), time-up.  Known before the observation,
 // which lets the cooperative kernel start the auto-reset observation concurrently.
-__device__ __forceinline__ int end_cause(const d2d_cfg& cfg, const d2d_scn& s, const Body& F, bool collided, int t) {
+__device__ __forceinline__ int end_cause(const d2d_cfg& cfg, const Scn& s, const Body& F, bool collided, int t) {
     const double W = cfg.screen_w, H = cfg.screen_h;
     const double tdx = invm1to1(m1to1(s.wp_last_x - F.px, 0.0, W), 0.0, W);
     const double tdy = invm1to1(m1to1(s.wp_last_y - F.py, 0.0, H), 0.0, H);
@@ -615,7 +721,7 @@ __device__ __forceinline__ Reward reward_final(const d2d_cfg& cfg, const Body& F
 }
 
 // full single-lane observation (reset kernel)
-__device__ __forceinline__ void observe(const d2d_cfg& cfg, const d2d_scn& s, const Body& F, uint32_t& flags,
+__device__ __forceinline__ void observe(const d2d_cfg& cfg, const Scn& s, const Body& F, uint32_t& flags,
                                         double obs[D2D_OBS_DIM]) {
     sensor_obs(cfg, s, F, obs);
     path_obs(cfg, s, F.px, F.py, F.a, flags, obs + 19);

@@ -8,6 +8,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <vector>
 
 #include "d2d_kernels.h"
 
@@ -34,11 +35,15 @@ struct d2d_handle {
     double* st = nullptr;
     int32_t* ist = nullptr;
     double* acc = nullptr;
-    d2d_scn* scn = nullptr;
+    d2d::Scn* scn = nullptr;    // device table: ABI scenarios + derived fields
     int32_t* env_scn = nullptr;
     uint64_t seed = 0;
     bool reset_done = false;
     uint64_t* stamps = nullptr;  // diagnostic builds (D2D_STAMPS) only
+    // auto-reset observation cache (d2d_kernels.h, "Auto-reset observation cache")
+    double* rc_bs = nullptr;     // [RC_NB][n]
+    int32_t* rc_i = nullptr;     // [RC_NI][n]
+    float* rc_obs = nullptr;     // [n][27]
 };
 
 namespace {
@@ -56,7 +61,15 @@ StepArgs make_args(const d2d_t* h) {
     a.damping_dt = std::pow(h->cfg.damping, 1.0 / 60.0);
     a.seed = h->seed;
     a.stamps = h->stamps;
+    a.rc_bs = h->rc_bs;
+    a.rc_i = h->rc_i;
+    a.rc_obs = h->rc_obs;
     return a;
+}
+
+// every cache entry invalid (status rows RC_PST, RC_SST = 0), ordered on `stream`
+hipError_t rc_invalidate(d2d_t* h, hipStream_t stream) {
+    return hipMemsetAsync(h->rc_i, 0, sizeof(int32_t) * 2 * (size_t)h->n, stream);
 }
 
 struct DeviceGuard {
@@ -94,7 +107,10 @@ int32_t d2d_create(const d2d_cfg* cfg, int32_t n_envs, int32_t device, d2d_t** o
     if ((e = hipMalloc(&h->st, sizeof(double) * D2D_NSTATE * n)) != hipSuccess ||
         (e = hipMalloc(&h->ist, sizeof(int32_t) * D2D_NISTATE * n)) != hipSuccess ||
         (e = hipMalloc(&h->acc, sizeof(double) * D2D_NSTATS * n)) != hipSuccess ||
-        (e = hipMalloc(&h->env_scn, sizeof(int32_t) * n)) != hipSuccess) {
+        (e = hipMalloc(&h->env_scn, sizeof(int32_t) * n)) != hipSuccess ||
+        (e = hipMalloc(&h->rc_bs, sizeof(double) * RC_NB * n)) != hipSuccess ||
+        (e = hipMalloc(&h->rc_i, sizeof(int32_t) * RC_NI * n)) != hipSuccess ||
+        (e = hipMalloc(&h->rc_obs, sizeof(float) * D2D_OBS_DIM * n)) != hipSuccess) {
         d2d_destroy(h);
         return hip_fail(e, "d2d_create: hipMalloc");
     }
@@ -102,6 +118,7 @@ int32_t d2d_create(const d2d_cfg* cfg, int32_t n_envs, int32_t device, d2d_t** o
     (void)hipMemset(h->ist, 0, sizeof(int32_t) * D2D_NISTATE * n);
     (void)hipMemset(h->acc, 0, sizeof(double) * D2D_NSTATS * n);
     (void)hipMemset(h->env_scn, 0, sizeof(int32_t) * n);
+    (void)hipMemset(h->rc_i, 0, sizeof(int32_t) * RC_NI * n);
     if ((e = hipDeviceSynchronize()) != hipSuccess) {
         d2d_destroy(h);
         return hip_fail(e, "d2d_create: memset");
@@ -118,6 +135,9 @@ void d2d_destroy(d2d_t* h) {
     if (h->acc) (void)hipFree(h->acc);
     if (h->scn) (void)hipFree(h->scn);
     if (h->env_scn) (void)hipFree(h->env_scn);
+    if (h->rc_bs) (void)hipFree(h->rc_bs);
+    if (h->rc_i) (void)hipFree(h->rc_i);
+    if (h->rc_obs) (void)hipFree(h->rc_obs);
     delete h;
 }
 
@@ -152,8 +172,14 @@ int32_t d2d_set_scenarios(d2d_t* h, const d2d_scn* scns, int32_t n_scn, const in
         (void)hipFree(h->scn);
         h->scn = nullptr;
     }
-    if ((e = hipMalloc(&h->scn, sizeof(d2d_scn) * (size_t)n_scn)) != hipSuccess) return hip_fail(e, "hipMalloc scn");
-    if ((e = hipMemcpy(h->scn, scns, sizeof(d2d_scn) * (size_t)n_scn, hipMemcpyHostToDevice)) != hipSuccess)
+    std::vector<d2d::Scn> tab((size_t)n_scn);
+    for (int k = 0; k < n_scn; ++k) {
+        static_cast<d2d_scn&>(tab[k]) = scns[k];
+        d2d::scn_derive(tab[k]);
+    }
+    const size_t bytes = sizeof(d2d::Scn) * (size_t)n_scn;
+    if ((e = hipMalloc(&h->scn, bytes)) != hipSuccess) return hip_fail(e, "hipMalloc scn");
+    if ((e = hipMemcpy(h->scn, tab.data(), bytes, hipMemcpyHostToDevice)) != hipSuccess)
         return hip_fail(e, "hipMemcpy scn");
     if (env_scn_host) {
         if ((e = hipMemcpy(h->env_scn, env_scn_host, sizeof(int32_t) * (size_t)h->n, hipMemcpyHostToDevice)) !=
@@ -171,15 +197,18 @@ int32_t d2d_reset(d2d_t* h, const uint8_t* mask_dev, uint64_t seed, float* obs_d
     if (h->n_scn <= 0) return fail(D2D_E_STATE, "d2d_reset: call d2d_set_scenarios first");
     DeviceGuard g(h->device);
     h->seed = seed;
+    // cached next-reset observations depend on the seed and the episode counters: drop them all
+    hipError_t e = rc_invalidate(h, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "d2d_reset: cache invalidate");
     StepArgs a = make_args(h);
     a.obs = obs_dev;
     a.mask = mask_dev;
     const dim3 grid((h->n + BLOCK - 1) / BLOCK);
     if (h->n_scn <= MAX_LDS_SCN)
-        hipLaunchKernelGGL(d2d_reset_kernel<true>, grid, dim3(BLOCK), sizeof(d2d_scn) * h->n_scn, (hipStream_t)stream, a);
+        hipLaunchKernelGGL(d2d_reset_kernel<true>, grid, dim3(BLOCK), sizeof(d2d::Scn) * h->n_scn, (hipStream_t)stream, a);
     else
         hipLaunchKernelGGL(d2d_reset_kernel<false>, grid, dim3(BLOCK), 0, (hipStream_t)stream, a);
-    hipError_t e = hipGetLastError();
+    e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "d2d_reset launch");
     h->reset_done = true;
     return D2D_OK;
@@ -202,7 +231,7 @@ int32_t d2d_step(d2d_t* h, const float* act_dev, float* obs_dev, float* rew_dev,
     a.tobs = term_obs_dev;
     const dim3 grid((h->n + EPB - 1) / EPB);
     if (h->n_scn <= MAX_LDS_SCN)
-        hipLaunchKernelGGL(d2d_step_kernel<true>, grid, dim3(K1_THREADS), sizeof(d2d_scn) * h->n_scn, (hipStream_t)stream, a);
+        hipLaunchKernelGGL(d2d_step_kernel<true>, grid, dim3(K1_THREADS), sizeof(d2d::Scn) * h->n_scn, (hipStream_t)stream, a);
     else
         hipLaunchKernelGGL(d2d_step_kernel<false>, grid, dim3(K1_THREADS), 0, (hipStream_t)stream, a);
     hipError_t e = hipGetLastError();
@@ -239,6 +268,7 @@ int32_t d2d_set_state(d2d_t* h, const double* state_dev, const int32_t* istate_d
         (e = hipMemcpyAsync(h->ist, istate_dev, sizeof(int32_t) * D2D_NISTATE * n, hipMemcpyDeviceToDevice,
                             (hipStream_t)stream)) != hipSuccess)
         return hip_fail(e, "d2d_set_state");
+    if ((e = rc_invalidate(h, (hipStream_t)stream)) != hipSuccess) return hip_fail(e, "d2d_set_state: cache invalidate");
     h->reset_done = true;
     return D2D_OK;
 }

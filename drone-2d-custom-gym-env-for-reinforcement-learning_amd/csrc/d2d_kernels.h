@@ -2,19 +2,24 @@
 //
 // K1 d2d_step_kernel (cooperative, wave-specialised).  One 256-lane workgroup owns 64 envs (one
 // per lane index); its four waves split one env step by role so that the long, independent fp64
-// latency chains run concurrently instead of back to back:
+// latency chains run concurrently instead of back to back.  The frame's post-step position depends
+// only on its pre-step position and velocity (forces act on velocities), so every wave derives it
+// from the state in HBM and no wave waits for another before its own chain:
 //
-//   phase 1  W0: load state, thrust, Chipmunk-equivalent 3-body/6-pivot step, collision, end
-//                cause (collision / reach / AA / time-up are all known right after physics),
-//                store post-physics state                         | W1: next-episode spawn draw
-//   phase 2  W0: path role (Brent) on the current state           | W1: sensor role + CA reward
-//            W2: path role on the spawn state of envs that ended  | W3: sensor role, same envs
-//   phase 3  W0: reward, bookkeeping, auto-reset state writes     | all: store the obs tile
+//   phase A  W0: load state, thrust, 3-body position update, collision, end cause, 6-pivot joint
+//                sweep, store the state, velocity part of the observation (obs 0-2, 17-18)
+//            W1: frame position -> sensor part (obs 3..16); for envs that end: spawn + full sensor
+//            W2: frame position -> path role (Brent closest point, obs 19..26)
+//            W3: for envs that end: spawn -> path role on the spawn state (auto-reset observation)
+//            W1 and W3 also fill the auto-reset observation cache (below) while W2 searches
+//   phase B  every role writes its columns of the workgroup's obs tile to LDS (the tile shares LDS
+//            with W0's joint constants, hence the barrier between A and B)
+//   phase C  all: store the 64x27 f32 tile as one contiguous span; W0: CA part, reward,
+//            bookkeeping, auto-reset state writes
 //
-// Hand-offs go through LDS with two __syncthreads.  The obs rows of the workgroup are assembled in
-// LDS and written as one contiguous 64x27 f32 span.  At 65 536 envs this is 1 024 workgroups =
-// 4 per CU = 4 waves per SIMD (VGPR <= 128, LDS <= 40 KB), against 1 wave per SIMD for the
-// one-lane-per-env fused kernel it replaces (see DESIGN.md "Kernel v2").
+// The critical path is W2's Brent search; the joint sweep, the sensing and the auto-reset roles
+// run under it.  At 65 536 envs this is 1 024 workgroups = 4 per CU = 4 waves per SIMD
+// (VGPR <= 128, LDS <= 40 KB even with 7 scenario tables).
 //
 // K2 d2d_reset_kernel: masked reset, one lane per env.  K3 d2d_stats_kernel: fixed-order reduction.
 #pragma once
@@ -27,6 +32,24 @@ constexpr int BLOCK = 256;      // K2 / K3 workgroup
 constexpr int EPB = 64;         // K1: envs per workgroup
 constexpr int K1_THREADS = 256; // K1: 4 waves
 constexpr int MAX_LDS_SCN = 8;
+// Wave priorities per role (s_setprio, 0..3) for phase A: the Brent waves win issue arbitration
+// on their SIMD over the other workgroups' physics / sensing waves.
+#ifndef D2D_PRIO_W0
+#define D2D_PRIO_W0 0
+#endif
+#ifndef D2D_PRIO_W1
+#define D2D_PRIO_W1 0
+#endif
+#ifndef D2D_PRIO_W2
+#define D2D_PRIO_W2 3
+#endif
+#ifndef D2D_PRIO_W3
+#define D2D_PRIO_W3 2
+#endif
+#define D2D_SETPRIO(p)                                \
+    do {                                              \
+        if ((p) != 0) __builtin_amdgcn_s_setprio(p);  \
+    } while (0)
 
 struct StepArgs {
     int n;
@@ -34,7 +57,7 @@ struct StepArgs {
     double* st;              // [NSTATE][n]
     int32_t* ist;            // [NISTATE][n]
     double* acc;             // [NSTATS][n]
-    const d2d_scn* scn;      // [n_scn]
+    const Scn* scn;          // [n_scn]
     const int32_t* env_scn;  // [n] or null (all scenario 0)
     d2d_cfg cfg;
     double damping_dt;       // pow(cfg.damping, dt), host glibc
@@ -48,7 +71,22 @@ struct StepArgs {
     float* tobs;
     const uint8_t* mask;     // reset kernel only
     uint64_t* stamps;        // diagnostic builds only (D2D_STAMPS): [waves][8] s_memtime stamps
+    // auto-reset observation cache (handle-internal; see K1 below)
+    double* rc_bs;           // [RC_NB][n] suspended Brent search of the next spawn
+    int32_t* rc_i;           // [RC_NI][n] path status, sensor status, Brent probe count, reset flags
+    float* rc_obs;           // [n][27] next reset observation
 };
+
+// Auto-reset observation cache.  The observation an env gets when it auto-resets depends only on
+// (seed, env id, episode counter, scenario), so it is computed ahead of time, while the env is
+// still running, by the waves that would otherwise idle: W1 the sensor part (obs 0..18), W3 the
+// path part (Brent + obs 19..26 + LA-lock flag).  W3 runs the Brent search at the lowest wave
+// priority and suspends it (state in rc_bs) as soon as W2 finishes the step's own search, so the
+// fill never lengthens a step; an env that ends before its entry is ready falls back to the
+// synchronous computation.  Entries are invalidated by every reset / set_state.
+constexpr int RC_NB = 10;             // a, b, fulc, ffulc, nfc, fnfc, xf, fx, rat, e
+constexpr int RC_PST = 0, RC_SST = 1, RC_NUM = 2, RC_RFLAGS = 3, RC_NI = 4;
+constexpr int RC_BRENT = 1, RC_UDONE = 2, RC_PATH = 4;   // path status bits (sensor status: 0 / 1)
 
 // Diagnostic phase stamps (separate timing-only build, never in the product): lane 0 of each wave
 // records s_memtime at the phase boundaries of K1.
@@ -57,6 +95,10 @@ struct StepArgs {
     do {                                                                                               \
         if (a.stamps && (threadIdx.x & 63) == 0)                                                       \
             a.stamps[(size_t)(blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
+        if (a.stamps && (threadIdx.x & 63) == 0 && (k) == 0)                                           \
+            a.stamps[(size_t)(blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + 7] =                          \
+                ((uint64_t)__builtin_amdgcn_s_getreg((3 << 11) | 20) << 32) |                          \
+                (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);                                   \
     } while (0)
 #else
 #define STAMP(k) \
@@ -65,9 +107,9 @@ struct StepArgs {
 #endif
 
 template <bool LDS, int NT>
-__device__ __forceinline__ const d2d_scn* stage_scenarios(const StepArgs& a, d2d_scn* lds) {
+__device__ __forceinline__ const Scn* stage_scenarios(const StepArgs& a, Scn* lds) {
     if (!LDS) return a.scn;
-    const int words = a.n_scn * (int)(sizeof(d2d_scn) / 8);
+    const int words = a.n_scn * (int)(sizeof(Scn) / 8);
     const double* src = reinterpret_cast<const double*>(a.scn);
     double* dst = reinterpret_cast<double*>(lds);
     for (int k = threadIdx.x; k < words; k += NT) dst[k] = src[k];
@@ -83,28 +125,132 @@ __device__ __forceinline__ T& fld(T* base, int f, int n, int i) {
     return fb[i];
 }
 
+// frame state as stored (pre-step)
+__device__ __forceinline__ Body load_frame(const StepArgs& a, int i) {
+    const int n = a.n;
+    return Body{fld(a.st, 0, n, i), fld(a.st, 1, n, i), fld(a.st, 2, n, i),
+                fld(a.st, 3, n, i), fld(a.st, 4, n, i), fld(a.st, 5, n, i)};
+}
+// end cause of this step from the pre-step state: position update + contact + end tests
+__device__ __forceinline__ int step_cause(const StepArgs& a, const Scn& S, int i, Body& F) {
+    const int n = a.n;
+    const bool hit = frame_advance(S, F);
+    const uint32_t fl = (uint32_t)fld(a.ist, D2D_I_FLAGS, n, i);
+    const int t = fld(a.ist, D2D_I_T, n, i) + 1;
+    return end_cause(a.cfg, S, F, hit || (fl & D2D_FLAG_COLLIDED) != 0, t);
+}
+// next-episode spawn (test-mode reset, drone_2d_env.py:218-311, Drone.py:20-52)
+__device__ __forceinline__ void spawn_state(const StepArgs& a, const Scn& S, int i, double sp[7]) {
+    const uint32_t ep = (uint32_t)fld(a.ist, D2D_I_EPISODE, a.n, i);
+    double x, y, th;
+    spawn_draw(S, a.seed, (uint32_t)a.cfg.env_id_base + (uint32_t)i, ep, x, y, th);
+    double sl, cl, sr, cr;
+    sincos_d(th + PI, sl, cl);
+    sincos_d(th, sr, cr);
+    sp[0] = x;
+    sp[1] = y;
+    sp[2] = th;
+    sp[3] = cl * DRONE_R + x;
+    sp[4] = sl * DRONE_R + y;
+    sp[5] = cr * DRONE_R + x;
+    sp[6] = sr * DRONE_R + y;
+}
+
+// wave-uniform read of an LDS flag written by another wave of the workgroup
+// (explicit LDS address space: a generic volatile access would become a flat load)
+using LdsU32 = __attribute__((address_space(3))) uint32_t;
+__device__ __forceinline__ bool stop_seen(const uint32_t& stop) {
+    return __builtin_amdgcn_readfirstlane(*(const volatile LdsU32*)&stop) != 0u;
+}
+__device__ __forceinline__ void stop_raise(uint32_t& stop) { *(volatile LdsU32*)&stop = 1u; }
+// W3's cache fill: advance the suspended Brent search of the next spawn of every env in `need`
+// until it converges or W2 raises `stop`, then (time permitting) finish the path part.
+__device__ __forceinline__ void rc_fill_path(const StepArgs& a, const Scn& S, int i, bool need, int32_t pst,
+                                             const uint32_t& stop) {
+    __builtin_amdgcn_s_setprio(0);
+    if (__ballot(need) == 0 || stop_seen(stop)) return;
+    const int n = a.n;
+    const PathK K = path_k(S);
+    double x = 0.0, y = 0.0, th = 0.0;
+    Brent B{};
+    const bool resumed = (pst & (RC_BRENT | RC_UDONE)) != 0;
+    if (need) {
+        const uint32_t ep = (uint32_t)fld(a.ist, D2D_I_EPISODE, n, i);
+        spawn_draw(S, a.seed, (uint32_t)a.cfg.env_id_base + (uint32_t)i, ep, x, y, th);
+        if (resumed) {
+            B.a = fld(a.rc_bs, 0, n, i);
+            B.b = fld(a.rc_bs, 1, n, i);
+            B.fulc = fld(a.rc_bs, 2, n, i);
+            B.ffulc = fld(a.rc_bs, 3, n, i);
+            B.nfc = fld(a.rc_bs, 4, n, i);
+            B.fnfc = fld(a.rc_bs, 5, n, i);
+            B.xf = fld(a.rc_bs, 6, n, i);
+            B.fx = fld(a.rc_bs, 7, n, i);
+            B.rat = fld(a.rc_bs, 8, n, i);
+            B.e = fld(a.rc_bs, 9, n, i);
+            B.num = fld(a.rc_i, RC_NUM, n, i);
+        } else {
+            brent_init(S, K, x, y, B);
+        }
+    }
+    bool act = need && !(pst & RC_UDONE) && brent_active(B);
+    while (__ballot(act) != 0 && !stop_seen(stop)) {
+        if (act) {
+            brent_step(S, K, x, y, B);
+            act = brent_active(B);
+        }
+    }
+    if (need && !(pst & RC_UDONE)) {
+        pst = brent_active(B) ? RC_BRENT : RC_UDONE;
+        fld(a.rc_bs, 0, n, i) = B.a;
+        fld(a.rc_bs, 1, n, i) = B.b;
+        fld(a.rc_bs, 2, n, i) = B.fulc;
+        fld(a.rc_bs, 3, n, i) = B.ffulc;
+        fld(a.rc_bs, 4, n, i) = B.nfc;
+        fld(a.rc_bs, 5, n, i) = B.fnfc;
+        fld(a.rc_bs, 6, n, i) = B.xf;
+        fld(a.rc_bs, 7, n, i) = B.fx;
+        fld(a.rc_bs, 8, n, i) = B.rat;
+        fld(a.rc_bs, 9, n, i) = B.e;
+        fld(a.rc_i, RC_NUM, n, i) = B.num;
+    }
+    const bool tail = need && (pst & RC_UDONE);
+    if (__ballot(tail) != 0 && !stop_seen(stop)) {
+        if (tail) {
+            uint32_t f = 0;
+            double o[8];
+            path_obs_u(a.cfg, S, x, y, th, B.xf, f, o);
+            float* c = a.rc_obs + (size_t)i * D2D_OBS_DIM + 19;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) c[k] = (float)o[k];
+            fld(a.rc_i, RC_RFLAGS, n, i) = (int32_t)f;
+            pst = RC_PATH;
+        }
+    }
+    if (need) fld(a.rc_i, RC_PST, n, i) = pst;
+}
+
 // ------------------------------------------------------------------------------------------ K1
 struct K1Shared {
-    double fr[6][EPB];        // post-physics frame: px, py, angle, vx, vy, w
-    double sp[7][EPB];        // next-episode spawn: x, y, th, left (x, y), right (x, y)
-    int cause[EPB];           // end cause of this step (0: running)
+    double sp[7][EPB];        // W3 -> W0: next-episode spawn of envs that end
     int scn[EPB];             // scenario index per env
-    uint32_t ep[EPB];         // episode counter (before this step's reset)
-    uint32_t rflags[EPB];     // flags of the reset observation (LA lock)
+    uint32_t pflags[EPB];     // W2 -> W0: LA-lock bit after the path role
+    uint32_t rflags[EPB];     // W3 -> W0: flags of the reset observation
+    uint32_t stop;            // W2 -> W1, W3: the step's own Brent search is finished
     union {
-        double jb[36][EPB];   // phase 1: W0's per-joint K^-1 (4) + bias (2), re-read every sweep
+        double jb[6 * JB_PER_JOINT][EPB];  // phase A: W0's per-joint K^-1 + bias, re-read every sweep
         struct {
-            double ca[5][EPB];             // sensor -> reward: vel_ang, ca, lpa, lca, dclose
+            double ca[3][EPB];             // W1 -> W0: obs 8, 9, 10 (fp64) for the CA reward part
+            double po[4][EPB];             // W2 -> W0: obs 19, 20, 23, 24 (fp64) for the reward
             float obs[EPB * D2D_OBS_DIM];  // the workgroup's obs rows
-        } p;                  // phases 2-3
+        } p;                               // phases B, C
     } u;
 };
 
 template <bool LDS>
 __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
-    // dynamic LDS: n_scn scenario tables (sized at launch, so a 1-scenario batch keeps 6 workgroups
-    // per CU by LDS and a 7-scenario mixed batch still fits 4)
-    extern __shared__ __attribute__((aligned(16))) d2d_scn s_scn[];
+    // dynamic LDS: n_scn scenario tables (sized at launch)
+    extern __shared__ __attribute__((aligned(16))) Scn s_scn[];
     __shared__ __attribute__((aligned(16))) K1Shared sh;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -112,19 +258,28 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
     const int i = e0 + lane;
     const bool valid = i < a.n;
     const int n = a.n;
+    const bool auto_reset = a.cfg.auto_reset != 0;
     STAMP(0);
-    const d2d_scn* scns = stage_scenarios<LDS, K1_THREADS>(a, s_scn);
+    const Scn* scns = stage_scenarios<LDS, K1_THREADS>(a, s_scn);
     if (wave == 0) sh.scn[lane] = (valid && a.env_scn && a.n_scn > 1) ? a.env_scn[i] : 0;
+    if (threadIdx.x == 0) sh.stop = 0u;
     __syncthreads();
     STAMP(1);
-    const d2d_scn& S = scns[sh.scn[lane]];
+    const Scn& S = scns[sh.scn[lane]];
+    float* const trow = a.tobs ? a.tobs + (size_t)i * D2D_OBS_DIM : nullptr;
 
-    // ---------------------------------------------------------------- phase 1
-    double path_err = 0.0, tot_rew = 0.0;
-    int t = 0;
+    // ---------------------------------------------------------------- phase A
+    // W0 results kept for phase C
+    Body F0{};
+    double path_err = 0.0, tot_rew = 0.0, ov[19];
+    int t = 0, cause = 0;
     uint32_t flags = 0;
-    int cause = 0;
+    // W1 / W2 / W3 results written to the tile in phase B
+    float row[19];
+    double cao[3] = {0.0, 0.0, 0.0}, po[8];
+    bool done = false;
     if (wave == 0) {
+        D2D_SETPRIO(D2D_PRIO_W0);
         if (valid) {
             Body B[3];
             double j[12];
@@ -152,117 +307,173 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
             if (phys_positions(S, B, (double)lf, (double)rf, cs, sn, fx, fy, tq)) flags |= D2D_FLAG_COLLIDED;
             t += 1;
             cause = end_cause(a.cfg, S, B[0], (flags & D2D_FLAG_COLLIDED) != 0, t);
-            // positions are final: retire them before the joint sweep (envs that end this step are
-            // overwritten with their spawn state in phase 3)
+            const Arms A = make_arms(cs, sn);
+            const double pos[6] = {B[0].px, B[0].py, B[1].px, B[1].py, B[2].px, B[2].py};
+            double vel[9] = {B[0].vx, B[0].vy, B[0].w, B[1].vx, B[1].vy, B[1].w, B[2].vx, B[2].vy, B[2].w};
+            phys_velocities<true>(A, pos, a.damping_dt, fx, fy, tq, vel, j, &sh.u.jb[0][lane], EPB);
+            // envs that end are overwritten with their spawn state in phase C
 #pragma unroll
             for (int b = 0; b < 3; ++b) {
                 fld(a.st, 6 * b + 0, n, i) = B[b].px;
                 fld(a.st, 6 * b + 1, n, i) = B[b].py;
                 fld(a.st, 6 * b + 2, n, i) = B[b].a;
-            }
-            sh.fr[0][lane] = B[0].px;
-            sh.fr[1][lane] = B[0].py;
-            sh.fr[2][lane] = B[0].a;
-            const Arms A = make_arms(cs, sn);
-            const double pos[6] = {B[0].px, B[0].py, B[1].px, B[1].py, B[2].px, B[2].py};
-            double vel[9] = {B[0].vx, B[0].vy, B[0].w, B[1].vx, B[1].vy, B[1].w, B[2].vx, B[2].vy, B[2].w};
-            phys_velocities<true>(A, pos, a.damping_dt, fx, fy, tq, vel, j, &sh.u.jb[0][lane], EPB);
-#pragma unroll
-            for (int b = 0; b < 3; ++b) {
                 fld(a.st, 6 * b + 3, n, i) = vel[3 * b + 0];
                 fld(a.st, 6 * b + 4, n, i) = vel[3 * b + 1];
                 fld(a.st, 6 * b + 5, n, i) = vel[3 * b + 2];
             }
 #pragma unroll
             for (int k = 0; k < 12; ++k) fld(a.st, D2D_S_J + k, n, i) = j[k];
-            sh.fr[3][lane] = vel[0];
-            sh.fr[4][lane] = vel[1];
-            sh.fr[5][lane] = vel[2];
+            F0 = Body{B[0].px, B[0].py, B[0].a, vel[0], vel[1], vel[2]};
+            sensor_vel(F0, ov);
+            done = cause != 0;
+            if (done && trow) {
+                trow[0] = (float)ov[0];
+                trow[1] = (float)ov[1];
+                trow[2] = (float)ov[2];
+                trow[17] = (float)ov[17];
+                trow[18] = (float)ov[18];
+            }
         }
-        sh.cause[lane] = cause;
-    } else if (wave == 1 && valid) {
-        // next-episode spawn (test-mode reset, drone_2d_env.py:218-311, Drone.py:20-52)
-        const uint32_t ep = (uint32_t)fld(a.ist, D2D_I_EPISODE, n, i);
-        double x, y, th;
-        spawn_draw(S, a.seed, (uint32_t)a.cfg.env_id_base + (uint32_t)i, ep, x, y, th);
-        double sl, cl, sr, cr;
-        sincos_d(th + PI, sl, cl);
-        sincos_d(th, sr, cr);
-        sh.sp[0][lane] = x;
-        sh.sp[1][lane] = y;
-        sh.sp[2][lane] = th;
-        sh.sp[3][lane] = cl * DRONE_R + x;
-        sh.sp[4][lane] = sl * DRONE_R + y;
-        sh.sp[5][lane] = cr * DRONE_R + x;
-        sh.sp[6][lane] = sr * DRONE_R + y;
-        sh.ep[lane] = ep;
+    } else if (wave == 1) {
+        // sensor role
+        D2D_SETPRIO(D2D_PRIO_W1);
+        int32_t sst = 0;
+        if (valid) {
+            Body F = load_frame(a, i);
+            done = step_cause(a, S, i, F) != 0;
+            if (auto_reset) sst = fld(a.rc_i, RC_SST, n, i);
+            double so[19];
+            sensor_pos(a.cfg, S, F.px, F.py, F.a, so);
+            cao[0] = so[8];
+            cao[1] = so[9];
+            cao[2] = so[10];
+            if (done && trow) {
+#pragma unroll
+                for (int k = 3; k < 17; ++k) trow[k] = (float)so[k];
+            }
+            if (done && auto_reset && sst != 0) {
+                // cached spawn-state sensor part; the new episode's entry is refilled from next step
+                const float* c = a.rc_obs + (size_t)i * D2D_OBS_DIM;
+#pragma unroll
+                for (int k = 0; k < 19; ++k) row[k] = c[k];
+                fld(a.rc_i, RC_SST, n, i) = 0;
+            } else {
+                if (done && auto_reset) {
+                    double sp[7];
+                    spawn_state(a, S, i, sp);
+                    sensor_obs(a.cfg, S, Body{sp[0], sp[1], sp[2], 0.0, 0.0, 0.0}, so);
+                }
+#pragma unroll
+                for (int k = 0; k < 19; ++k) row[k] = (float)so[k];
+            }
+        }
+        // cache fill: spawn-state sensor part of the next reset of envs that keep running, started
+        // only while W2's search is still running
+        __builtin_amdgcn_s_setprio(0);
+        if (auto_reset && !stop_seen(sh.stop)) {
+            if (valid && !done && sst == 0) {
+                double sp[7], so[19];
+                spawn_state(a, S, i, sp);
+                sensor_obs(a.cfg, S, Body{sp[0], sp[1], sp[2], 0.0, 0.0, 0.0}, so);
+                float* c = a.rc_obs + (size_t)i * D2D_OBS_DIM;
+#pragma unroll
+                for (int k = 0; k < 19; ++k) c[k] = (float)so[k];
+                fld(a.rc_i, RC_SST, n, i) = 1;
+            }
+        }
+    } else if (wave == 2) {
+        // path role on the current state: the critical path, so it wins issue arbitration on its SIMD
+        D2D_SETPRIO(D2D_PRIO_W2);
+        if (valid) {
+            Body F = load_frame(a, i);
+            advance_position(F);
+            uint32_t f = (uint32_t)fld(a.ist, D2D_I_FLAGS, n, i);
+            path_obs(a.cfg, S, F.px, F.py, F.a, f, po);
+            sh.pflags[lane] = f & D2D_FLAG_LA_LOCK;
+        }
+        if (lane == 0) stop_raise(sh.stop);
+    } else {
+        // path role on the spawn state of envs that end (auto-reset observation)
+        D2D_SETPRIO(D2D_PRIO_W3);
+        int32_t pst = 0;
+        if (valid) {
+            Body F = load_frame(a, i);
+            done = step_cause(a, S, i, F) != 0;
+            if (auto_reset) pst = fld(a.rc_i, RC_PST, n, i);
+            if (done && auto_reset) {
+                double sp[7];
+                spawn_state(a, S, i, sp);
+#pragma unroll
+                for (int k = 0; k < 7; ++k) sh.sp[k][lane] = sp[k];
+                if (pst & RC_PATH) {
+                    const float* c = a.rc_obs + (size_t)i * D2D_OBS_DIM + 19;
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) po[k] = (double)c[k];
+                    sh.rflags[lane] = (uint32_t)fld(a.rc_i, RC_RFLAGS, n, i);
+                } else {
+                    uint32_t f = 0;
+                    path_obs(a.cfg, S, sp[0], sp[1], sp[2], f, po);
+                    sh.rflags[lane] = f;
+                }
+                fld(a.rc_i, RC_PST, n, i) = 0;
+            }
+        }
+        if (auto_reset) rc_fill_path(a, S, i, valid && !done && !(pst & RC_PATH), pst, sh.stop);
     }
     STAMP(2);
     __syncthreads();
     STAMP(3);
 
-    // ---------------------------------------------------------------- phase 2
-    const int my_cause = sh.cause[lane];
-    const bool done = valid && my_cause != 0;
-    const bool auto_reset = a.cfg.auto_reset != 0;
-    double po[8];
+    // ---------------------------------------------------------------- phase B: obs tile
     float* orow = &sh.u.p.obs[lane * D2D_OBS_DIM];
-    if (wave == 0 || wave == 2) {
-        // path role: W0 current state, W2 spawn state of envs that ended (auto-reset)
-        const bool rs = (wave == 2);
-        if (valid && (!rs || (done && auto_reset))) {
-            const double x = rs ? sh.sp[0][lane] : sh.fr[0][lane];
-            const double y = rs ? sh.sp[1][lane] : sh.fr[1][lane];
-            const double al = rs ? sh.sp[2][lane] : sh.fr[2][lane];
-            uint32_t f = rs ? 0u : flags;
-            path_obs(a.cfg, S, x, y, al, f, po);
-            if (rs) sh.rflags[lane] = f;
-            else flags = f;
-            if (rs || !(done && auto_reset)) {
-#pragma unroll
-                for (int k = 0; k < 8; ++k) orow[19 + k] = (float)po[k];
+    if (valid) {
+        if (wave == 0) {
+            if (!(done && auto_reset)) {
+                orow[0] = (float)ov[0];
+                orow[1] = (float)ov[1];
+                orow[2] = (float)ov[2];
+                orow[17] = (float)ov[17];
+                orow[18] = (float)ov[18];
             }
-            if (!rs && done && a.tobs) {
+        } else if (wave == 1) {
+            // a reset row holds the whole spawn-state sensor part, otherwise obs 3..16
+            if (done && auto_reset) {
 #pragma unroll
-                for (int k = 0; k < 8; ++k) a.tobs[(size_t)i * D2D_OBS_DIM + 19 + k] = (float)po[k];
-            }
-        }
-    } else {
-        // sensor role: W1 current state (+ the reward's CA part), W3 spawn state of ended envs
-        const bool rs = (wave == 3);
-        if (valid && (!rs || (done && auto_reset))) {
-            Body F;
-            if (rs) {
-                F = Body{sh.sp[0][lane], sh.sp[1][lane], sh.sp[2][lane], 0.0, 0.0, 0.0};
+                for (int k = 0; k < 19; ++k) orow[k] = row[k];
             } else {
-                F = Body{sh.fr[0][lane], sh.fr[1][lane], sh.fr[2][lane], sh.fr[3][lane], sh.fr[4][lane],
-                         sh.fr[5][lane]};
-            }
-            double so[19];
-            sensor_obs(a.cfg, S, F, so);
-            if (!rs) {
-                const CAPart P = reward_ca_part(a.cfg, S, so);
-                sh.u.p.ca[0][lane] = P.vel_ang;
-                sh.u.p.ca[1][lane] = P.ca;
-                sh.u.p.ca[2][lane] = P.lpa;
-                sh.u.p.ca[3][lane] = P.lca;
-                sh.u.p.ca[4][lane] = P.dclose;
-            }
-            if (rs || !(done && auto_reset)) {
 #pragma unroll
-                for (int k = 0; k < 19; ++k) orow[k] = (float)so[k];
+                for (int k = 3; k < 17; ++k) orow[k] = row[k];
             }
-            if (!rs && done && a.tobs) {
+            sh.u.p.ca[0][lane] = cao[0];
+            sh.u.p.ca[1][lane] = cao[1];
+            sh.u.p.ca[2][lane] = cao[2];
+        } else if (wave == 2) {
+            // every row gets the current-state path part; W3 replaces it on reset rows below
+            sh.u.p.po[0][lane] = po[0];
+            sh.u.p.po[1][lane] = po[1];
+            sh.u.p.po[2][lane] = po[4];
+            sh.u.p.po[3][lane] = po[5];
 #pragma unroll
-                for (int k = 0; k < 19; ++k) a.tobs[(size_t)i * D2D_OBS_DIM + k] = (float)so[k];
-            }
+            for (int k = 0; k < 8; ++k) orow[19 + k] = (float)po[k];
         }
     }
     STAMP(4);
     __syncthreads();
+    // W3 (which knows which envs end): terminal-obs copy of the path part, then the reset row
+    if (wave == 3 && valid && done) {
+        if (trow) {
+#pragma unroll
+            for (int k = 19; k < 27; ++k) trow[k] = orow[k];
+        }
+        if (auto_reset) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) orow[19 + k] = (float)po[k];
+        }
+    }
+    __syncthreads();
     STAMP(5);
 
-    // ---------------------------------------------------------------- phase 3
+    // ---------------------------------------------------------------- phase C
     // obs tile: rows [e0, e0+rows) are one contiguous span of global memory
     {
         const int rows = min(EPB, n - e0);
@@ -271,14 +482,22 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
         for (int k = threadIdx.x; k < words; k += K1_THREADS) dst[k] = sh.u.p.obs[k];
     }
     if (wave == 0 && valid) {
-        const Body F{sh.fr[0][lane], sh.fr[1][lane], sh.fr[2][lane], sh.fr[3][lane], sh.fr[4][lane], sh.fr[5][lane]};
-        const CAPart P{sh.u.p.ca[0][lane], sh.u.p.ca[1][lane], sh.u.p.ca[2][lane], sh.u.p.ca[3][lane], sh.u.p.ca[4][lane]};
-        const Reward R = reward_final(a.cfg, F, po, P, my_cause);
+        flags = (flags & ~D2D_FLAG_LA_LOCK) | sh.pflags[lane];
+        ov[8] = sh.u.p.ca[0][lane];
+        ov[9] = sh.u.p.ca[1][lane];
+        ov[10] = sh.u.p.ca[2][lane];
+        const CAPart P = reward_ca_part(a.cfg, S, ov);
+        double pw[8];
+        pw[0] = sh.u.p.po[0][lane];
+        pw[1] = sh.u.p.po[1][lane];
+        pw[4] = sh.u.p.po[2][lane];
+        pw[5] = sh.u.p.po[3][lane];
+        const Reward R = reward_final(a.cfg, F0, pw, P, cause);
         path_err += R.dist_path;
         const double ape = path_err / (double)t;
         tot_rew += R.reward;
         bool trunc = false, term = done;
-        if (a.cfg.timeup_truncates && done && my_cause == D2D_END_TIMEUP) {
+        if (a.cfg.timeup_truncates && done && cause == D2D_END_TIMEUP) {
             trunc = true;
             term = false;
         }
@@ -295,15 +514,15 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
             r[D2D_INFO_AA] = (float)R.aa;
             r[D2D_INFO_DCLOSE] = (float)R.dclose;
             r[D2D_INFO_STEPS] = (float)t;
-            r[D2D_INFO_CAUSE] = (float)my_cause;
+            r[D2D_INFO_CAUSE] = (float)cause;
             r[D2D_INFO_APE] = done ? (float)ape : 0.0f;
             r[D2D_INFO_TOTREW] = done ? (float)tot_rew : 0.0f;
             r[D2D_INFO_REWARD] = (float)R.reward;
         }
         if (done) {
             // finished-episode accumulators (info counters of drone_2d_env.py:593-613)
-            const bool c1 = my_cause & D2D_END_COLLISION, c2 = my_cause & D2D_END_REACH;
-            const bool c4 = my_cause & D2D_END_TIMEUP, c5 = my_cause & D2D_END_AA;
+            const bool c1 = cause & D2D_END_COLLISION, c2 = cause & D2D_END_REACH;
+            const bool c4 = cause & D2D_END_TIMEUP, c5 = cause & D2D_END_AA;
             fld(a.acc, D2D_ST_RETURN, n, i) += tot_rew;
             fld(a.acc, D2D_ST_EPISODES, n, i) += 1.0;
             fld(a.acc, D2D_ST_SUCCESS, n, i) += c2 ? 1.0 : 0.0;
@@ -324,7 +543,7 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
             fld(a.st, D2D_S_TOT_REW, n, i) = 0.0;
             fld(a.ist, D2D_I_T, n, i) = 0;
             fld(a.ist, D2D_I_FLAGS, n, i) = (int32_t)sh.rflags[lane];
-            fld(a.ist, D2D_I_EPISODE, n, i) = (int32_t)(sh.ep[lane] + 1u);
+            fld(a.ist, D2D_I_EPISODE, n, i) += 1;
         } else {
             fld(a.st, D2D_S_PATH_ERR, n, i) = path_err;
             fld(a.st, D2D_S_TOT_REW, n, i) = tot_rew;
@@ -338,25 +557,22 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
 // ------------------------------------------------------------------------------------------ K2
 template <bool LDS>
 __global__ __launch_bounds__(BLOCK) void d2d_reset_kernel(StepArgs a) {
-    extern __shared__ __attribute__((aligned(16))) d2d_scn s_scn[];
-    const d2d_scn* scns = stage_scenarios<LDS, BLOCK>(a, s_scn);
+    extern __shared__ __attribute__((aligned(16))) Scn s_scn[];
+    const Scn* scns = stage_scenarios<LDS, BLOCK>(a, s_scn);
     __syncthreads();
     const int i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= a.n) return;
     if (a.mask && !a.mask[i]) return;
     const int n = a.n;
-    const d2d_scn& s = scns[(a.env_scn && a.n_scn > 1) ? a.env_scn[i] : 0];
-    const uint32_t ep = (uint32_t)fld(a.ist, D2D_I_EPISODE, n, i);
-    double x, y, th;
-    spawn_draw(s, a.seed, (uint32_t)a.cfg.env_id_base + (uint32_t)i, ep, x, y, th);
-    double sl, cl, sr, cr;
-    sincos_d(th + PI, sl, cl);
-    sincos_d(th, sr, cr);
-    const double bodies[18] = {x, y, th, 0.0, 0.0, 0.0, cl * DRONE_R + x, sl * DRONE_R + y, th, 0.0, 0.0, 0.0,
-                               cr * DRONE_R + x, sr * DRONE_R + y, th, 0.0, 0.0, 0.0};
+    const Scn& s = scns[(a.env_scn && a.n_scn > 1) ? a.env_scn[i] : 0];
+    double sp[7];
+    spawn_state(a, s, i, sp);
+    const double th = sp[2];
+    const double bodies[18] = {sp[0], sp[1], th, 0.0, 0.0, 0.0, sp[3], sp[4], th, 0.0, 0.0, 0.0,
+                               sp[5], sp[6], th, 0.0, 0.0, 0.0};
     uint32_t flags = 0;
     double obs[D2D_OBS_DIM];
-    observe(a.cfg, s, Body{x, y, th, 0.0, 0.0, 0.0}, flags, obs);
+    observe(a.cfg, s, Body{sp[0], sp[1], th, 0.0, 0.0, 0.0}, flags, obs);
 #pragma unroll
     for (int f = 0; f < 18; ++f) fld(a.st, f, n, i) = bodies[f];
 #pragma unroll
@@ -365,7 +581,7 @@ __global__ __launch_bounds__(BLOCK) void d2d_reset_kernel(StepArgs a) {
     fld(a.st, D2D_S_TOT_REW, n, i) = 0.0;
     fld(a.ist, D2D_I_T, n, i) = 0;
     fld(a.ist, D2D_I_FLAGS, n, i) = (int32_t)flags;
-    fld(a.ist, D2D_I_EPISODE, n, i) = (int32_t)(ep + 1u);
+    fld(a.ist, D2D_I_EPISODE, n, i) += 1;
     if (a.obs) {
 #pragma unroll
         for (int k = 0; k < D2D_OBS_DIM; ++k) a.obs[(size_t)i * D2D_OBS_DIM + k] = (float)obs[k];

@@ -124,8 +124,8 @@ class Drone2dVecEnv:
         # double-buffered outputs: the tensors returned by step k stay valid during step k+1
         self._bufs = [dict(obs=torch.empty(N, abi.OBS_DIM, dtype=torch.float32, device=dev),
                            rew=torch.empty(N, dtype=torch.float32, device=dev),
-                           term=torch.empty(N, dtype=torch.uint8, device=dev),
-                           trunc=torch.empty(N, dtype=torch.uint8, device=dev),
+                           term=torch.empty(N, dtype=torch.bool, device=dev),   # written as 0/1 bytes
+                           trunc=torch.empty(N, dtype=torch.bool, device=dev),
                            info=torch.empty(N, abi.INFO_DIM, dtype=torch.float32, device=dev),
                            tobs=torch.zeros(N, abi.OBS_DIM, dtype=torch.float32, device=dev))
                       for _ in range(2)]
@@ -186,7 +186,7 @@ class Drone2dVecEnv:
                                  self._ptr(b["info"]) if self.with_info else None,
                                  self._ptr(b["tobs"]), self._stream()), "d2d_step")
         self._last_actions = a  # keep alive until the kernel has consumed it
-        return b["obs"], b["rew"], b["term"].bool(), b["trunc"].bool(), (b["info"] if self.with_info else None)
+        return b["obs"], b["rew"], b["term"], b["trunc"], (b["info"] if self.with_info else None)
 
     @property
     def terminal_obs(self) -> torch.Tensor:

@@ -67,6 +67,46 @@ def test_vs_oracle_teacher_forced(d2, scn):
     venv.close()
 
 
+def test_reset_cache_invalidation(d2):
+    """The auto-reset observation cache (filled ahead of time by the idle waves) must be dropped
+    by a full reset with a new seed and by set_state (episode counters may change)."""
+    venv, orc = make_pair(d2, 2048, ["corridor"], seed=99, kwargs=_cfgkw())
+    rng = np.random.default_rng(4)
+
+    def run(steps):
+        d = 0
+        for _t in range(steps):
+            act = np.clip(rng.normal(0.0, 0.6, (venv.num_envs, 2)), -1, 1).astype(np.float32)
+            compare_step(venv, orc, act)
+            d += int(orc.term.sum())
+        return d
+
+    assert run(60) > 0
+    obs_g = venv.reset(seed=123).cpu().numpy()
+    obs_o = orc.reset(123)
+    np.testing.assert_allclose(obs_g, obs_o, rtol=0, atol=OBS_ATOL)
+    assert run(100) > 20
+    st, ist = venv.get_state()
+    ist[2] += 5  # jump every episode counter: cached spawns are stale
+    venv.set_state(st, ist)
+    orc.set_state(st.cpu().numpy(), ist.cpu().numpy())
+    assert run(100) > 20
+    venv.close()
+
+
+def test_reset_cache_short_episodes(d2):
+    """Episodes shorter than the cache fill: a mix of cached and synchronous reset observations."""
+    venv, orc = make_pair(d2, 1024, SCENARIOS, seed=8, kwargs=_cfgkw(n_steps=3))
+    rng = np.random.default_rng(5)
+    dones = 0
+    for t in range(30):
+        act = rng.uniform(-1, 1, (venv.num_envs, 2)).astype(np.float32)
+        compare_step(venv, orc, act)
+        dones += int(orc.term.sum())
+    assert dones >= 9 * 1000
+    venv.close()
+
+
 def test_free_running_agreement(d2):
     """No teacher forcing: both batches evolve independently from the same reset."""
     venv, orc = make_pair(d2, 1024, SCENARIOS, seed=5, kwargs=_cfgkw())

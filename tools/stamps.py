@@ -21,24 +21,29 @@ sys.path.insert(0, REPO)
 LIB = os.path.join(REPO, "tools", "_abl", "libd2d_stamps.so")
 
 
-def build():
+def lib_path(tag):
+    return LIB if not tag else LIB.replace(".so", f"_{tag}.so")
+
+
+def build(tag="", defines=()):
     import drone2d_amd  # noqa: F401
     from drone2d_amd import _build
 
-    os.makedirs(os.path.dirname(LIB), exist_ok=True)
-    subprocess.run([_build.hipcc(), *_build.HIPCC_FLAGS, "-DD2D_STAMPS", "-I", os.path.join(REPO, "include"),
-                    _build.SRC, "-o", LIB], check=True)
-    print("built", LIB)
+    out = lib_path(tag)
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    subprocess.run([_build.hipcc(), *_build.HIPCC_FLAGS, "-DD2D_STAMPS", *[f"-D{d}" for d in defines],
+                    "-I", os.path.join(REPO, "include"), _build.SRC, "-o", out], check=True)
+    print("built", out)
 
 
-def run(scenario, n, steps_warm):
+def run(scenario, n, steps_warm, lib=LIB):
     import numpy as np
     import torch
 
     import drone2d_amd as d2
     from drone2d_amd.config import ENV_TRAIN_CONFIG
 
-    venv = d2.Drone2dVecEnv(n, seed=3, with_info=False, native_lib=LIB, **dict(ENV_TRAIN_CONFIG, scenario=scenario))
+    venv = d2.Drone2dVecEnv(n, seed=3, with_info=False, native_lib=lib, **dict(ENV_TRAIN_CONFIG, scenario=scenario))
     lib = venv._lib
     lib.d2d_debug_stamps.argtypes = [C.c_void_p, C.c_void_p]
     nw = (n + 63) // 64 * 4
@@ -58,8 +63,29 @@ def run(scenario, n, steps_warm):
         res[f"wave{w}"] = {nm: [int(np.median(d[:, k])), int(np.percentile(d[:, k], 95)), int(d[:, k].max())]
                            for k, nm in enumerate(names)}
         res[f"wave{w}"]["total"] = [int(np.median(s[:, w, 6] - s[:, w, 0])), int((s[:, w, 6] - s[:, w, 0]).max())]
-    starts = s[:, 0, 0] - t0
-    res["block_start_spread"] = [int(np.median(starts)), int(starts.max())]
+    # placement: slot 7 = XCC_ID << 32 | HW_ID (wave, simd [5:4], cu [11:8], sh [12], se [15:13])
+    hw = s[:, :, 7]
+    xcc = (hw >> 32) & 0xF
+    hid = hw & 0xFFFFFFFF
+    simd = (hid >> 4) & 3
+    cu = (xcc << 8) | (((hid >> 13) & 7) << 5) | (((hid >> 12) & 1) << 4) | ((hid >> 8) & 0xF)
+    res["simd_of_wave_hist"] = [np.bincount(simd[:, w], minlength=4).tolist() for w in range(4)]
+    # Brent waves (wave 2) sharing a SIMD, and W2's phase-A duration by that count
+    key = cu * 4 + simd
+    cnt = {}
+    for b in range(s.shape[0]):
+        cnt[key[b, 2]] = cnt.get(key[b, 2], 0) + 1
+    share = np.array([cnt[key[b, 2]] for b in range(s.shape[0])])
+    dA = s[:, 2, 2] - s[:, 2, 1]
+    res["w2_by_simd_share"] = {int(k): [int((share == k).sum()), int(np.median(dA[share == k]))]
+                               for k in np.unique(share)}
+    res["blocks_per_cu"] = np.bincount(np.unique(cu[:, 0], return_inverse=True)[1]).tolist()[:8]
+    # per-XCD clocks differ: span from per-XCD t0
+    spans = []
+    for x in np.unique(xcc[:, 0]):
+        m = xcc[:, 0] == x
+        spans.append(int(s[m, :, 6].max() - s[m, :, 0].min()))
+    res["kernel_span_cycles_per_xcd"] = spans
     print(json.dumps(res, indent=1))
     return res
 
@@ -70,10 +96,17 @@ if __name__ == "__main__":
     ap.add_argument("--scenario", default="corridor")
     ap.add_argument("--envs", type=int, default=65536)
     ap.add_argument("--warm", type=int, default=40)
+    ap.add_argument("--tag", default="", help="variant library suffix")
+    ap.add_argument("-D", dest="defines", action="append", default=[], help="extra -D for the variant")
+    ap.add_argument("--small", type=int, default=16384, help="second (1 workgroup per CU) size; 0 = skip")
     a = ap.parse_args()
     if a.mode == "build":
-        build()
+        build(a.tag, a.defines)
     else:
-        out = [run(a.scenario, a.envs, a.warm), run(a.scenario, 16384, a.warm)]
+        lib = lib_path(a.tag)
+        out = [run(a.scenario, a.envs, a.warm, lib)]
+        if a.small:
+            out.append(run(a.scenario, a.small, a.warm, lib))
         os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
-        json.dump(out, open(os.path.join(REPO, "gpurun_out", "stamps.json"), "w"), indent=1)
+        name = "stamps.json" if not a.tag else f"stamps_{a.tag}.json"
+        json.dump(out, open(os.path.join(REPO, "gpurun_out", name), "w"), indent=1)

@@ -1,0 +1,90 @@
+#!/usr/bin/env python3
+"""A/B timing of compile-time variants of the product library (diagnostic builds, never shipped).
+
+    python tools/variants.py build base p0:D2D_PRIO=0     # CPU container: tools/_abl/libd2d_var_<tag>.so
+    python tools/variants.py run base p0 [--envs N]        # GPU box: ms/step of each, interleaved rounds
+
+A spec is TAG[:DEF[,DEF...]]; DEF is passed as -DDEF.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tools"))
+ABL = os.path.join(REPO, "tools", "_abl")
+
+
+def lib_for(tag):
+    return os.path.join(ABL, f"libd2d_var_{tag}.so")
+
+
+def build(specs):
+    import drone2d_amd  # noqa: F401
+    from drone2d_amd import _build
+
+    os.makedirs(ABL, exist_ok=True)
+    for spec in specs:
+        tag, _, defs = spec.partition(":")
+        d = [f"-D{x}" for x in defs.split(",") if x]
+        subprocess.run([_build.hipcc(), *_build.HIPCC_FLAGS, *d, "-I", os.path.join(REPO, "include"), _build.SRC,
+                        "-o", lib_for(tag)], check=True)
+        print("built", lib_for(tag), d)
+
+
+def time_variant(d2, torch, lib, n, scenario, steps=200, warmup=30, auto_reset=True):
+    from drone2d_amd.config import ENV_TRAIN_CONFIG
+
+    venv = d2.Drone2dVecEnv(n, seed=1, with_info=False, native_lib=lib, auto_reset=auto_reset,
+                            **dict(ENV_TRAIN_CONFIG, scenario=scenario))
+    venv.reset()
+    acts = [torch.rand(n, 2, device=venv.device) * 2 - 1 for _ in range(8)]
+    for k in range(warmup):
+        venv.step(acts[k % 8])
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for k in range(steps):
+        venv.step(acts[k % 8])
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    venv.close()
+    return ms
+
+
+def run(tags, n, scenario, rounds, auto_reset=True):
+    import torch
+
+    import drone2d_amd as d2
+
+    res = {t: [] for t in tags}
+    for r in range(rounds):
+        for t in tags:
+            res[t].append(time_variant(d2, torch, lib_for(t), n, scenario, auto_reset=auto_reset))
+    out = {t: {"ms_per_step_min": min(v), "ms_per_step_all": v} for t, v in res.items()}
+    out = {"envs": n, "scenario": scenario, "auto_reset": auto_reset, "variants": out}
+    print(json.dumps(out, indent=1))
+    os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(REPO, "gpurun_out", "variants.json"), "a") as f:
+        f.write(json.dumps(out) + "\n")
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("mode", choices=["build", "run"])
+    ap.add_argument("specs", nargs="+")
+    ap.add_argument("--envs", type=int, default=65536)
+    ap.add_argument("--scenario", default="corridor")
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--no-auto-reset", action="store_true")
+    a = ap.parse_args()
+    if a.mode == "build":
+        build(a.specs)
+    else:
+        run([s.partition(":")[0] for s in a.specs], a.envs, a.scenario, a.rounds, not a.no_auto_reset)
