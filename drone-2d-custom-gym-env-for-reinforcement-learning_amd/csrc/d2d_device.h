@@ -45,19 +45,55 @@ constexpr double DRONE_R = 40.0;              // Drone.py:11 (100/2 - 20/2)
 constexpr double FRAME_HX = 50.0, FRAME_HY = 5.0;   // Drone.py:16 box (100, 10)
 constexpr double VEL_MAX = 1330.0;            // drone_2d_env.py:635
 
-// Device-side scenario: the ABI table plus fields derived once in d2d_set_scenarios.
-// us[k >= n_wps] = +inf (unused knots never count in u_index);
-// inv_du[n] = RN(1 / (us[n+1] - us[n])) (only read where the blend case selects it).
-struct Scn : d2d_scn {
-    double inv_du[D2D_MAX_WPS];
+// Device-side scenario, built once from the ABI table (d2d_scn) by scn_build in d2d_set_scenarios.
+//   us[k >= n_wps] = +inf: unused knots never count in u_index.
+//   rec[.][n] = everything QPMI2D.__call__ needs once u's knot interval n is known, read from one
+//   per-lane base (field-major, so lanes in different intervals hit different LDS banks) instead
+//   of the scattered coefficient gathers: the "B" quadratic min(n, nseg-1), the "A" quadratic of
+//   the blend (n-1, or the last one for n = 0: Python's x_params[-1]), us[n], us[n+1] and
+//   RN(1 / (us[n+1] - us[n])).
+enum { REC_XB = 0, REC_XA = 6, REC_U0 = 12, REC_U1 = 13, REC_IDU = 14, REC_N = 15 };
+struct Scn {
+    int32_t n_wps, n_circles;
+    double us[D2D_MAX_WPS];
+    double rec[REC_N][D2D_MAX_WPS];
+    double cx[D2D_MAX_CIRCLES], cy[D2D_MAX_CIRCLES], cr[D2D_MAX_CIRCLES];
+    double wp_last_x, wp_last_y;
+    double spawn_xmin, spawn_xmax, spawn_ymin, spawn_ymax, spawn_amin, spawn_amax;
 };
-static_assert(sizeof(Scn) == sizeof(d2d_scn) + 8 * D2D_MAX_WPS, "Scn layout");
-__host__ __device__ inline void scn_derive(Scn& s) {
-    for (int k = s.n_wps; k < D2D_MAX_WPS; ++k) s.us[k] = __builtin_inf();
-    for (int k = 0; k < D2D_MAX_WPS; ++k) {
-        const int k1 = (k + 1 < D2D_MAX_WPS) ? k + 1 : D2D_MAX_WPS - 1;
-        s.inv_du[k] = 1.0 / (s.us[k1] - s.us[k]);
+// Returns false if the table is outside what the record form reproduces exactly: the last-segment
+// window us[nw-2] - 0.001 must not reach back past us[nw-3] (always true for real waypoints).
+inline bool scn_build(const d2d_scn& a, Scn& s) {
+    const int nw = a.n_wps, nseg = nw - 2;
+    if (nw >= 4 && !(a.us[nw - 2] - 0.001 > a.us[nw - 3])) return false;
+    s.n_wps = nw;
+    s.n_circles = a.n_circles;
+    for (int k = 0; k < D2D_MAX_WPS; ++k) s.us[k] = (k < nw) ? a.us[k] : __builtin_inf();
+    for (int n = 0; n < D2D_MAX_WPS; ++n) {
+        const int b = (n < nseg - 1) ? n : nseg - 1;
+        const int q = (n == 0) ? nseg - 1 : ((n - 1 < nseg - 1) ? n - 1 : nseg - 1);
+        const double v[REC_N] = {a.xa[b], a.xb[b], a.xc[b], a.ya[b], a.yb[b], a.yc[b],
+                                 a.xa[q], a.xb[q], a.xc[q], a.ya[q], a.yb[q], a.yc[q], 0.0, 0.0, 0.0};
+        for (int f = 0; f < REC_N; ++f) s.rec[f][n] = v[f];
+        const int n1 = (n + 1 < D2D_MAX_WPS) ? n + 1 : D2D_MAX_WPS - 1;
+        s.rec[REC_U0][n] = s.us[n];
+        s.rec[REC_U1][n] = s.us[n1];
+        s.rec[REC_IDU][n] = 1.0 / (s.us[n1] - s.us[n]);
     }
+    for (int k = 0; k < D2D_MAX_CIRCLES; ++k) {
+        s.cx[k] = a.cx[k];
+        s.cy[k] = a.cy[k];
+        s.cr[k] = a.cr[k];
+    }
+    s.wp_last_x = a.wp_last_x;
+    s.wp_last_y = a.wp_last_y;
+    s.spawn_xmin = a.spawn_xmin;
+    s.spawn_xmax = a.spawn_xmax;
+    s.spawn_ymin = a.spawn_ymin;
+    s.spawn_ymax = a.spawn_ymax;
+    s.spawn_amin = a.spawn_amin;
+    s.spawn_amax = a.spawn_amax;
+    return true;
 }
 // a / b correctly rounded from y = RN(1/b) (Markstein): q = RN(a*y) is within 1 ulp of a/b, the
 // residual a - q*b is exact under fma, and RN(q + r*y) == RN(a/b) for normal operands.  Three
@@ -65,6 +101,36 @@ __host__ __device__ inline void scn_derive(Scn& s) {
 __device__ __forceinline__ double div_by_recip(double a, double b, double y) {
     const double q = a * y;
     const double r = fma(-q, b, a);
+    return fma(r, y, q);
+}
+// Correctly rounded sqrt for x == 0 or 2^-767 <= x < inf: the device library's sequence (rsq
+// estimate + Goldschmidt/Newton refinement) without its range-scaling steps, which only act below
+// 2^-767.  Squared distances between fp64 points are 0 or far above that.  Checked bitwise against
+// sqrt() by d2d_selftest.
+__device__ __forceinline__ double sqrt_nz(double x) {
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y;
+    double h = 0.5 * y;
+    const double r = fma(-h, g, 0.5);
+    g = fma(g, r, g);
+    h = fma(h, r, h);
+    double d = fma(-g, g, x);
+    g = fma(d, h, g);
+    d = fma(-g, g, x);
+    g = fma(d, h, g);
+    return (x == 0.0) ? x : g;
+}
+// Correctly rounded a / b for normal operands with a normal quotient (no div_scale / div_fixup
+// range handling: results for zero / inf / NaN / extreme-exponent operands are unspecified).
+// Checked bitwise against '/' by d2d_selftest.
+__device__ __forceinline__ double div_normal(double a, double b) {
+    double y = __builtin_amdgcn_rcp(b);
+    double e = fma(-b, y, 1.0);
+    y = fma(y, e, y);
+    e = fma(-b, y, 1.0);
+    y = fma(y, e, y);
+    const double q = a * y;
+    const double r = fma(-b, q, a);
     return fma(r, y, q);
 }
 
@@ -141,57 +207,57 @@ __device__ __forceinline__ void spawn_draw(const Scn& s, uint64_t seed, uint32_t
 // ------------------------------------------------------------------------------ QPMI2D path
 // get_u_index (predef_path.py:53-63): first n with u <= us[n+1]; for non-decreasing knots this is
 // the number of knots k >= 1 with !(u <= us[k]) (NaN -> n_wps-1, as the Python loop).
-// The device table pads us[k >= n_wps] with +inf (scn_derive), so those knots never count for a
-// non-NaN u; the min() maps NaN (every comparison false) to n_wps - 1 as the Python loop does.
-// `kmax` is a wave-uniform bound on n_wps (the loop stops early when all lanes share a scenario).
-__device__ __forceinline__ int u_index(const Scn& s, double u, int kmax) {
-    int n = 0;
+// The knots are counted from the sign bit of (us[k] - u): that difference is negative exactly when
+// u > us[k] (equal values give +0), padded +inf knots give +inf (u finite) or NaN (u = +inf, sign
+// clear), and u = -inf gives +inf -- the Python loop's counts in every case; NaN u maps to
+// n_wps - 1 as the loop does.  No compare masks, so the 15 knot tests issue back to back.
+#ifndef D2D_KNOT_CMP
+#define D2D_KNOT_CMP 1   // 1: compares (measured faster in the full kernel), 0: sign bits (faster alone)
+#endif
+__device__ __forceinline__ int u_index(const Scn& s, double u) {
+    uint32_t c = 0;
 #pragma unroll
     for (int k = 1; k < D2D_MAX_WPS; ++k) {
-        if (k < kmax) n += !(u <= s.us[k]) ? 1 : 0;
+        if (D2D_KNOT_CMP) c += !(u <= s.us[k]) ? 1u : 0u;
+        else c += (uint32_t)__double2hiint(s.us[k] - u) >> 31;
     }
-    return min(n, s.n_wps - 1);
-}
-__device__ __forceinline__ int u_index(const Scn& s, double u) { return u_index(s, u, D2D_MAX_WPS); }
-// wave-uniform upper bound on the knot count of the active lanes' scenarios
-__device__ __forceinline__ int wave_knots(const Scn& s) {
-    const int nw = s.n_wps;
-    const int f = __builtin_amdgcn_readfirstlane(nw);
-    return (__ballot(nw != f) == 0) ? f : D2D_MAX_WPS;
+    const int nw1 = s.n_wps - 1;
+    return (u != u) ? nw1 : min((int)c, nw1);
 }
 // loop invariants of path_eval (hoisted out of the Brent loop)
 struct PathK {
-    double us0, us1, last_lo, L;
-    int nw, kmax;
+    double us0, last_lo, L;
+    int nw;
 };
 __device__ __forceinline__ PathK path_k(const Scn& s) {
     const int nw = s.n_wps;
-    return PathK{s.us[0], s.us[1], s.us[nw - 2] - 0.001, s.us[nw - 1], nw, wave_knots(s)};
+    return PathK{s.us[0], s.us[nw - 2] - 0.001, s.us[nw - 1], nw};
 }
 // QPMI2D.__call__ (predef_path.py:88-142), branch-free: both candidate quadratics are evaluated
 // and the reference's case analysis picks the result with selects (same arithmetic per case).
-// Conditions combine with non-short-circuit & / | so the compiler emits selects, not branches.
+// first <=> n == 0 && u >= us[0];  last <=> u in [us[nw-2] - 0.001, L] or n == nw-1, and in every
+// first / last case the record's "B" quadratic is the one the reference uses (scn_build).
 __device__ __forceinline__ void path_eval(const Scn& s, const PathK& K, double u, double& x, double& y) {
-    const int nw = K.nw, nseg = nw - 2;
-    const int n = u_index(s, u, K.kmax);
-    const bool first = (u >= K.us0) & (u <= K.us1);
+    const int nw = K.nw;
+    const int n = u_index(s, u);
+    double r[REC_N];
+#pragma unroll
+    for (int f = 0; f < REC_N; ++f) r[f] = s.rec[f][n];
+    const bool first = (n == 0) & (u >= K.us0);
     const bool last = !first & (((u >= K.last_lo) & (u <= K.L)) | (n == nw - 1));
     const bool blend = !first & !last;
-    const int kb = first ? 0 : (last ? nseg - 1 : n);
-    const int ka = (n == 0) ? nseg - 1 : n - 1;  // python x_params[n-1]
-    const int n1 = (n + 1 < D2D_MAX_WPS) ? n + 1 : D2D_MAX_WPS - 1;
-    const double u0 = s.us[n], u1 = s.us[n1];
     const double uu = u * u;
-    const double xB = s.xa[kb] * uu + s.xb[kb] * u + s.xc[kb];
-    const double yB = s.ya[kb] * uu + s.yb[kb] * u + s.yc[kb];
-    const int kas = blend ? ka : kb;
-    const double xA = s.xa[kas] * uu + s.xb[kas] * u + s.xc[kas];
-    const double yA = s.ya[kas] * uu + s.yb[kas] * u + s.yc[kas];
-    const double du = u1 - u0, idu = s.inv_du[n];
+    const double xB = r[REC_XB + 0] * uu + r[REC_XB + 1] * u + r[REC_XB + 2];
+    const double yB = r[REC_XB + 3] * uu + r[REC_XB + 4] * u + r[REC_XB + 5];
+    const double xA = r[REC_XA + 0] * uu + r[REC_XA + 1] * u + r[REC_XA + 2];
+    const double yA = r[REC_XA + 3] * uu + r[REC_XA + 4] * u + r[REC_XA + 5];
+    const double u0 = r[REC_U0], u1 = r[REC_U1], idu = r[REC_IDU];
+    const double du = u1 - u0;
     const double mu_r = div_by_recip(u - u0, du, idu);   // (u - u0) / (u1 - u0)
     const double mu_f = div_by_recip(u1 - u, du, idu);   // (u1 - u) / (u1 - u0)
-    x = blend ? mu_r * xB + mu_f * xA : xB;
-    y = blend ? mu_r * yB + mu_f * yA : yB;
+    const double xb = mu_r * xB + mu_f * xA, yb = mu_r * yB + mu_f * yA;
+    x = blend ? xb : xB;
+    y = blend ? yb : yB;
 }
 __device__ __forceinline__ void path_eval(const Scn& s, double u, double& x, double& y) {
     path_eval(s, path_k(s), u, x, y);
@@ -199,6 +265,7 @@ __device__ __forceinline__ void path_eval(const Scn& s, double u, double& x, dou
 __device__ __forceinline__ double path_dist(const Scn& s, const PathK& K, double u, double px, double py) {
     double x, y;
     path_eval(s, K, u, x, y);
+    // (sqrt_nz measured slower here than the library sequence: tools/ubench_brent.py)
     return norm2(x - px, y - py);
 }
 // get_closest_u (predef_path.py:226-248) = scipy fminbound(x1=-10, x2=L+10, xtol=1e-6, maxfun=500),
@@ -246,7 +313,8 @@ __device__ __forceinline__ void brent_step(const Scn& s, const PathK& K, double 
     p = (q > 0.0) ? -p : p;
     q = fabs(q);
     const bool par = (fabs(B.e) > tol1) & (fabs(p) < fabs(0.5 * q * B.e)) & (p > q * (a - xf)) & (p < q * (b - xf));
-    double rat_p = (p + 0.0) / q;
+    // only used when `par` holds: then q > 0 and |p / q| < |e| / 2, a normal quotient
+    double rat_p = div_normal(p + 0.0, q);
     const double xp = xf + rat_p;
     rat_p = (((xp - a) < tol2) | ((b - xp) < tol2)) ? tol1 * sgn_nz(xm - xf) : rat_p;
     // golden-section candidate
@@ -718,6 +786,52 @@ __device__ __forceinline__ Reward reward_final(const d2d_cfg& cfg, const Body& F
     R.dclose = P.dclose;
     R.cause = cause;
     return R;
+}
+
+// reward_final split at its data dependencies, for the cooperative kernel: the part that needs only
+// the post-step frame and the CA part (known long before the path search ends) ...
+struct RewardPre {
+    double aa, lpa, coll, cal, reach, sv, vel_ang, pxd, pyd;
+};
+__device__ __forceinline__ RewardPre reward_pre(const d2d_cfg& cfg, const Body& F, const CAPart& P, int cause) {
+    const double W = cfg.screen_w, H = cfg.screen_h;
+    RewardPre R;
+    const double vxd = invm1to1(m1to1(F.vx, -VEL_MAX, VEL_MAX), -VEL_MAX, VEL_MAX);
+    const double vyd = invm1to1(m1to1(F.vy, -VEL_MAX, VEL_MAX), -VEL_MAX, VEL_MAX);
+    const double alpha = (F.a / PI) * PI;
+    R.pxd = invm1to1(m1to1(F.px, 0.0, W), 0.0, W);
+    R.pyd = invm1to1(m1to1(F.py, 0.0, H), 0.0, H);
+    const double vel = sqrt(vxd * vxd + vyd * vyd);
+    R.sv = vel * cfg.pp_vel_scale;
+    R.coll = (cause & D2D_END_COLLISION) ? cfg.rew_collision : 0.0;
+    R.reach = (cause & D2D_END_REACH) ? cfg.rew_reach_end : 0.0;
+    double aa = 0.0;
+    if (alpha > cfg.aa_band) aa = -sin(alpha);
+    if (alpha < -cfg.aa_band) aa = sin(alpha);
+    if (cause & D2D_END_AA) aa = cfg.rew_aa;
+    R.aa = aa;
+    R.lpa = P.lpa;
+    R.cal = P.ca * P.lca;
+    R.vel_ang = P.vel_ang;
+    return R;
+}
+// ... and the part that needs the path observation (po = obs 19..26).  Same arithmetic and the
+// same summation order as reward_final.
+struct RewardPost {
+    double reward, pa, pp, dist;
+};
+__device__ __forceinline__ RewardPost reward_post(const d2d_cfg& cfg, const RewardPre& R, const double* po) {
+    const double W = cfg.screen_w, H = cfg.screen_h;
+    RewardPost Q;
+    const double cpx = invm1to1(po[0], 0.0, W), cpy = invm1to1(po[1], 0.0, H);
+    const double la_ang = pymod_2pi(atan2(po[4], po[5]) + TWO_PI);
+    Q.dist = norm2(cpx - R.pxd, cpy - R.pyd);
+    const double pa = -(2.0 * (clipd(Q.dist, 0.0, cfg.pa_band_edge) / cfg.pa_band_edge) - 1.0) * cfg.pa_scale;
+    const double vla = fabs(pymod_2pi(la_ang - R.vel_ang + PI) - PI);
+    Q.pp = clipd(cos(vla) * R.sv, cfg.pp_rew_min, cfg.pp_rew_max);
+    Q.pa = pa * R.lpa;
+    Q.reward = R.aa + Q.pa + Q.pp + R.coll + R.cal + R.reach;
+    return Q;
 }
 
 // full single-lane observation (reset kernel)

@@ -174,8 +174,8 @@ int32_t d2d_set_scenarios(d2d_t* h, const d2d_scn* scns, int32_t n_scn, const in
     }
     std::vector<d2d::Scn> tab((size_t)n_scn);
     for (int k = 0; k < n_scn; ++k) {
-        static_cast<d2d_scn&>(tab[k]) = scns[k];
-        d2d::scn_derive(tab[k]);
+        if (!d2d::scn_build(scns[k], tab[k]))
+            return fail(D2D_E_ARG, "d2d_set_scenarios: us[n_wps-2] - us[n_wps-3] must exceed 0.001");
     }
     const size_t bytes = sizeof(d2d::Scn) * (size_t)n_scn;
     if ((e = hipMalloc(&h->scn, bytes)) != hipSuccess) return hip_fail(e, "hipMalloc scn");
@@ -204,7 +204,7 @@ int32_t d2d_reset(d2d_t* h, const uint8_t* mask_dev, uint64_t seed, float* obs_d
     a.obs = obs_dev;
     a.mask = mask_dev;
     const dim3 grid((h->n + BLOCK - 1) / BLOCK);
-    if (h->n_scn <= MAX_LDS_SCN)
+    if (sizeof(d2d::Scn) * (size_t)h->n_scn <= K2_LDS_BUDGET)
         hipLaunchKernelGGL(d2d_reset_kernel<true>, grid, dim3(BLOCK), sizeof(d2d::Scn) * h->n_scn, (hipStream_t)stream, a);
     else
         hipLaunchKernelGGL(d2d_reset_kernel<false>, grid, dim3(BLOCK), 0, (hipStream_t)stream, a);
@@ -230,7 +230,7 @@ int32_t d2d_step(d2d_t* h, const float* act_dev, float* obs_dev, float* rew_dev,
     a.info = info_dev;
     a.tobs = term_obs_dev;
     const dim3 grid((h->n + EPB - 1) / EPB);
-    if (h->n_scn <= MAX_LDS_SCN)
+    if (sizeof(d2d::Scn) * (size_t)h->n_scn + sizeof(K1Shared) <= K1_LDS_BUDGET)
         hipLaunchKernelGGL(d2d_step_kernel<true>, grid, dim3(K1_THREADS), sizeof(d2d::Scn) * h->n_scn, (hipStream_t)stream, a);
     else
         hipLaunchKernelGGL(d2d_step_kernel<false>, grid, dim3(K1_THREADS), 0, (hipStream_t)stream, a);
@@ -280,6 +280,22 @@ int32_t d2d_episode_stats(d2d_t* h, double* out_dev, int32_t clear, void* stream
                        out_dev, clear, h->acc);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "d2d_episode_stats launch");
+    return D2D_OK;
+}
+
+int32_t d2d_selftest(int32_t which, int64_t n, uint64_t seed, uint64_t* mismatches) {
+    if (!mismatches || n < 0 || which < 0 || which > 2) return fail(D2D_E_ARG, "d2d_selftest: bad arguments");
+    unsigned long long* bad = nullptr;
+    hipError_t e;
+    if ((e = hipMalloc(&bad, sizeof(unsigned long long))) != hipSuccess) return hip_fail(e, "d2d_selftest alloc");
+    (void)hipMemset(bad, 0, sizeof(unsigned long long));
+    hipLaunchKernelGGL(d2d_selftest_kernel, dim3(2048), dim3(256), 0, 0, which, (long long)n, seed, bad);
+    e = hipGetLastError();
+    unsigned long long h = 0;
+    if (e == hipSuccess) e = hipMemcpy(&h, bad, sizeof(h), hipMemcpyDeviceToHost);
+    (void)hipFree(bad);
+    if (e != hipSuccess) return hip_fail(e, "d2d_selftest");
+    *mismatches = (uint64_t)h;
     return D2D_OK;
 }
 

@@ -1,4 +1,4 @@
-// d2d_kernels.h -- the three kernels of libdrone2d_hip.so (included by d2d_hip.hip).
+// d2d_kernels.h -- the kernels of libdrone2d_hip.so (included by d2d_hip.hip).
 //
 // K1 d2d_step_kernel (cooperative, wave-specialised).  One 256-lane workgroup owns 64 envs (one
 // per lane index); its four waves split one env step by role so that the long, independent fp64
@@ -6,20 +6,19 @@
 // only on its pre-step position and velocity (forces act on velocities), so every wave derives it
 // from the state in HBM and no wave waits for another before its own chain:
 //
-//   phase A  W0: load state, thrust, 3-body position update, collision, end cause, 6-pivot joint
-//                sweep, store the state, velocity part of the observation (obs 0-2, 17-18)
-//            W1: frame position -> sensor part (obs 3..16); for envs that end: spawn + full sensor
-//            W2: frame position -> path role (Brent closest point, obs 19..26)
-//            W3: for envs that end: spawn -> path role on the spawn state (auto-reset observation)
-//            W1 and W3 also fill the auto-reset observation cache (below) while W2 searches
-//   phase B  every role writes its columns of the workgroup's obs tile to LDS (the tile shares LDS
-//            with W0's joint constants, hence the barrier between A and B)
-//   phase C  all: store the 64x27 f32 tile as one contiguous span; W0: CA part, reward,
-//            bookkeeping, auto-reset state writes
+//   W0  load state, thrust, 3-body position update, collision, end cause, 6-pivot joint sweep,
+//       store the state; velocity part of the observation (obs 0-2, 17-18); frame / CA part of
+//       the reward
+//   W1  sensor part (obs 3..16, CA inputs); for envs that end: the spawn-state sensor part
+//   W2  path role: Brent closest point, obs 19..26, then the path part of the reward
+//   W3  end test first (for W2), then for envs that end: the spawn-state path part
+//   W1 and W3 then fill the auto-reset observation cache (below) while W2 is still searching.
+//   epilogue (after the one barrier): the 64x27 f32 obs tile is stored as one contiguous span;
+//   W0 writes reward / flags / info / bookkeeping / auto-reset state.
 //
-// The critical path is W2's Brent search; the joint sweep, the sensing and the auto-reset roles
-// run under it.  At 65 536 envs this is 1 024 workgroups = 4 per CU = 4 waves per SIMD
-// (VGPR <= 128, LDS <= 40 KB even with 7 scenario tables).
+// The critical path is W2's Brent search (highest wave priority); everything else runs under it.
+// At 65 536 envs this is 1 024 workgroups = 4 per CU = 4 waves per SIMD (VGPR <= 128, LDS <= 40 KB
+// even with 7 scenario tables).
 //
 // K2 d2d_reset_kernel: masked reset, one lane per env.  K3 d2d_stats_kernel: fixed-order reduction.
 #pragma once
@@ -31,7 +30,10 @@ using namespace d2d;
 constexpr int BLOCK = 256;      // K2 / K3 workgroup
 constexpr int EPB = 64;         // K1: envs per workgroup
 constexpr int K1_THREADS = 256; // K1: 4 waves
-constexpr int MAX_LDS_SCN = 8;
+// scenario tables go to LDS when they fit next to K1's own LDS within the 4-workgroups-per-CU
+// budget (160 KB / 4); larger sets are read from global memory (L1/L2 resident)
+constexpr size_t K1_LDS_BUDGET = 40 * 1024;
+constexpr size_t K2_LDS_BUDGET = 64 * 1024;
 // Wave priorities per role (s_setprio, 0..3) for phase A: the Brent waves win issue arbitration
 // on their SIMD over the other workgroups' physics / sensing waves.
 #ifndef D2D_PRIO_W0
@@ -84,6 +86,12 @@ struct StepArgs {
 // priority and suspends it (state in rc_bs) as soon as W2 finishes the step's own search, so the
 // fill never lengthens a step; an env that ends before its entry is ready falls back to the
 // synchronous computation.  Entries are invalidated by every reset / set_state.
+#ifndef D2D_RC_FILL
+#define D2D_RC_FILL 1    // diagnostic builds may disable W3's path-part fill (fallback only)
+#endif
+#ifndef D2D_RC_SLEEP
+#define D2D_RC_SLEEP 0   // s_sleep (x64 cycles) between W3 fill iterations
+#endif
 constexpr int RC_NB = 10;             // a, b, fulc, ffulc, nfc, fnfc, xf, fx, rat, e
 constexpr int RC_PST = 0, RC_SST = 1, RC_NUM = 2, RC_RFLAGS = 3, RC_NI = 4;
 constexpr int RC_BRENT = 1, RC_UDONE = 2, RC_PATH = 4;   // path status bits (sensor status: 0 / 1)
@@ -195,6 +203,7 @@ __device__ __forceinline__ void rc_fill_path(const StepArgs& a, const Scn& S, in
     }
     bool act = need && !(pst & RC_UDONE) && brent_active(B);
     while (__ballot(act) != 0 && !stop_seen(stop)) {
+        if (D2D_RC_SLEEP) __builtin_amdgcn_s_sleep(D2D_RC_SLEEP);  // leave issue slots to W2
         if (act) {
             brent_step(S, K, x, y, B);
             act = brent_active(B);
@@ -231,21 +240,39 @@ __device__ __forceinline__ void rc_fill_path(const StepArgs& a, const Scn& S, in
 }
 
 // ------------------------------------------------------------------------------------------ K1
+// Intra-workgroup hand-offs are LDS flags (raised after a release fence, polled with s_sleep), so
+// no wave waits at a barrier for work it does not depend on.  Dependencies (all acyclic):
+//   f_done  W3 -> W2        which envs end this step (W3 derives it first thing)
+//   f_ca    W1 -> W0        obs 8..10 for the CA reward part
+//   f_gs    W0 -> W1,W2,W3  joint sweep finished: the jb region becomes the obs tile
+//   f_pre   W0 -> W2        frame/velocity/CA part of the reward
+//   stop    W2 -> W1,W3     own path search finished: cache fills stop
 struct K1Shared {
     double sp[7][EPB];        // W3 -> W0: next-episode spawn of envs that end
+    double cao[3][EPB];       // W1 -> W0: obs 8, 9, 10 (fp64)
     int scn[EPB];             // scenario index per env
+    uint32_t done[EPB];       // W3 -> W2: env ends this step
     uint32_t pflags[EPB];     // W2 -> W0: LA-lock bit after the path role
     uint32_t rflags[EPB];     // W3 -> W0: flags of the reset observation
-    uint32_t stop;            // W2 -> W1, W3: the step's own Brent search is finished
+    uint32_t f_done, f_ca, f_gs, f_pre, stop;
     union {
-        double jb[6 * JB_PER_JOINT][EPB];  // phase A: W0's per-joint K^-1 + bias, re-read every sweep
+        double jb[6 * JB_PER_JOINT][EPB];  // W0's joint sweep: per-joint K^-1 + bias
         struct {
-            double ca[3][EPB];             // W1 -> W0: obs 8, 9, 10 (fp64) for the CA reward part
-            double po[4][EPB];             // W2 -> W0: obs 19, 20, 23, 24 (fp64) for the reward
+            double pre[9][EPB];            // W0 -> W2: RewardPre
+            double post[4][EPB];           // W2 -> W0: RewardPost
             float obs[EPB * D2D_OBS_DIM];  // the workgroup's obs rows
-        } p;                               // phases B, C
+        } p;                               // after f_gs
     } u;
 };
+
+__device__ __forceinline__ void flag_raise(uint32_t& f) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if ((threadIdx.x & 63) == 0) *(volatile LdsU32*)&f = 1u;
+}
+__device__ __forceinline__ void flag_wait(const uint32_t& f) {
+    while (!stop_seen(f)) __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
 
 template <bool LDS>
 __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
@@ -262,24 +289,31 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
     STAMP(0);
     const Scn* scns = stage_scenarios<LDS, K1_THREADS>(a, s_scn);
     if (wave == 0) sh.scn[lane] = (valid && a.env_scn && a.n_scn > 1) ? a.env_scn[i] : 0;
-    if (threadIdx.x == 0) sh.stop = 0u;
+    if (threadIdx.x == 0) {
+        sh.f_done = 0u;
+        sh.f_ca = 0u;
+        sh.f_gs = 0u;
+        sh.f_pre = 0u;
+        sh.stop = 0u;
+    }
     __syncthreads();
     STAMP(1);
     const Scn& S = scns[sh.scn[lane]];
     float* const trow = a.tobs ? a.tobs + (size_t)i * D2D_OBS_DIM : nullptr;
+    float* const orow = &sh.u.p.obs[lane * D2D_OBS_DIM];
 
-    // ---------------------------------------------------------------- phase A
-    // W0 results kept for phase C
+    // W0 results kept for the epilogue
     Body F0{};
-    double path_err = 0.0, tot_rew = 0.0, ov[19];
+    double path_err = 0.0, tot_rew = 0.0;
     int t = 0, cause = 0;
     uint32_t flags = 0;
-    // W1 / W2 / W3 results written to the tile in phase B
-    float row[19];
-    double cao[3] = {0.0, 0.0, 0.0}, po[8];
+    RewardPre RP{};
+    double dclose = 0.0;
     bool done = false;
     if (wave == 0) {
+        // ---------------------------------------------------------------- physics
         D2D_SETPRIO(D2D_PRIO_W0);
+        double ov[19];
         if (valid) {
             Body B[3];
             double j[12];
@@ -311,7 +345,7 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
             const double pos[6] = {B[0].px, B[0].py, B[1].px, B[1].py, B[2].px, B[2].py};
             double vel[9] = {B[0].vx, B[0].vy, B[0].w, B[1].vx, B[1].vy, B[1].w, B[2].vx, B[2].vy, B[2].w};
             phys_velocities<true>(A, pos, a.damping_dt, fx, fy, tq, vel, j, &sh.u.jb[0][lane], EPB);
-            // envs that end are overwritten with their spawn state in phase C
+            // envs that end are overwritten with their spawn state in the epilogue
 #pragma unroll
             for (int b = 0; b < 3; ++b) {
                 fld(a.st, 6 * b + 0, n, i) = B[b].px;
@@ -324,8 +358,19 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
 #pragma unroll
             for (int k = 0; k < 12; ++k) fld(a.st, D2D_S_J + k, n, i) = j[k];
             F0 = Body{B[0].px, B[0].py, B[0].a, vel[0], vel[1], vel[2]};
-            sensor_vel(F0, ov);
             done = cause != 0;
+        }
+        flag_raise(sh.f_gs);
+        // velocity part of the observation (obs 0-2, 17-18) into the tile / terminal obs
+        if (valid) {
+            sensor_vel(F0, ov);
+            if (!(done && auto_reset)) {
+                orow[0] = (float)ov[0];
+                orow[1] = (float)ov[1];
+                orow[2] = (float)ov[2];
+                orow[17] = (float)ov[17];
+                orow[18] = (float)ov[18];
+            }
             if (done && trow) {
                 trow[0] = (float)ov[0];
                 trow[1] = (float)ov[1];
@@ -334,19 +379,40 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
                 trow[18] = (float)ov[18];
             }
         }
+        // frame / velocity / CA part of the reward, for W2
+        flag_wait(sh.f_ca);
+        if (valid) {
+            ov[8] = sh.cao[0][lane];
+            ov[9] = sh.cao[1][lane];
+            ov[10] = sh.cao[2][lane];
+            const CAPart P = reward_ca_part(a.cfg, S, ov);
+            RP = reward_pre(a.cfg, F0, P, cause);
+            sh.u.p.pre[0][lane] = RP.aa;
+            sh.u.p.pre[1][lane] = RP.lpa;
+            sh.u.p.pre[2][lane] = RP.coll;
+            sh.u.p.pre[3][lane] = RP.cal;
+            sh.u.p.pre[4][lane] = RP.reach;
+            sh.u.p.pre[5][lane] = RP.sv;
+            sh.u.p.pre[6][lane] = RP.vel_ang;
+            sh.u.p.pre[7][lane] = RP.pxd;
+            sh.u.p.pre[8][lane] = RP.pyd;
+            dclose = P.dclose;
+        }
+        flag_raise(sh.f_pre);
     } else if (wave == 1) {
-        // sensor role
+        // ---------------------------------------------------------------- sensing
         D2D_SETPRIO(D2D_PRIO_W1);
         int32_t sst = 0;
+        float row[19];
         if (valid) {
             Body F = load_frame(a, i);
             done = step_cause(a, S, i, F) != 0;
             if (auto_reset) sst = fld(a.rc_i, RC_SST, n, i);
             double so[19];
             sensor_pos(a.cfg, S, F.px, F.py, F.a, so);
-            cao[0] = so[8];
-            cao[1] = so[9];
-            cao[2] = so[10];
+            sh.cao[0][lane] = so[8];
+            sh.cao[1][lane] = so[9];
+            sh.cao[2][lane] = so[10];
             if (done && trow) {
 #pragma unroll
                 for (int k = 3; k < 17; ++k) trow[k] = (float)so[k];
@@ -367,6 +433,18 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
                 for (int k = 0; k < 19; ++k) row[k] = (float)so[k];
             }
         }
+        flag_raise(sh.f_ca);
+        flag_wait(sh.f_gs);
+        if (valid) {
+            // a reset row holds the whole spawn-state sensor part, otherwise obs 3..16
+            if (done && auto_reset) {
+#pragma unroll
+                for (int k = 0; k < 19; ++k) orow[k] = row[k];
+            } else {
+#pragma unroll
+                for (int k = 3; k < 17; ++k) orow[k] = row[k];
+            }
+        }
         // cache fill: spawn-state sensor part of the next reset of envs that keep running, started
         // only while W2's search is still running
         __builtin_amdgcn_s_setprio(0);
@@ -382,8 +460,10 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
             }
         }
     } else if (wave == 2) {
-        // path role on the current state: the critical path, so it wins issue arbitration on its SIMD
+        // ---------------------------------------------------------------- path search (critical)
+        // the critical path, so it wins issue arbitration on its SIMD
         D2D_SETPRIO(D2D_PRIO_W2);
+        double po[8];
         if (valid) {
             Body F = load_frame(a, i);
             advance_position(F);
@@ -391,14 +471,50 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
             path_obs(a.cfg, S, F.px, F.py, F.a, f, po);
             sh.pflags[lane] = f & D2D_FLAG_LA_LOCK;
         }
-        if (lane == 0) stop_raise(sh.stop);
+        stop_raise(sh.stop);
+        flag_wait(sh.f_done);
+        flag_wait(sh.f_gs);
+        if (valid) {
+            const bool d = sh.done[lane] != 0u;
+            if (!(d && auto_reset)) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) orow[19 + k] = (float)po[k];
+            }
+            if (d && trow) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) trow[19 + k] = (float)po[k];
+            }
+        }
+        flag_wait(sh.f_pre);
+        if (valid) {
+            RewardPre R;
+            R.aa = sh.u.p.pre[0][lane];
+            R.lpa = sh.u.p.pre[1][lane];
+            R.coll = sh.u.p.pre[2][lane];
+            R.cal = sh.u.p.pre[3][lane];
+            R.reach = sh.u.p.pre[4][lane];
+            R.sv = sh.u.p.pre[5][lane];
+            R.vel_ang = sh.u.p.pre[6][lane];
+            R.pxd = sh.u.p.pre[7][lane];
+            R.pyd = sh.u.p.pre[8][lane];
+            const RewardPost Q = reward_post(a.cfg, R, po);
+            sh.u.p.post[0][lane] = Q.reward;
+            sh.u.p.post[1][lane] = Q.pa;
+            sh.u.p.post[2][lane] = Q.pp;
+            sh.u.p.post[3][lane] = Q.dist;
+        }
     } else {
-        // path role on the spawn state of envs that end (auto-reset observation)
+        // ---------------------------------------------------------------- auto-reset observation
         D2D_SETPRIO(D2D_PRIO_W3);
         int32_t pst = 0;
+        double po[8];
         if (valid) {
             Body F = load_frame(a, i);
             done = step_cause(a, S, i, F) != 0;
+            sh.done[lane] = done ? 1u : 0u;
+        }
+        flag_raise(sh.f_done);
+        if (valid) {
             if (auto_reset) pst = fld(a.rc_i, RC_PST, n, i);
             if (done && auto_reset) {
                 double sp[7];
@@ -418,62 +534,18 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
                 fld(a.rc_i, RC_PST, n, i) = 0;
             }
         }
-        if (auto_reset) rc_fill_path(a, S, i, valid && !done && !(pst & RC_PATH), pst, sh.stop);
+        flag_wait(sh.f_gs);
+        if (valid && done && auto_reset) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) orow[19 + k] = (float)po[k];
+        }
+        if (auto_reset && D2D_RC_FILL) rc_fill_path(a, S, i, valid && !done && !(pst & RC_PATH), pst, sh.stop);
     }
     STAMP(2);
     __syncthreads();
     STAMP(3);
 
-    // ---------------------------------------------------------------- phase B: obs tile
-    float* orow = &sh.u.p.obs[lane * D2D_OBS_DIM];
-    if (valid) {
-        if (wave == 0) {
-            if (!(done && auto_reset)) {
-                orow[0] = (float)ov[0];
-                orow[1] = (float)ov[1];
-                orow[2] = (float)ov[2];
-                orow[17] = (float)ov[17];
-                orow[18] = (float)ov[18];
-            }
-        } else if (wave == 1) {
-            // a reset row holds the whole spawn-state sensor part, otherwise obs 3..16
-            if (done && auto_reset) {
-#pragma unroll
-                for (int k = 0; k < 19; ++k) orow[k] = row[k];
-            } else {
-#pragma unroll
-                for (int k = 3; k < 17; ++k) orow[k] = row[k];
-            }
-            sh.u.p.ca[0][lane] = cao[0];
-            sh.u.p.ca[1][lane] = cao[1];
-            sh.u.p.ca[2][lane] = cao[2];
-        } else if (wave == 2) {
-            // every row gets the current-state path part; W3 replaces it on reset rows below
-            sh.u.p.po[0][lane] = po[0];
-            sh.u.p.po[1][lane] = po[1];
-            sh.u.p.po[2][lane] = po[4];
-            sh.u.p.po[3][lane] = po[5];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) orow[19 + k] = (float)po[k];
-        }
-    }
-    STAMP(4);
-    __syncthreads();
-    // W3 (which knows which envs end): terminal-obs copy of the path part, then the reset row
-    if (wave == 3 && valid && done) {
-        if (trow) {
-#pragma unroll
-            for (int k = 19; k < 27; ++k) trow[k] = orow[k];
-        }
-        if (auto_reset) {
-#pragma unroll
-            for (int k = 0; k < 8; ++k) orow[19 + k] = (float)po[k];
-        }
-    }
-    __syncthreads();
-    STAMP(5);
-
-    // ---------------------------------------------------------------- phase C
+    // ---------------------------------------------------------------- epilogue
     // obs tile: rows [e0, e0+rows) are one contiguous span of global memory
     {
         const int rows = min(EPB, n - e0);
@@ -483,41 +555,32 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
     }
     if (wave == 0 && valid) {
         flags = (flags & ~D2D_FLAG_LA_LOCK) | sh.pflags[lane];
-        ov[8] = sh.u.p.ca[0][lane];
-        ov[9] = sh.u.p.ca[1][lane];
-        ov[10] = sh.u.p.ca[2][lane];
-        const CAPart P = reward_ca_part(a.cfg, S, ov);
-        double pw[8];
-        pw[0] = sh.u.p.po[0][lane];
-        pw[1] = sh.u.p.po[1][lane];
-        pw[4] = sh.u.p.po[2][lane];
-        pw[5] = sh.u.p.po[3][lane];
-        const Reward R = reward_final(a.cfg, F0, pw, P, cause);
-        path_err += R.dist_path;
+        const double reward = sh.u.p.post[0][lane];
+        path_err += sh.u.p.post[3][lane];
         const double ape = path_err / (double)t;
-        tot_rew += R.reward;
+        tot_rew += reward;
         bool trunc = false, term = done;
         if (a.cfg.timeup_truncates && done && cause == D2D_END_TIMEUP) {
             trunc = true;
             term = false;
         }
-        a.rew[i] = (float)R.reward;
+        a.rew[i] = (float)reward;
         a.term[i] = (uint8_t)term;
         a.trunc[i] = (uint8_t)trunc;
         if (a.info) {
             float* r = a.info + (size_t)i * D2D_INFO_DIM;
-            r[D2D_INFO_CA] = (float)R.ca;
-            r[D2D_INFO_PA] = (float)R.pa;
-            r[D2D_INFO_PP] = (float)R.pp;
-            r[D2D_INFO_COLL] = (float)R.coll;
-            r[D2D_INFO_REACH] = (float)R.reach;
-            r[D2D_INFO_AA] = (float)R.aa;
-            r[D2D_INFO_DCLOSE] = (float)R.dclose;
+            r[D2D_INFO_CA] = (float)RP.cal;
+            r[D2D_INFO_PA] = (float)sh.u.p.post[1][lane];
+            r[D2D_INFO_PP] = (float)sh.u.p.post[2][lane];
+            r[D2D_INFO_COLL] = (float)RP.coll;
+            r[D2D_INFO_REACH] = (float)RP.reach;
+            r[D2D_INFO_AA] = (float)RP.aa;
+            r[D2D_INFO_DCLOSE] = (float)dclose;
             r[D2D_INFO_STEPS] = (float)t;
             r[D2D_INFO_CAUSE] = (float)cause;
             r[D2D_INFO_APE] = done ? (float)ape : 0.0f;
             r[D2D_INFO_TOTREW] = done ? (float)tot_rew : 0.0f;
-            r[D2D_INFO_REWARD] = (float)R.reward;
+            r[D2D_INFO_REWARD] = (float)reward;
         }
         if (done) {
             // finished-episode accumulators (info counters of drone_2d_env.py:593-613)
@@ -586,6 +649,38 @@ __global__ __launch_bounds__(BLOCK) void d2d_reset_kernel(StepArgs a) {
 #pragma unroll
         for (int k = 0; k < D2D_OBS_DIM; ++k) a.obs[(size_t)i * D2D_OBS_DIM + k] = (float)obs[k];
     }
+}
+
+// ------------------------------------------------------------------------------------ self-test
+// random fp64 with a biased exponent in [emin, emax] and 52 random mantissa bits
+__device__ __forceinline__ double st_rand(uint32_t hi, uint32_t lo, int emin, int emax, uint32_t sign) {
+    const uint32_t span = (uint32_t)(emax - emin + 1);
+    const uint64_t ex = (uint64_t)(emin + (int)((hi >> 20) % span));
+    const uint64_t bits = ((uint64_t)(sign & 1u) << 63) | (ex << 52) | ((uint64_t)(hi & 0xFFFFFu) << 32) | lo;
+    return __longlong_as_double((long long)bits);
+}
+__global__ __launch_bounds__(256) void d2d_selftest_kernel(int which, long long n, uint64_t seed,
+                                                           unsigned long long* bad) {
+    unsigned long long cnt = 0;
+    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    for (long long k = (long long)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (long long)gridDim.x * blockDim.x) {
+        uint32_t o[4], p[4];
+        philox((uint32_t)k, (uint32_t)(k >> 32), 0x5E1F7E57u, (uint32_t)which, k0, k1, o);
+        philox((uint32_t)k, (uint32_t)(k >> 32), 0x5E1F7E58u, (uint32_t)which, k0, k1, p);
+        double got, want;
+        if (which == D2D_SELFTEST_SQRT) {
+            const double x = ((p[0] & 63u) == 0u) ? 0.0 : st_rand(o[0], o[1], 1023 - 767, 2046, 0u);
+            got = sqrt_nz(x);
+            want = sqrt(x);
+        } else {
+            const double a = st_rand(o[0], o[1], 1023 - 400, 1023 + 400, o[2]);
+            const double b = st_rand(p[0], p[1], 1023 - 400, 1023 + 400, p[2]);
+            want = a / b;
+            got = (which == D2D_SELFTEST_DIV) ? div_normal(a, b) : div_by_recip(a, b, 1.0 / b);
+        }
+        cnt += (__double_as_longlong(got) != __double_as_longlong(want)) ? 1ull : 0ull;
+    }
+    if (cnt) atomicAdd(bad, cnt);
 }
 
 // ------------------------------------------------------------------------------------------ K3

@@ -177,6 +177,14 @@ int32_t d2d_set_state(d2d_t* h, const double* state_dev, const int32_t* istate_d
  * fixed-order (bitwise reproducible) block reduction; clear != 0 zeroes the accumulators after. */
 int32_t d2d_episode_stats(d2d_t* h, double* out_dev, int32_t clear, void* stream);
 
+/* Device arithmetic self-check (no reference counterpart): runs n seeded random cases of one of the
+ * kernels' shortcut fp64 routines against the IEEE operation on the current device and stores the
+ * number of bitwise mismatches in *mismatches (host pointer).  which: D2D_SELFTEST_*. */
+#define D2D_SELFTEST_SQRT 0      /* range-limited sqrt (Brent distance) vs sqrt()        */
+#define D2D_SELFTEST_DIV 1       /* range-limited division (parabolic step) vs '/'       */
+#define D2D_SELFTEST_RECIP_DIV 2 /* division by a precomputed reciprocal (path blend)    */
+int32_t d2d_selftest(int32_t which, int64_t n, uint64_t seed, uint64_t* mismatches);
+
 /* Error codes */
 #define D2D_OK 0
 #define D2D_E_ARG 1

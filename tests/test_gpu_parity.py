@@ -255,3 +255,17 @@ def test_single_env_api(d2):
     _, _, done2, _ = env.step([0.0, 0.0])
     assert done2  # done is sticky until reset (drone_2d_env.py:594)
     env.close()
+
+
+@pytest.mark.parametrize("which", [0, 1, 2])
+def test_device_math_selftest(d2, which):
+    """The kernels' shortcut fp64 routines (range-limited sqrt and division, division by a
+    precomputed reciprocal) are bitwise equal to the IEEE operations on 2^26 random operands."""
+    import ctypes as C
+
+    from drone2d_amd import _native
+
+    lib = _native.load()
+    bad = C.c_uint64(123)
+    assert lib.d2d_selftest(which, 1 << 26, 2024 + which, C.byref(bad)) == 0
+    assert bad.value == 0

@@ -86,6 +86,15 @@ def run(scenario, n, steps_warm, lib=LIB):
         m = xcc[:, 0] == x
         spans.append(int(s[m, :, 6].max() - s[m, :, 0].min()))
     res["kernel_span_cycles_per_xcd"] = spans
+    # slowest 5% of workgroups: which wave ends phase A last, relative to W2's end (cycles)
+    tot = s[:, 0, 6] - s[:, :, 0].min(1)
+    slow = np.argsort(tot)[-max(1, len(tot) // 20):]
+    endA = s[slow, :, 2] - s[slow, 2, 2][:, None]
+    res["slow_blocks"] = {"total_med": int(np.median(tot[slow])),
+                          "last_wave_hist": np.bincount(np.argmax(s[slow, :, 2], 1), minlength=4).tolist(),
+                          "endA_minus_w2_med": [int(np.median(endA[:, w])) for w in range(4)],
+                          "w2_endA_from_start_med": int(np.median(s[slow, 2, 2] - s[slow, 2, 0])),
+                          "after_A_med": int(np.median(s[slow, 0, 6] - s[slow, :, 2].max(1)))}
     print(json.dumps(res, indent=1))
     return res
 

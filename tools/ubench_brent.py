@@ -19,8 +19,7 @@ import numpy as np
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 OUT = os.path.join(REPO, "tools", "_abl")
-VARIANTS = {"full": [], "nosqrt": ["UB_NOSQRT=1"], "nodiv": ["UB_NODIV=1"], "noidx": ["UB_NOIDX=1"],
-            "bare": ["UB_NOSQRT=1", "UB_NODIV=1", "UB_NOIDX=1"], "rec": ["UB_REC=1"]}
+VARIANTS = {"prod": [], "inl": ["UB_INLINE=1"]}
 
 
 def lib(v):
