@@ -9,12 +9,16 @@ A "step" = one ``d2d_step`` (libdrone2d_hip.so) over all envs of a GPU: thrust -
 equivalent 3-body/6-joint solve -> collision -> 3-nearest sensing -> Brent closest point ->
 27-dim obs -> reward/termination -> in-kernel auto-reset.  Workload (BASELINE.json configs[2]):
 65 536 envs per GPU on the ``corridor`` test scenario (18 circles), U(-1,1) float32 actions
-pre-generated on the device (a bank of 16, cycled), inputs resident in HBM before timing.
+pre-generated on the device (a bank of 16, cycled), inputs resident in HBM before timing.  The 16
+steps of one bank pass are captured once as a hipGraph and the timed loop replays it (no host work
+per step); ``--eager`` launches each step from Python instead.  Either way every step runs the full
+kernel on fresh state.
 Multi-GPU: one process per GPU, each with its own 65 536 envs (weak scaling, global env ids), no
 collective in the step; the episode statistics are all-reduced once per timed interval (RCCL).
 
 Prints ONE JSON line (rank 0).  ``roofline.achieved`` = 650 algorithmic bytes per env-step x envs
-per launch / mean step-kernel duration (HIP events on the launch stream); ``cpu_baseline`` = the C
+per launch / mean step-kernel duration (HIP events on the launch stream, per graph replay / 16
+steps); ``cpu_baseline`` = the C
 oracle (a scalar port of the same algorithm) timed on this host's cores on a bounded sample.
 """
 from __future__ import annotations
@@ -47,9 +51,10 @@ def parse():
     p.add_argument("--warmup", type=int, default=50)
     p.add_argument("--envs", type=int, default=ENVS_PER_GPU)
     p.add_argument("--scenario", default=SCENARIO)
-    p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (s)")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--graph", action="store_true", help="replay the step loop as a hipGraph")
+    p.add_argument("--eager", action="store_true",
+                   help="launch every step from Python instead of replaying the captured hipGraph")
     return p.parse_args()
 
 
@@ -91,7 +96,7 @@ def cpu_baseline(args, kwargs):
     t0 = time.perf_counter()
     b.step(act, nthreads=threads)  # one step to size the sample
     one = time.perf_counter() - t0
-    steps = max(1, min(200, int(args.cpu_seconds / max(one, 1e-6))))
+    steps = max(1, min(20000, int(args.cpu_seconds / max(one, 1e-6))))
     t0 = time.perf_counter()
     for _ in range(steps):
         b.step(act, nthreads=threads)
@@ -123,7 +128,7 @@ def main():
     venv.episode_stats(clear=True)
 
     graph = None
-    if args.graph:
+    if not args.eager:
         # capture ACTION_BANK steps (even count: the output double-buffer returns to its start)
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
