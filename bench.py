@@ -59,13 +59,10 @@ def parse():
 
 
 def setup_dist(args):
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
+    from drone2d_amd import shard
+
+    rank, world, local = shard.init_process_group_from_env("nccl")
+    if world == 1:
         torch.cuda.set_device(0)
     return rank, world, local
 
@@ -110,14 +107,17 @@ def cpu_baseline(args, kwargs):
 
 def main():
     args = parse()
-    rank, world, local = setup_dist(args)
-    import drone2d_amd as d2
+    import drone2d_amd  # noqa: F401  (registers the package as drone2d_amd)
+    from drone2d_amd import shard
     from drone2d_amd.config import ENV_TRAIN_CONFIG
+
+    rank, world, local = setup_dist(args)
 
     kwargs = dict(ENV_TRAIN_CONFIG, scenario=args.scenario)
     dev = torch.device("cuda", torch.cuda.current_device())
     n = args.envs
-    venv = d2.Drone2dVecEnv(n, device=dev, seed=12345, env_id_offset=rank * n, with_info=False, **kwargs)
+    # this rank's block of a global batch of world x n envs (global env ids, no step collective)
+    venv = shard.make_shard_venv(n * world, rank, world, device=dev, seed=12345, with_info=False, **kwargs)
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
     bank = [(torch.rand(n, 2, device=dev, generator=g) * 2 - 1).contiguous() for _ in range(ACTION_BANK)]
     venv.reset()
@@ -162,7 +162,7 @@ def main():
     t_ar = 0.0
     if world > 1:
         t1 = time.perf_counter()
-        dist.all_reduce(stats)
+        shard.allreduce_stats(stats)  # the one RCCL collective: 8 doubles per logging interval
         torch.cuda.synchronize()
         t_ar = time.perf_counter() - t1
     if graph is not None:

@@ -1,0 +1,126 @@
+"""Multi-rank sharding on CPU (gloo, world size 2) -- SURVEY.md §8(e).
+
+Each rank steps its contiguous block of a global batch (the C oracle stands in for the per-GPU
+kernel: test infrastructure) with global env ids and the globally computed env -> scenario map;
+the episode statistics are SUM-all-reduced through ``drone2d_amd.shard.allreduce_stats``.  The
+gathered per-env outputs and the reduced statistics must equal one unsharded batch bit for bit.
+The same helpers drive bench.py's RCCL path on GPUs.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+N_TOTAL = 301          # odd on purpose: uneven shards
+STEPS = 60
+SCN = ["corridor", "S_corridor", "large", "parallel", "perpendicular", "S_parallel", "impossible"]
+
+
+def _kw():
+    from drone2d_amd.config import ENV_TRAIN_CONFIG
+
+    return dict(ENV_TRAIN_CONFIG, scenario=SCN)
+
+
+def _actions():
+    return np.random.default_rng(11).uniform(-1, 1, (STEPS, N_TOTAL, 2)).astype(np.float32)
+
+
+def _run(backend, acts):
+    obs_all, rew_all = [], []
+    backend.reset()
+    for t in range(STEPS):
+        obs, rew, term, trunc, info = backend.step(torch.from_numpy(acts[t]))
+        obs_all.append(obs.clone())
+        rew_all.append(rew.clone())
+    return torch.stack(obs_all), torch.stack(rew_all), backend.episode_stats()
+
+
+def _worker(rank, world, port, out_dir):
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (here, os.path.dirname(here), os.path.join(os.path.dirname(here), "oracle")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import drone2d_amd  # noqa: F401
+    from drone2d_amd import shard
+    from oracle_backend import OracleVecBackend
+
+    r, w, _ = shard.init_process_group_from_env("gloo")
+    assert (r, w) == (rank, world)
+    off, cnt = shard.shard_range(N_TOTAL, world, rank)
+    es = shard.shard_env_scenario(shard.global_env_scenario(N_TOTAL, len(SCN)), off, cnt)
+    be = OracleVecBackend(cnt, seed=21, env_scenario=es, env_id_offset=off, **_kw())
+    obs, rew, stats = _run(be, _actions()[:, off:off + cnt])
+    stats = shard.allreduce_stats(stats.clone())
+    # gather the per-env outputs (uneven shards: pad to the largest block)
+    big = shard.shard_range(N_TOTAL, world, 0)[1]
+    pad_o = torch.zeros(STEPS, big, 27)
+    pad_o[:, :cnt] = obs
+    pad_r = torch.zeros(STEPS, big)
+    pad_r[:, :cnt] = rew
+    go = [torch.zeros_like(pad_o) for _ in range(world)]
+    gr = [torch.zeros_like(pad_r) for _ in range(world)]
+    dist.all_gather(go, pad_o)
+    dist.all_gather(gr, pad_r)
+    if rank == 0:
+        cnts = [shard.shard_range(N_TOTAL, world, k)[1] for k in range(world)]
+        obs_g = torch.cat([g[:, :c] for g, c in zip(go, cnts)], 1)
+        rew_g = torch.cat([g[:, :c] for g, c in zip(gr, cnts)], 1)
+        torch.save({"obs": obs_g, "rew": rew_g, "stats": stats}, os.path.join(out_dir, "sharded.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+    be.close()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_shard_range_partitions():
+    from drone2d_amd.shard import shard_range
+
+    for n, w in ((65536, 8), (301, 2), (10, 3), (7, 7)):
+        parts = [shard_range(n, w, r) for r in range(w)]
+        assert parts[0][0] == 0 and sum(c for _, c in parts) == n
+        for (o0, c0), (o1, _) in zip(parts, parts[1:]):
+            assert o0 + c0 == o1
+        assert max(c for _, c in parts) - min(c for _, c in parts) <= 1
+    with pytest.raises(ValueError):
+        shard_range(3, 4, 0)
+
+
+def test_two_rank_gloo_sharding_matches_single_batch(tmp_path, d2):
+    from oracle_backend import OracleVecBackend
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, str(tmp_path))) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    got = torch.load(os.path.join(tmp_path, "sharded.pt"), weights_only=True)
+    single = OracleVecBackend(N_TOTAL, seed=21, **_kw())
+    obs, rew, stats = _run(single, _actions())
+    single.close()
+    assert torch.equal(got["obs"], obs)
+    assert torch.equal(got["rew"], rew)
+    # per-env accumulators are identical; the reduction order differs (block sums), so compare the
+    # integer counts exactly and the float sums to rounding
+    np.testing.assert_array_equal(got["stats"][[1, 2, 3, 4]].numpy(), stats[[1, 2, 3, 4]].numpy())
+    np.testing.assert_allclose(got["stats"].numpy(), stats.numpy(), rtol=1e-12, atol=1e-9)
+    assert stats[1] > 0  # episodes finished
