@@ -1,0 +1,113 @@
+"""Test harness on the batched env: the reference's ``mode == "test"`` loop
+(main.py:242-327) -- run a policy until every env finishes its first episode, then report the same
+metrics and files (``results.txt`` lines, ``apes/collisions/rewards/time_spent.npy``) -- with all
+envs of a scenario stepping in one batch instead of 100 sequential runs.
+
+``MlpActor`` is SB3's default ``MlpPolicy`` actor (27-64-64-2, tanh; policy_kwargs {} in the
+shipped agents), loaded from the float32 weights extracted from an agent zip
+(tests/golden/make_agent_fixture.py).  ``model.predict(obs)`` in the reference is stochastic
+(deterministic=False): a = clip(mean + exp(log_std) * N(0, 1), -1, 1).
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+
+from . import abi
+from .env import info_dicts
+
+
+class MlpActor(torch.nn.Module):
+    def __init__(self, w: dict):
+        super().__init__()
+        t = {k: torch.as_tensor(np.asarray(v, np.float32)) for k, v in w.items()}
+        self.l0 = torch.nn.Linear(27, 64)
+        self.l1 = torch.nn.Linear(64, 64)
+        self.out = torch.nn.Linear(64, 2)
+        with torch.no_grad():
+            self.l0.weight.copy_(t["mlp_extractor_policy_net_0_weight"])
+            self.l0.bias.copy_(t["mlp_extractor_policy_net_0_bias"])
+            self.l1.weight.copy_(t["mlp_extractor_policy_net_2_weight"])
+            self.l1.bias.copy_(t["mlp_extractor_policy_net_2_bias"])
+            self.out.weight.copy_(t["action_net_weight"])
+            self.out.bias.copy_(t["action_net_bias"])
+        self.register_buffer("log_std", t["log_std"].clone())
+
+    @classmethod
+    def from_npz(cls, path: str) -> "MlpActor":
+        with np.load(path, allow_pickle=False) as z:
+            return cls({k: z[k] for k in z.files})
+
+    def forward(self, obs: torch.Tensor) -> torch.Tensor:
+        return self.out(torch.tanh(self.l1(torch.tanh(self.l0(obs)))))
+
+    @torch.no_grad()
+    def act(self, obs: torch.Tensor, deterministic: bool = False, generator: torch.Generator | None = None):
+        mean = self(obs)
+        if not deterministic:
+            noise = torch.randn(mean.shape, device=mean.device, dtype=mean.dtype, generator=generator)
+            mean = mean + torch.exp(self.log_std) * noise
+        return torch.clamp(mean, -1.0, 1.0)
+
+
+def run_first_episodes(venv, policy: MlpActor, *, deterministic: bool = False, seed: int = 0,
+                       max_steps: int | None = None, n_obstacles: int | None = None) -> dict:
+    """Step ``venv`` (with info rows) under ``policy`` until every env has finished its first
+    episode; per-episode records as the reference's test loop keeps them (main.py:273-281)."""
+    dev = venv.device
+    gen = torch.Generator(device=dev).manual_seed(seed)
+    policy = policy.to(dev)
+    obs = venv.reset(seed=seed)
+    n = venv.num_envs
+    finished = torch.zeros(n, dtype=torch.bool, device=dev)
+    rows = torch.zeros(n, abi.INFO_DIM, dtype=torch.float32, device=dev)
+    cap = max_steps if max_steps is not None else int(venv.kwargs["n_steps"]) + 1
+    nobs = n_obstacles if n_obstacles is not None else len(venv.scenarios[0].circles)
+    for _ in range(cap):
+        a = policy.act(obs, deterministic=deterministic, generator=gen)
+        obs, rew, term, trunc, info = venv.step(a)
+        new = (term | trunc) & ~finished
+        rows[new] = info[new]
+        finished |= term | trunc
+        if bool(finished.all()):
+            break
+    rows = rows[finished].cpu().numpy()
+    recs = [info_dicts(r, nobs) for r in rows]
+    return {
+        "successes": int(sum(d["n_successful_runs"] == 1 for d in recs)),
+        "fails": int(sum(d["n_failed_runs"] == 1 for d in recs)),
+        "collisions": np.array([d["n_collisions"] for d in recs], np.int64),
+        "apes": np.array([d["APE"] for d in recs], np.float64),
+        "time_spent": np.array([d["env_steps"] for d in recs], np.int64),
+        "rewards": np.array([d["total_reward"] for d in recs], np.float64),
+        "unfinished": int(n - len(recs)),
+    }
+
+
+def summary(m: dict) -> dict:
+    """The numbers of the reference's results.txt (main.py:318-325)."""
+    runs = m["successes"] + m["fails"]
+    col = int(m["collisions"].sum())
+    return {"Successes": m["successes"], "Fails": m["fails"], "Collisions": col,
+            "Success rate": m["successes"] / max(runs, 1), "Collision rate": col / max(runs, 1),
+            "Average APE": float(np.mean(m["apes"])) if len(m["apes"]) else float("nan"),
+            "Average flight time": float(np.mean(m["time_spent"])) if len(m["time_spent"]) else float("nan")}
+
+
+def write_results(m: dict, out_dir: str, scenario: str, agent_nr: str, agent_path: str):
+    """The reference's per-scenario files: results.txt + collisions/rewards/apes/time_spent .npy."""
+    os.makedirs(out_dir, exist_ok=True)
+    for k in ("collisions", "rewards", "apes", "time_spent"):
+        np.save(os.path.join(out_dir, f"{k}.npy"), m[k])
+    s = summary(m)
+    with open(os.path.join(out_dir, f"{scenario}_{agent_nr}_results.txt"), "w") as f:
+        for k in ("Successes", "Fails", "Collisions", "Success rate", "Collision rate", "Average APE",
+                  "Average flight time"):
+            f.write(f"{k}: {s[k]}\n")
+        f.write(f"Agent path: {agent_path}\n")
+    return s
+
+
+__all__ = ["MlpActor", "run_first_episodes", "summary", "write_results"]

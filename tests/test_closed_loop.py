@@ -1,0 +1,38 @@
+"""Closed-loop distributional parity with the shipped agent -- needs an MI355X.
+
+The reference publishes, for agent PFCA_see_3_obs_17_90, 100-run success / collision rates per test
+scenario (best_models_config_and_res/run17see3/res/*/results.txt, in tests/golden/
+agent_17_90_results.json).  The same actor (weights in tests/golden/agent_17_90.npz), sampled
+stochastically as the reference's ``model.predict(obs)`` does, flies 1 000 first episodes per
+scenario in the HIP env; the success rate must agree within 4 standard errors of the difference.
+This is the one check of the (otherwise unpinned) Chipmunk-equivalent physics against the
+reference's own behaviour.  Harness metrics are computed exactly as main.py:273-325 does.
+"""
+import json
+import math
+import os
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.mark.parametrize("scn", ["corridor", "large", "S_corridor", "impossible"])
+def test_agent_success_rate_matches_reference(d2, scn):
+    from drone2d_amd import harness
+    from drone2d_amd.config import ENV_TEST_CONFIG
+
+    ref = json.load(open(os.path.join(HERE, "golden", "agent_17_90_results.json")))["results"][scn]
+    pol = harness.MlpActor.from_npz(os.path.join(HERE, "golden", "agent_17_90.npz"))
+    venv = d2.Drone2dVecEnv(1000, seed=5, with_info=True, **dict(ENV_TEST_CONFIG, scenario=scn))
+    m = harness.run_first_episodes(venv, pol, seed=5)
+    venv.close()
+    s = harness.summary(m)
+    assert m["unfinished"] == 0 and s["Successes"] + s["Fails"] == 1000
+    p, q = s["Success rate"], ref["Success rate"]
+    se = math.sqrt(max(q * (1 - q), 0.0099) / 100 + max(p * (1 - p), 0.0099) / 1000)
+    assert abs(p - q) < 4 * se, (scn, p, q)
+    c, cq = s["Collision rate"], ref["Collision rate"]
+    sec = math.sqrt(max(cq * (1 - cq), 0.0099) / 100 + max(c * (1 - c), 0.0099) / 1000)
+    assert abs(c - cq) < 4 * sec, (scn, c, cq)

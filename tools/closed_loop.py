@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""Closed-loop distributional parity, GPU box.
+
+Runs the shipped agent PFCA_see_3_obs_17_90 (weights: tests/golden/agent_17_90.npz) on every test
+scenario with N envs each (stochastic policy, as the reference's ``model.predict(obs)``), writes the
+reference's result files under gpurun_out/Tests/agent_17/<scenario>/ and compares success /
+collision rates with the reference's own 100-run results (tests/golden/agent_17_90_results.json).
+
+    python tools/closed_loop.py [--envs 2000] [--seed 0]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+SCENARIOS = ["perpendicular", "parallel", "S_parallel", "corridor", "S_corridor", "large", "impossible"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--envs", type=int, default=2000)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--scenarios", default=",".join(SCENARIOS))
+    a = ap.parse_args()
+    import torch  # noqa: F401
+
+    import drone2d_amd as d2
+    from drone2d_amd import harness
+    from drone2d_amd.config import ENV_TEST_CONFIG
+
+    ref = json.load(open(os.path.join(REPO, "tests", "golden", "agent_17_90_results.json")))
+    pol = harness.MlpActor.from_npz(os.path.join(REPO, "tests", "golden", "agent_17_90.npz"))
+    out = {}
+    for scn in a.scenarios.split(","):
+        t0 = time.perf_counter()
+        venv = d2.Drone2dVecEnv(a.envs, seed=a.seed, with_info=True, **dict(ENV_TEST_CONFIG, scenario=scn))
+        m = harness.run_first_episodes(venv, pol, seed=a.seed)
+        venv.close()
+        s = harness.write_results(m, os.path.join(REPO, "gpurun_out", "Tests", "agent_17", scn), scn, "17",
+                                  ref["agent"])
+        r = ref["results"][scn]
+        p, q = s["Success rate"], r["Success rate"]
+        n_ours, n_ref = s["Successes"] + s["Fails"], r["Successes"] + r["Fails"]
+        se = math.sqrt(max(q * (1 - q), 0.01 * 0.99) / n_ref + max(p * (1 - p), 0.01 * 0.99) / max(n_ours, 1))
+        out[scn] = {"ours": s, "reference": {k: r[k] for k in ("Success rate", "Collision rate", "Average APE",
+                                                               "Average flight time")},
+                    "runs": [n_ours, n_ref], "success_z": (p - q) / se, "unfinished": m["unfinished"],
+                    "seconds": time.perf_counter() - t0}
+        print(scn, json.dumps(out[scn]), flush=True)
+    os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+    json.dump(out, open(os.path.join(REPO, "gpurun_out", "closed_loop.json"), "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()

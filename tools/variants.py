@@ -30,8 +30,9 @@ def build(specs):
 
     os.makedirs(ABL, exist_ok=True)
     for spec in specs:
+        spec, _, flags = spec.partition("::")   # TAG[:DEF,DEF][::flag+flag] (e.g. -mllvm+-misched=...)
         tag, _, defs = spec.partition(":")
-        d = [f"-D{x}" for x in defs.split(",") if x]
+        d = [f"-D{x}" for x in defs.split(",") if x] + [f for f in flags.split("+") if f]
         subprocess.run([_build.hipcc(), *_build.HIPCC_FLAGS, *d, "-I", os.path.join(REPO, "include"), _build.SRC,
                         "-o", lib_for(tag)], check=True)
         print("built", lib_for(tag), d)
@@ -87,4 +88,4 @@ if __name__ == "__main__":
     if a.mode == "build":
         build(a.specs)
     else:
-        run([s.partition(":")[0] for s in a.specs], a.envs, a.scenario, a.rounds, not a.no_auto_reset)
+        run([s.partition("::")[0].partition(":")[0] for s in a.specs], a.envs, a.scenario, a.rounds, not a.no_auto_reset)
