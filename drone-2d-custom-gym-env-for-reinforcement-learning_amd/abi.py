@@ -7,7 +7,7 @@ from __future__ import annotations
 
 import ctypes as C
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 MAX_WPS = 16
 MAX_SEGS = MAX_WPS - 2
@@ -56,6 +56,7 @@ class D2DCfg(C.Structure):
         ("auto_reset", C.c_int32),
         ("timeup_truncates", C.c_int32),
         ("env_id_base", C.c_int32),
+        ("scn_pool", C.c_int32),
     ]
 
 

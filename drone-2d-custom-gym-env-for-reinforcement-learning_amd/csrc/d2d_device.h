@@ -191,6 +191,12 @@ __device__ __forceinline__ double u53(uint32_t a, uint32_t b) {
     return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * (1.0 / 9007199254740992.0);
 }
 // test-mode spawn draw (drone_2d_env.py:229-232): x, y, theta for (seed, global env id, episode)
+// curriculum pool (d2d_cfg.scn_pool): scenario of the episode that starts at this reset
+__device__ __forceinline__ int pool_pick(uint64_t seed, uint32_t gid, uint32_t episode, int n_scn) {
+    uint32_t o[4];
+    philox(gid, episode, 2u, 0u, (uint32_t)seed, (uint32_t)(seed >> 32), o);
+    return (int)(o[0] % (uint32_t)n_scn);
+}
 __device__ __forceinline__ void spawn_draw(const Scn& s, uint64_t seed, uint32_t gid, uint32_t episode,
                                            double& x, double& y, double& th) {
     uint32_t o[4];

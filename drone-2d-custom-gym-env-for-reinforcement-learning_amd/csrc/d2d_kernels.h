@@ -60,7 +60,7 @@ struct StepArgs {
     int32_t* ist;            // [NISTATE][n]
     double* acc;             // [NSTATS][n]
     const Scn* scn;          // [n_scn]
-    const int32_t* env_scn;  // [n] or null (all scenario 0)
+    int32_t* env_scn;        // [n] or null (all scenario 0); rewritten at resets in pool mode
     d2d_cfg cfg;
     double damping_dt;       // pow(cfg.damping, dt), host glibc
     uint64_t seed;
@@ -299,6 +299,12 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
     __syncthreads();
     STAMP(1);
     const Scn& S = scns[sh.scn[lane]];
+    // scenario of the episode an auto-reset would start (curriculum pool: a fresh draw)
+    const int nscn = (a.cfg.scn_pool && a.n_scn > 1 && valid)
+                         ? pool_pick(a.seed, (uint32_t)a.cfg.env_id_base + (uint32_t)i,
+                                     (uint32_t)fld(a.ist, D2D_I_EPISODE, n, i), a.n_scn)
+                         : sh.scn[lane];
+    const Scn& SN = scns[nscn];
     float* const trow = a.tobs ? a.tobs + (size_t)i * D2D_OBS_DIM : nullptr;
     float* const orow = &sh.u.p.obs[lane * D2D_OBS_DIM];
 
@@ -426,8 +432,8 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
             } else {
                 if (done && auto_reset) {
                     double sp[7];
-                    spawn_state(a, S, i, sp);
-                    sensor_obs(a.cfg, S, Body{sp[0], sp[1], sp[2], 0.0, 0.0, 0.0}, so);
+                    spawn_state(a, SN, i, sp);
+                    sensor_obs(a.cfg, SN, Body{sp[0], sp[1], sp[2], 0.0, 0.0, 0.0}, so);
                 }
 #pragma unroll
                 for (int k = 0; k < 19; ++k) row[k] = (float)so[k];
@@ -451,8 +457,8 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
         if (auto_reset && !stop_seen(sh.stop)) {
             if (valid && !done && sst == 0) {
                 double sp[7], so[19];
-                spawn_state(a, S, i, sp);
-                sensor_obs(a.cfg, S, Body{sp[0], sp[1], sp[2], 0.0, 0.0, 0.0}, so);
+                spawn_state(a, SN, i, sp);
+                sensor_obs(a.cfg, SN, Body{sp[0], sp[1], sp[2], 0.0, 0.0, 0.0}, so);
                 float* c = a.rc_obs + (size_t)i * D2D_OBS_DIM;
 #pragma unroll
                 for (int k = 0; k < 19; ++k) c[k] = (float)so[k];
@@ -518,7 +524,7 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
             if (auto_reset) pst = fld(a.rc_i, RC_PST, n, i);
             if (done && auto_reset) {
                 double sp[7];
-                spawn_state(a, S, i, sp);
+                spawn_state(a, SN, i, sp);
 #pragma unroll
                 for (int k = 0; k < 7; ++k) sh.sp[k][lane] = sp[k];
                 if (pst & RC_PATH) {
@@ -528,7 +534,7 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
                     sh.rflags[lane] = (uint32_t)fld(a.rc_i, RC_RFLAGS, n, i);
                 } else {
                     uint32_t f = 0;
-                    path_obs(a.cfg, S, sp[0], sp[1], sp[2], f, po);
+                    path_obs(a.cfg, SN, sp[0], sp[1], sp[2], f, po);
                     sh.rflags[lane] = f;
                 }
                 fld(a.rc_i, RC_PST, n, i) = 0;
@@ -539,7 +545,7 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) orow[19 + k] = (float)po[k];
         }
-        if (auto_reset && D2D_RC_FILL) rc_fill_path(a, S, i, valid && !done && !(pst & RC_PATH), pst, sh.stop);
+        if (auto_reset && D2D_RC_FILL) rc_fill_path(a, SN, i, valid && !done && !(pst & RC_PATH), pst, sh.stop);
     }
     STAMP(2);
     __syncthreads();
@@ -607,6 +613,7 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
             fld(a.ist, D2D_I_T, n, i) = 0;
             fld(a.ist, D2D_I_FLAGS, n, i) = (int32_t)sh.rflags[lane];
             fld(a.ist, D2D_I_EPISODE, n, i) += 1;
+            if (a.cfg.scn_pool && a.env_scn) a.env_scn[i] = nscn;
         } else {
             fld(a.st, D2D_S_PATH_ERR, n, i) = path_err;
             fld(a.st, D2D_S_TOT_REW, n, i) = tot_rew;
@@ -627,7 +634,13 @@ __global__ __launch_bounds__(BLOCK) void d2d_reset_kernel(StepArgs a) {
     if (i >= a.n) return;
     if (a.mask && !a.mask[i]) return;
     const int n = a.n;
-    const Scn& s = scns[(a.env_scn && a.n_scn > 1) ? a.env_scn[i] : 0];
+    int si = (a.env_scn && a.n_scn > 1) ? a.env_scn[i] : 0;
+    if (a.cfg.scn_pool && a.n_scn > 1) {
+        si = pool_pick(a.seed, (uint32_t)a.cfg.env_id_base + (uint32_t)i, (uint32_t)fld(a.ist, D2D_I_EPISODE, n, i),
+                       a.n_scn);
+        a.env_scn[i] = si;
+    }
+    const Scn& s = scns[si];
     double sp[7];
     spawn_state(a, s, i, sp);
     const double th = sp[2];

@@ -56,6 +56,16 @@ def build_scenarios(kwargs: dict) -> list[Scenario]:
     """Scenario list for ``mode='test'``: one name, a list of names, or Scenario objects."""
     W, H = kwargs["screensize_x"], kwargs["screensize_y"]
     spec = kwargs["scenario"]
+    if is_curriculum(kwargs):
+        # a pool of curriculum resets (drone2d_amd.curriculum); the kernel draws one per episode
+        from .curriculum import curriculum_pool, stage_for_sim_num
+
+        if spec in CURRICULUM_STAGES:
+            stage, chance = spec, None
+        else:
+            stage, chance = stage_for_sim_num(int(kwargs.get("sim_num", 0)))
+        return curriculum_pool(stage, kwargs, int(kwargs.get("curriculum_pool", 1024)),
+                               seed=int(kwargs.get("curriculum_seed", 0)), spawn_chance=chance)
     if isinstance(spec, (str, Scenario)):
         spec = [spec]
     out = []
@@ -66,11 +76,15 @@ def build_scenarios(kwargs: dict) -> list[Scenario]:
             out.append(create_test_scenario(s, W, H))
         elif isinstance(s, str) and s.endswith("_free") and s[:-5] in TEST_SCENARIOS:
             out.append(free_flight(create_test_scenario(s[:-5], W, H)))
-        elif s in CURRICULUM_STAGES or kwargs["mode"] == "curriculum":
-            raise NotImplementedError("curriculum stages are not implemented in this build (SURVEY.md §8f row 2)")
         else:
             raise ValueError(f"unknown scenario {s!r}")
     return out
+
+
+def is_curriculum(kwargs: dict) -> bool:
+    """mode='curriculum' or an explicit stage_k scenario (drone_2d_env.py:75-86, 199-215)."""
+    spec = kwargs.get("scenario")
+    return kwargs.get("mode") == "curriculum" or (isinstance(spec, str) and spec in CURRICULUM_STAGES)
 
 
 class Drone2dVecEnv:
@@ -83,6 +97,11 @@ class Drone2dVecEnv:
       env_id_offset   global id of env 0 (multi-GPU shards keep per-env RNG streams global)
       auto_reset      SB3 VecEnv semantics (done envs are reset inside the step kernel)
       timeup_truncates  report time-up as truncation instead of termination (reference: False)
+    Curriculum (``mode='curriculum'`` or ``scenario='stage_k'``): a pool of
+    ``kwargs['curriculum_pool']`` (default 1024) reference-identical curriculum resets is generated
+    from ``kwargs['curriculum_seed']`` for the stage (explicit, or from ``kwargs['sim_num']`` by the
+    reference's schedule) and every episode of every env draws one entry (drone2d_amd.curriculum).
+    ``set_curriculum(stage=..., sim_num=...)`` regenerates the pool and resets all envs.
     """
 
     def __init__(self, num_envs: int, device=None, seed: int = 0, *,
@@ -102,6 +121,8 @@ class Drone2dVecEnv:
         self.cfg = make_cfg(self.kwargs, auto_reset=auto_reset, timeup_truncates=timeup_truncates,
                             env_id_base=env_id_offset)
         self.scenarios = build_scenarios(self.kwargs)
+        # curriculum: every reset draws a fresh pool entry (d2d_cfg.scn_pool)
+        self.cfg.scn_pool = 1 if is_curriculum(self.kwargs) else 0
         self.seed_value = int(seed)
         self.with_info = with_info
         self.action_space = _make_box(-np.ones(2), np.ones(2))
@@ -110,15 +131,7 @@ class Drone2dVecEnv:
         h = C.c_void_p()
         check(self._lib.d2d_create(C.byref(self.cfg), self.num_envs, self.device.index, C.byref(h)), "d2d_create")
         self._h = h
-        n_scn = len(self.scenarios)
-        arr = (abi.D2DScn * n_scn)(*[s.to_c() for s in self.scenarios])
-        if env_scenario is None:
-            env_scenario = np.arange(self.num_envs) % n_scn
-        es = np.ascontiguousarray(np.asarray(env_scenario, dtype=np.int32))
-        if es.shape != (self.num_envs,):
-            raise ValueError("env_scenario must have shape [num_envs]")
-        self.env_scenario = es
-        check(self._lib.d2d_set_scenarios(h, arr, n_scn, es.ctypes.data_as(C.POINTER(C.c_int32))), "d2d_set_scenarios")
+        self._upload_scenarios(env_scenario)
 
         N, dev = self.num_envs, self.device
         # double-buffered outputs: the tensors returned by step k stay valid during step k+1
@@ -133,6 +146,39 @@ class Drone2dVecEnv:
         self._stats = torch.zeros(abi.NSTATS, dtype=torch.float64, device=dev)
 
     # ------------------------------------------------------------------ plumbing
+    def _upload_scenarios(self, env_scenario=None):
+        n_scn = len(self.scenarios)
+        arr = (abi.D2DScn * n_scn)(*[s.to_c() for s in self.scenarios])
+        if env_scenario is None:
+            env_scenario = np.arange(self.num_envs) % n_scn
+        es = np.ascontiguousarray(np.asarray(env_scenario, dtype=np.int32))
+        if es.shape != (self.num_envs,):
+            raise ValueError("env_scenario must have shape [num_envs]")
+        self.env_scenario = es  # in curriculum mode: the initial map only (resets redraw on device)
+        check(self._lib.d2d_set_scenarios(self._h, arr, n_scn, es.ctypes.data_as(C.POINTER(C.c_int32))),
+              "d2d_set_scenarios")
+
+    def set_curriculum(self, stage: str | None = None, sim_num: int | None = None, pool: int | None = None,
+                       seed: int | None = None) -> torch.Tensor:
+        """Regenerate the curriculum pool (explicit ``stage`` or the reference's ``sim_num``
+        schedule), upload it and reset every env; returns the reset observations."""
+        if not self.cfg.scn_pool:
+            raise ValueError("set_curriculum needs an env created in curriculum mode (mode='curriculum')")
+        if stage is not None:
+            self.kwargs["scenario"] = stage
+        elif sim_num is not None:
+            self.kwargs["scenario"] = "curriculum"
+            self.kwargs["sim_num"] = int(sim_num)
+        self.kwargs["mode"] = "curriculum"
+        if pool is not None:
+            self.kwargs["curriculum_pool"] = int(pool)
+        if seed is not None:
+            self.kwargs["curriculum_seed"] = int(seed)
+        self.scenarios = build_scenarios(self.kwargs)
+        torch.cuda.synchronize(self.device)
+        self._upload_scenarios()
+        return self.reset()
+
     def _stream(self):
         return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 

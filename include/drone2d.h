@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define D2D_ABI_VERSION 1
+#define D2D_ABI_VERSION 2
 
 #define D2D_MAX_WPS 16                    /* largest test path: 'large' has 14 waypoints   */
 #define D2D_MAX_SEGS (D2D_MAX_WPS - 2)    /* QPMI2D fits n_wps-2 quadratics (predef_path.py:34) */
@@ -116,6 +116,10 @@ typedef struct d2d_cfg {
     int32_t env_id_base;               /* global id of env 0: the Philox spawn stream is keyed by
                                           (seed, env_id_base + i, episode), so a sharded run draws
                                           the same spawns as one big batch               */
+    int32_t scn_pool;                  /* 0: env i always runs scenario env_scn[i] (test mode);
+                                          1: curriculum pool -- at every reset env i draws its next
+                                          scenario uniformly from the n_scn uploaded, from its
+                                          Philox stream (counter (gid, episode, 2, 0))     */
 } d2d_cfg;
 
 /* One scenario: a QPMI2D path + circle obstacles + spawn distribution.

@@ -98,6 +98,12 @@ void d2dcpu_spawn_uniforms(uint64_t seed, uint32_t env_id, uint32_t episode, dou
     philox(env_id, episode, 1u, 0u, (uint32_t)seed, (uint32_t)(seed >> 32), o);
     u[2] = u53(o[0], o[1]);
 }
+/* curriculum pool (d2d_cfg.scn_pool): the scenario of the episode that starts at this reset */
+uint32_t d2dcpu_pool_pick(uint64_t seed, uint32_t env_id, uint32_t episode, uint32_t n_scn) {
+    uint32_t o[4];
+    philox(env_id, episode, 2u, 0u, (uint32_t)seed, (uint32_t)(seed >> 32), o);
+    return o[0] % n_scn;
+}
 
 /* ------------------------------------------------------------------------------------------ */
 /* QPMI2D path (predef_path.py)                                                                */
@@ -597,8 +603,11 @@ static void write_obs(float* dst, const double* obs) {
 
 /* test-mode reset of env i (drone_2d_env.py:218-311 + Drone.py:20-52 + reset :908-912) */
 static void o_reset_env(d2dcpu_t* h, int i, float* obs_out) {
-    const d2d_scn* s = &h->scn[h->env_scn[i]];
     uint32_t ep = (uint32_t)h->ist[(size_t)D2D_I_EPISODE * h->n + i];
+    if (h->cfg.scn_pool && h->n_scn > 1)
+        h->env_scn[i] = (int32_t)d2dcpu_pool_pick(h->seed, (uint32_t)h->cfg.env_id_base + (uint32_t)i, ep,
+                                                  (uint32_t)h->n_scn);
+    const d2d_scn* s = &h->scn[h->env_scn[i]];
     double u[3];
     d2dcpu_spawn_uniforms(h->seed, (uint32_t)h->cfg.env_id_base + (uint32_t)i, ep, u);
     double x = s->spawn_xmin + (s->spawn_xmax - s->spawn_xmin) * u[0];

@@ -32,6 +32,7 @@ int32_t d2dcpu_physics_step(const d2d_cfg* cfg, const d2d_scn* s, double* st, do
                             int32_t collided);
 double d2dcpu_moment_box(double m, double w, double h);
 void d2dcpu_spawn_uniforms(uint64_t seed, uint32_t env_id, uint32_t episode, double u[3]);
+uint32_t d2dcpu_pool_pick(uint64_t seed, uint32_t env_id, uint32_t episode, uint32_t n_scn);
 void d2dcpu_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
 #ifdef __cplusplus
 }

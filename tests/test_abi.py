@@ -63,12 +63,12 @@ def hip_lib(d2):
 
 
 def test_hip_library_exports_every_header_symbol(hip_lib):
-    from drone2d_amd import _native
+    from drone2d_amd import _native, abi
 
     for f in header_functions():
         assert hasattr(hip_lib, f), f
         assert f in _native.SIGNATURES, f  # and the ctypes binding declares it
-    assert hip_lib.d2d_abi_version() == 1
+    assert hip_lib.d2d_abi_version() == abi.ABI_VERSION == 2
 
 
 def test_hip_library_is_gfx950(d2):

@@ -94,6 +94,31 @@ def test_reset_cache_invalidation(d2):
     venv.close()
 
 
+@pytest.mark.parametrize("stage", ["stage_2", "stage_3", "stage_5"])
+def test_curriculum_pool_vs_oracle(d2, stage):
+    """Curriculum mode: every reset draws the env's next scenario from the pool on device; the
+    oracle makes the same draws (teacher-forced over many auto-resets)."""
+    import oracle
+    from drone2d_amd.config import make_cfg
+
+    kw = _cfgkw(stage, mode="curriculum", curriculum_pool=64, curriculum_seed=2)
+    n = 2048
+    venv = d2.Drone2dVecEnv(n, seed=17, **kw)
+    assert venv.cfg.scn_pool == 1 and len(venv.scenarios) == 64
+    cfg = make_cfg(dict(kw))
+    cfg.scn_pool = 1
+    orc = oracle.OracleBatch(cfg, [s.to_c() for s in venv.scenarios], n, env_scenario=venv.env_scenario)
+    np.testing.assert_allclose(venv.reset().cpu().numpy(), orc.reset(17), rtol=0, atol=OBS_ATOL)
+    rng = np.random.default_rng(6)
+    dones = 0
+    for t in range(120):
+        act = rng.uniform(-1, 1, (n, 2)).astype(np.float32)
+        compare_step(venv, orc, act)
+        dones += int(orc.term.sum())
+    assert dones > 200
+    venv.close()
+
+
 def test_reset_cache_short_episodes(d2):
     """Episodes shorter than the cache fill: a mix of cached and synchronous reset observations."""
     venv, orc = make_pair(d2, 1024, SCENARIOS, seed=8, kwargs=_cfgkw(n_steps=3))
