@@ -1,6 +1,7 @@
 // d2d_hip.hip -- kernels + C ABI of libdrone2d_hip.so (see include/drone2d.h).
 //
-// Kernels: see d2d_kernels.h (K1 cooperative step, K2 masked reset, K3 episode statistics).
+// Kernels: see d2d_kernels.h (K1 cooperative step, K2 masked reset, K3 episode statistics, K4 reset
+// observation cache fill).
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -41,9 +42,11 @@ struct d2d_handle {
     bool reset_done = false;
     uint64_t* stamps = nullptr;  // diagnostic builds (D2D_STAMPS) only
     // auto-reset observation cache (d2d_kernels.h, "Auto-reset observation cache")
-    double* rc_bs = nullptr;     // [RC_NB][n]
-    int32_t* rc_i = nullptr;     // [RC_NI][n]
     float* rc_obs = nullptr;     // [n][27]
+    int32_t* rc_rfl = nullptr;   // [n]
+    int32_t* rc_tag = nullptr;   // [n]
+    bool rc_dirty = true;        // scenarios changed since the cache was last dropped
+    uint64_t n_steps = 0;        // d2d_step calls (fill cadence)
 };
 
 namespace {
@@ -61,15 +64,28 @@ StepArgs make_args(const d2d_t* h) {
     a.damping_dt = std::pow(h->cfg.damping, 1.0 / 60.0);
     a.seed = h->seed;
     a.stamps = h->stamps;
-    a.rc_bs = h->rc_bs;
-    a.rc_i = h->rc_i;
     a.rc_obs = h->rc_obs;
+    a.rc_rfl = h->rc_rfl;
+    a.rc_tag = h->rc_tag;
     return a;
 }
 
-// every cache entry invalid (status rows RC_PST, RC_SST = 0), ordered on `stream`
-hipError_t rc_invalidate(d2d_t* h, hipStream_t stream) {
-    return hipMemsetAsync(h->rc_i, 0, sizeof(int32_t) * 2 * (size_t)h->n, stream);
+// K4: fill every cache entry that does not belong to its env's current episode, ordered on `stream`
+hipError_t rc_fill(d2d_t* h, hipStream_t stream) {
+    StepArgs a = make_args(h);
+    const dim3 grid((h->n + BLOCK - 1) / BLOCK);
+    if (sizeof(d2d::Scn) * (size_t)h->n_scn <= K2_LDS_BUDGET)
+        hipLaunchKernelGGL(d2d_fill_kernel<true>, grid, dim3(BLOCK), sizeof(d2d::Scn) * h->n_scn, stream, a);
+    else
+        hipLaunchKernelGGL(d2d_fill_kernel<false>, grid, dim3(BLOCK), 0, stream, a);
+    return hipGetLastError();
+}
+// drop every entry (new seed, counters or scenarios) and refill, ordered on `stream`
+hipError_t rc_rebuild(d2d_t* h, hipStream_t stream) {
+    hipError_t e = hipMemsetAsync(h->rc_tag, 0xFF, sizeof(int32_t) * (size_t)h->n, stream);
+    if (e == hipSuccess && D2D_FILL_PERIOD > 0) e = rc_fill(h, stream);
+    if (e == hipSuccess) h->rc_dirty = false;
+    return e;
 }
 
 struct DeviceGuard {
@@ -108,9 +124,9 @@ int32_t d2d_create(const d2d_cfg* cfg, int32_t n_envs, int32_t device, d2d_t** o
         (e = hipMalloc(&h->ist, sizeof(int32_t) * D2D_NISTATE * n)) != hipSuccess ||
         (e = hipMalloc(&h->acc, sizeof(double) * D2D_NSTATS * n)) != hipSuccess ||
         (e = hipMalloc(&h->env_scn, sizeof(int32_t) * n)) != hipSuccess ||
-        (e = hipMalloc(&h->rc_bs, sizeof(double) * RC_NB * n)) != hipSuccess ||
-        (e = hipMalloc(&h->rc_i, sizeof(int32_t) * RC_NI * n)) != hipSuccess ||
-        (e = hipMalloc(&h->rc_obs, sizeof(float) * D2D_OBS_DIM * n)) != hipSuccess) {
+        (e = hipMalloc(&h->rc_obs, sizeof(float) * D2D_OBS_DIM * n)) != hipSuccess ||
+        (e = hipMalloc(&h->rc_rfl, sizeof(int32_t) * n)) != hipSuccess ||
+        (e = hipMalloc(&h->rc_tag, sizeof(int32_t) * n)) != hipSuccess) {
         d2d_destroy(h);
         return hip_fail(e, "d2d_create: hipMalloc");
     }
@@ -118,7 +134,7 @@ int32_t d2d_create(const d2d_cfg* cfg, int32_t n_envs, int32_t device, d2d_t** o
     (void)hipMemset(h->ist, 0, sizeof(int32_t) * D2D_NISTATE * n);
     (void)hipMemset(h->acc, 0, sizeof(double) * D2D_NSTATS * n);
     (void)hipMemset(h->env_scn, 0, sizeof(int32_t) * n);
-    (void)hipMemset(h->rc_i, 0, sizeof(int32_t) * RC_NI * n);
+    (void)hipMemset(h->rc_tag, 0xFF, sizeof(int32_t) * n);
     if ((e = hipDeviceSynchronize()) != hipSuccess) {
         d2d_destroy(h);
         return hip_fail(e, "d2d_create: memset");
@@ -135,9 +151,9 @@ void d2d_destroy(d2d_t* h) {
     if (h->acc) (void)hipFree(h->acc);
     if (h->scn) (void)hipFree(h->scn);
     if (h->env_scn) (void)hipFree(h->env_scn);
-    if (h->rc_bs) (void)hipFree(h->rc_bs);
-    if (h->rc_i) (void)hipFree(h->rc_i);
     if (h->rc_obs) (void)hipFree(h->rc_obs);
+    if (h->rc_rfl) (void)hipFree(h->rc_rfl);
+    if (h->rc_tag) (void)hipFree(h->rc_tag);
     delete h;
 }
 
@@ -189,6 +205,7 @@ int32_t d2d_set_scenarios(d2d_t* h, const d2d_scn* scns, int32_t n_scn, const in
         return hip_fail(e, "hipMemset env_scn");
     }
     h->n_scn = n_scn;
+    h->rc_dirty = true;  // cached reset observations belong to the old scenarios
     return D2D_OK;
 }
 
@@ -197,9 +214,6 @@ int32_t d2d_reset(d2d_t* h, const uint8_t* mask_dev, uint64_t seed, float* obs_d
     if (h->n_scn <= 0) return fail(D2D_E_STATE, "d2d_reset: call d2d_set_scenarios first");
     DeviceGuard g(h->device);
     h->seed = seed;
-    // cached next-reset observations depend on the seed and the episode counters: drop them all
-    hipError_t e = rc_invalidate(h, (hipStream_t)stream);
-    if (e != hipSuccess) return hip_fail(e, "d2d_reset: cache invalidate");
     StepArgs a = make_args(h);
     a.obs = obs_dev;
     a.mask = mask_dev;
@@ -208,8 +222,10 @@ int32_t d2d_reset(d2d_t* h, const uint8_t* mask_dev, uint64_t seed, float* obs_d
         hipLaunchKernelGGL(d2d_reset_kernel<true>, grid, dim3(BLOCK), sizeof(d2d::Scn) * h->n_scn, (hipStream_t)stream, a);
     else
         hipLaunchKernelGGL(d2d_reset_kernel<false>, grid, dim3(BLOCK), 0, (hipStream_t)stream, a);
-    e = hipGetLastError();
+    hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "d2d_reset launch");
+    // cached next-reset observations depend on the seed and the episode counters: drop and refill
+    if ((e = rc_rebuild(h, (hipStream_t)stream)) != hipSuccess) return hip_fail(e, "d2d_reset: cache rebuild");
     h->reset_done = true;
     return D2D_OK;
 }
@@ -221,6 +237,9 @@ int32_t d2d_step(d2d_t* h, const float* act_dev, float* obs_dev, float* rew_dev,
     if (!h->reset_done) return fail(D2D_E_STATE, "d2d_step: call d2d_reset first");
     if (((uintptr_t)act_dev & 7u) != 0) return fail(D2D_E_ARG, "d2d_step: act_dev must be 8-byte aligned");
     DeviceGuard g(h->device);
+    hipError_t e;
+    if (h->rc_dirty && (e = rc_rebuild(h, (hipStream_t)stream)) != hipSuccess)
+        return hip_fail(e, "d2d_step: cache rebuild");
     StepArgs a = make_args(h);
     a.act = act_dev;
     a.obs = obs_dev;
@@ -234,8 +253,11 @@ int32_t d2d_step(d2d_t* h, const float* act_dev, float* obs_dev, float* rew_dev,
         hipLaunchKernelGGL(d2d_step_kernel<true>, grid, dim3(K1_THREADS), sizeof(d2d::Scn) * h->n_scn, (hipStream_t)stream, a);
     else
         hipLaunchKernelGGL(d2d_step_kernel<false>, grid, dim3(K1_THREADS), 0, (hipStream_t)stream, a);
-    hipError_t e = hipGetLastError();
+    e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "d2d_step launch");
+    if (D2D_FILL_PERIOD > 0 && h->cfg.auto_reset && ++h->n_steps % D2D_FILL_PERIOD == 0 &&
+        (e = rc_fill(h, (hipStream_t)stream)) != hipSuccess)
+        return hip_fail(e, "d2d_step: cache fill");
     return D2D_OK;
 }
 
@@ -268,7 +290,7 @@ int32_t d2d_set_state(d2d_t* h, const double* state_dev, const int32_t* istate_d
         (e = hipMemcpyAsync(h->ist, istate_dev, sizeof(int32_t) * D2D_NISTATE * n, hipMemcpyDeviceToDevice,
                             (hipStream_t)stream)) != hipSuccess)
         return hip_fail(e, "d2d_set_state");
-    if ((e = rc_invalidate(h, (hipStream_t)stream)) != hipSuccess) return hip_fail(e, "d2d_set_state: cache invalidate");
+    if ((e = rc_rebuild(h, (hipStream_t)stream)) != hipSuccess) return hip_fail(e, "d2d_set_state: cache rebuild");
     h->reset_done = true;
     return D2D_OK;
 }

@@ -21,6 +21,7 @@
 // even with 7 scenario tables).
 //
 // K2 d2d_reset_kernel: masked reset, one lane per env.  K3 d2d_stats_kernel: fixed-order reduction.
+// K4 d2d_fill_kernel: fills the auto-reset observation cache (one lane per env).
 #pragma once
 #include "d2d_device.h"
 
@@ -73,31 +74,36 @@ struct StepArgs {
     float* tobs;
     const uint8_t* mask;     // reset kernel only
     uint64_t* stamps;        // diagnostic builds only (D2D_STAMPS): [waves][8] s_memtime stamps
-    // auto-reset observation cache (handle-internal; see K1 below)
-    double* rc_bs;           // [RC_NB][n] suspended Brent search of the next spawn
-    int32_t* rc_i;           // [RC_NI][n] path status, sensor status, Brent probe count, reset flags
+    // auto-reset observation cache (handle-internal; see "Auto-reset observation cache" below)
     float* rc_obs;           // [n][27] next reset observation
+    int32_t* rc_rfl;         // [n] flags of the next reset observation (LA lock)
+    int32_t* rc_tag;         // [n] episode counter the entry belongs to (-1: none)
 };
 
 // Auto-reset observation cache.  The observation an env gets when it auto-resets depends only on
-// (seed, env id, episode counter, scenario), so it is computed ahead of time, while the env is
-// still running, by the waves that would otherwise idle: W1 the sensor part (obs 0..18), W3 the
-// path part (Brent + obs 19..26 + LA-lock flag).  W3 runs the Brent search at the lowest wave
-// priority and suspends it (state in rc_bs) as soon as W2 finishes the step's own search, so the
-// fill never lengthens a step; an env that ends before its entry is ready falls back to the
-// synchronous computation.  Entries are invalidated by every reset / set_state.
-#ifndef D2D_RC_FILL
-#define D2D_RC_FILL 1    // diagnostic builds may disable W3's path-part fill (fallback only)
+// (seed, env id, episode counter, scenario), so it is computed ahead of time, while the env is still
+// running, by the fill kernel K4 that d2d_step launches after every D2D_FILL_PERIOD-th step (and
+// d2d_reset / d2d_set_state after theirs): one lane per env, every env whose entry is not tagged
+// with its current episode counter computes the spawn-state observation of its next episode.  K1
+// takes an entry only when its tag matches; otherwise (an episode shorter than the fill period) it
+// computes the observation synchronously.  Running the fill as its own kernel keeps it off K1's
+// issue slots: inside K1 it would run a whole wave for the ~0.5 of 64 envs that reset per step.
+#ifndef D2D_ABL
+#define D2D_ABL 0        // diagnostic builds only: bit r skips role r's compute, bit 4 = perfect
+                         // reset cache (no fills, every entry taken as ready): timing ablations
 #endif
-#ifndef D2D_RC_SLEEP
-#define D2D_RC_SLEEP 0   // s_sleep (x64 cycles) between W3 fill iterations
+#ifndef D2D_STOP_AFTER_PRE
+#define D2D_STOP_AFTER_PRE 0  // W2 raises `stop` after W0's reward part arrived (not right after its search)
 #endif
-constexpr int RC_NB = 10;             // a, b, fulc, ffulc, nfc, fnfc, xf, fx, rat, e
-constexpr int RC_PST = 0, RC_SST = 1, RC_NUM = 2, RC_RFLAGS = 3, RC_NI = 4;
-constexpr int RC_BRENT = 1, RC_UDONE = 2, RC_PATH = 4;   // path status bits (sensor status: 0 / 1)
+#ifndef D2D_W3_FILL_FIRST
+#define D2D_W3_FILL_FIRST 0   // W3 fills the cache before waiting for the joint sweep (obs tile write after)
+#endif
+#ifndef D2D_FILL_PERIOD
+#define D2D_FILL_PERIOD 16  // K4 after every this many steps (0: never; every reset synchronous)
+#endif
 
 // Diagnostic phase stamps (separate timing-only build, never in the product): lane 0 of each wave
-// records s_memtime at the phase boundaries of K1.
+// records s_memtime at the phase boundaries of K1 (slots 4, 5: role-specific hand-off points).
 #ifdef D2D_STAMPS
 #define STAMP(k)                                                                                       \
     do {                                                                                               \
@@ -171,72 +177,11 @@ __device__ __forceinline__ bool stop_seen(const uint32_t& stop) {
     return __builtin_amdgcn_readfirstlane(*(const volatile LdsU32*)&stop) != 0u;
 }
 __device__ __forceinline__ void stop_raise(uint32_t& stop) { *(volatile LdsU32*)&stop = 1u; }
-// W3's cache fill: advance the suspended Brent search of the next spawn of every env in `need`
-// until it converges or W2 raises `stop`, then (time permitting) finish the path part.
-__device__ __forceinline__ void rc_fill_path(const StepArgs& a, const Scn& S, int i, bool need, int32_t pst,
-                                             const uint32_t& stop) {
-    __builtin_amdgcn_s_setprio(0);
-    if (__ballot(need) == 0 || stop_seen(stop)) return;
-    const int n = a.n;
-    const PathK K = path_k(S);
-    double x = 0.0, y = 0.0, th = 0.0;
-    Brent B{};
-    const bool resumed = (pst & (RC_BRENT | RC_UDONE)) != 0;
-    if (need) {
-        const uint32_t ep = (uint32_t)fld(a.ist, D2D_I_EPISODE, n, i);
-        spawn_draw(S, a.seed, (uint32_t)a.cfg.env_id_base + (uint32_t)i, ep, x, y, th);
-        if (resumed) {
-            B.a = fld(a.rc_bs, 0, n, i);
-            B.b = fld(a.rc_bs, 1, n, i);
-            B.fulc = fld(a.rc_bs, 2, n, i);
-            B.ffulc = fld(a.rc_bs, 3, n, i);
-            B.nfc = fld(a.rc_bs, 4, n, i);
-            B.fnfc = fld(a.rc_bs, 5, n, i);
-            B.xf = fld(a.rc_bs, 6, n, i);
-            B.fx = fld(a.rc_bs, 7, n, i);
-            B.rat = fld(a.rc_bs, 8, n, i);
-            B.e = fld(a.rc_bs, 9, n, i);
-            B.num = fld(a.rc_i, RC_NUM, n, i);
-        } else {
-            brent_init(S, K, x, y, B);
-        }
-    }
-    bool act = need && !(pst & RC_UDONE) && brent_active(B);
-    while (__ballot(act) != 0 && !stop_seen(stop)) {
-        if (D2D_RC_SLEEP) __builtin_amdgcn_s_sleep(D2D_RC_SLEEP);  // leave issue slots to W2
-        if (act) {
-            brent_step(S, K, x, y, B);
-            act = brent_active(B);
-        }
-    }
-    if (need && !(pst & RC_UDONE)) {
-        pst = brent_active(B) ? RC_BRENT : RC_UDONE;
-        fld(a.rc_bs, 0, n, i) = B.a;
-        fld(a.rc_bs, 1, n, i) = B.b;
-        fld(a.rc_bs, 2, n, i) = B.fulc;
-        fld(a.rc_bs, 3, n, i) = B.ffulc;
-        fld(a.rc_bs, 4, n, i) = B.nfc;
-        fld(a.rc_bs, 5, n, i) = B.fnfc;
-        fld(a.rc_bs, 6, n, i) = B.xf;
-        fld(a.rc_bs, 7, n, i) = B.fx;
-        fld(a.rc_bs, 8, n, i) = B.rat;
-        fld(a.rc_bs, 9, n, i) = B.e;
-        fld(a.rc_i, RC_NUM, n, i) = B.num;
-    }
-    const bool tail = need && (pst & RC_UDONE);
-    if (__ballot(tail) != 0 && !stop_seen(stop)) {
-        if (tail) {
-            uint32_t f = 0;
-            double o[8];
-            path_obs_u(a.cfg, S, x, y, th, B.xf, f, o);
-            float* c = a.rc_obs + (size_t)i * D2D_OBS_DIM + 19;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) c[k] = (float)o[k];
-            fld(a.rc_i, RC_RFLAGS, n, i) = (int32_t)f;
-            pst = RC_PATH;
-        }
-    }
-    if (need) fld(a.rc_i, RC_PST, n, i) = pst;
+// scenario of the episode that follows episode counter `ep` of env j (curriculum pool: a fresh draw)
+__device__ __forceinline__ int next_scenario(const StepArgs& a, int j, uint32_t ep) {
+    if (a.n_scn <= 1) return 0;
+    if (a.cfg.scn_pool) return pool_pick(a.seed, (uint32_t)a.cfg.env_id_base + (uint32_t)j, ep, a.n_scn);
+    return a.env_scn[j];
 }
 
 // ------------------------------------------------------------------------------------------ K1
@@ -251,7 +196,8 @@ struct K1Shared {
     double sp[7][EPB];        // W3 -> W0: next-episode spawn of envs that end
     double cao[3][EPB];       // W1 -> W0: obs 8, 9, 10 (fp64)
     int scn[EPB];             // scenario index per env
-    uint32_t done[EPB];       // W3 -> W2: env ends this step
+    uint32_t done[EPB];       // W3 -> W1, W2: env ends this step
+    uint32_t cvalid[EPB];     // W3 -> W1: the env's reset-cache entry is ready
     uint32_t pflags[EPB];     // W2 -> W0: LA-lock bit after the path role
     uint32_t rflags[EPB];     // W3 -> W0: flags of the reset observation
     uint32_t f_done, f_ca, f_gs, f_pre, stop;
@@ -320,7 +266,7 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
         // ---------------------------------------------------------------- physics
         D2D_SETPRIO(D2D_PRIO_W0);
         double ov[19];
-        if (valid) {
+        if (valid && !(D2D_ABL & 1)) {
             Body B[3];
             double j[12];
 #pragma unroll
@@ -367,6 +313,7 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
             done = cause != 0;
         }
         flag_raise(sh.f_gs);
+        STAMP(4);
         // velocity part of the observation (obs 0-2, 17-18) into the tile / terminal obs
         if (valid) {
             sensor_vel(F0, ov);
@@ -387,6 +334,7 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
         }
         // frame / velocity / CA part of the reward, for W2
         flag_wait(sh.f_ca);
+        STAMP(5);
         if (valid) {
             ov[8] = sh.cao[0][lane];
             ov[9] = sh.cao[1][lane];
@@ -408,12 +356,12 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
     } else if (wave == 1) {
         // ---------------------------------------------------------------- sensing
         D2D_SETPRIO(D2D_PRIO_W1);
-        int32_t sst = 0;
         float row[19];
-        if (valid) {
+        bool need = false;
+        if (valid && !(D2D_ABL & 2)) {
             Body F = load_frame(a, i);
             done = step_cause(a, S, i, F) != 0;
-            if (auto_reset) sst = fld(a.rc_i, RC_SST, n, i);
+            need = done && auto_reset;
             double so[19];
             sensor_pos(a.cfg, S, F.px, F.py, F.a, so);
             sh.cao[0][lane] = so[8];
@@ -423,27 +371,33 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
 #pragma unroll
                 for (int k = 3; k < 17; ++k) trow[k] = (float)so[k];
             }
-            if (done && auto_reset && sst != 0) {
-                // cached spawn-state sensor part; the new episode's entry is refilled from next step
-                const float* c = a.rc_obs + (size_t)i * D2D_OBS_DIM;
 #pragma unroll
-                for (int k = 0; k < 19; ++k) row[k] = c[k];
-                fld(a.rc_i, RC_SST, n, i) = 0;
-            } else {
-                if (done && auto_reset) {
-                    double sp[7];
-                    spawn_state(a, SN, i, sp);
-                    sensor_obs(a.cfg, SN, Body{sp[0], sp[1], sp[2], 0.0, 0.0, 0.0}, so);
-                }
-#pragma unroll
-                for (int k = 0; k < 19; ++k) row[k] = (float)so[k];
-            }
+            for (int k = 0; k < 19; ++k) row[k] = (float)so[k];
         }
         flag_raise(sh.f_ca);
+        // envs that end: the spawn-state sensor part, from the cache when its entry is ready
+        if (__ballot(need) != 0ull) {
+            flag_wait(sh.f_done);
+            if (need) {
+                if (sh.cvalid[lane] != 0u) {
+                    const float* c = a.rc_obs + (size_t)i * D2D_OBS_DIM;
+#pragma unroll
+                    for (int k = 0; k < 19; ++k) row[k] = c[k];
+                } else {
+                    double sp[7], so[19];
+                    spawn_state(a, SN, i, sp);
+                    sensor_obs(a.cfg, SN, Body{sp[0], sp[1], sp[2], 0.0, 0.0, 0.0}, so);
+#pragma unroll
+                    for (int k = 0; k < 19; ++k) row[k] = (float)so[k];
+                }
+            }
+        }
+        STAMP(4);
         flag_wait(sh.f_gs);
+        STAMP(5);
         if (valid) {
             // a reset row holds the whole spawn-state sensor part, otherwise obs 3..16
-            if (done && auto_reset) {
+            if (need) {
 #pragma unroll
                 for (int k = 0; k < 19; ++k) orow[k] = row[k];
             } else {
@@ -451,33 +405,20 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
                 for (int k = 3; k < 17; ++k) orow[k] = row[k];
             }
         }
-        // cache fill: spawn-state sensor part of the next reset of envs that keep running, started
-        // only while W2's search is still running
-        __builtin_amdgcn_s_setprio(0);
-        if (auto_reset && !stop_seen(sh.stop)) {
-            if (valid && !done && sst == 0) {
-                double sp[7], so[19];
-                spawn_state(a, SN, i, sp);
-                sensor_obs(a.cfg, SN, Body{sp[0], sp[1], sp[2], 0.0, 0.0, 0.0}, so);
-                float* c = a.rc_obs + (size_t)i * D2D_OBS_DIM;
-#pragma unroll
-                for (int k = 0; k < 19; ++k) c[k] = (float)so[k];
-                fld(a.rc_i, RC_SST, n, i) = 1;
-            }
-        }
     } else if (wave == 2) {
         // ---------------------------------------------------------------- path search (critical)
         // the critical path, so it wins issue arbitration on its SIMD
         D2D_SETPRIO(D2D_PRIO_W2);
         double po[8];
-        if (valid) {
+        if (valid && !(D2D_ABL & 4)) {
             Body F = load_frame(a, i);
             advance_position(F);
             uint32_t f = (uint32_t)fld(a.ist, D2D_I_FLAGS, n, i);
             path_obs(a.cfg, S, F.px, F.py, F.a, f, po);
             sh.pflags[lane] = f & D2D_FLAG_LA_LOCK;
         }
-        stop_raise(sh.stop);
+        STAMP(4);
+        if (!D2D_STOP_AFTER_PRE) stop_raise(sh.stop);
         flag_wait(sh.f_done);
         flag_wait(sh.f_gs);
         if (valid) {
@@ -492,6 +433,8 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
             }
         }
         flag_wait(sh.f_pre);
+        if (D2D_STOP_AFTER_PRE) stop_raise(sh.stop);
+        STAMP(5);
         if (valid) {
             RewardPre R;
             R.aa = sh.u.p.pre[0][lane];
@@ -512,40 +455,39 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
     } else {
         // ---------------------------------------------------------------- auto-reset observation
         D2D_SETPRIO(D2D_PRIO_W3);
-        int32_t pst = 0;
         double po[8];
-        if (valid) {
+        bool cv = false;
+        if (valid && !(D2D_ABL & 8)) {
             Body F = load_frame(a, i);
             done = step_cause(a, S, i, F) != 0;
+            if (done && auto_reset) cv = (D2D_ABL & 16) != 0 || a.rc_tag[i] == fld(a.ist, D2D_I_EPISODE, n, i);
             sh.done[lane] = done ? 1u : 0u;
+            sh.cvalid[lane] = cv ? 1u : 0u;
         }
         flag_raise(sh.f_done);
-        if (valid) {
-            if (auto_reset) pst = fld(a.rc_i, RC_PST, n, i);
-            if (done && auto_reset) {
-                double sp[7];
-                spawn_state(a, SN, i, sp);
+        if (valid && done && auto_reset) {
+            double sp[7];
+            spawn_state(a, SN, i, sp);
 #pragma unroll
-                for (int k = 0; k < 7; ++k) sh.sp[k][lane] = sp[k];
-                if (pst & RC_PATH) {
-                    const float* c = a.rc_obs + (size_t)i * D2D_OBS_DIM + 19;
+            for (int k = 0; k < 7; ++k) sh.sp[k][lane] = sp[k];
+            if (cv) {
+                const float* c = a.rc_obs + (size_t)i * D2D_OBS_DIM + 19;
 #pragma unroll
-                    for (int k = 0; k < 8; ++k) po[k] = (double)c[k];
-                    sh.rflags[lane] = (uint32_t)fld(a.rc_i, RC_RFLAGS, n, i);
-                } else {
-                    uint32_t f = 0;
-                    path_obs(a.cfg, SN, sp[0], sp[1], sp[2], f, po);
-                    sh.rflags[lane] = f;
-                }
-                fld(a.rc_i, RC_PST, n, i) = 0;
+                for (int k = 0; k < 8; ++k) po[k] = (double)c[k];
+                sh.rflags[lane] = (uint32_t)a.rc_rfl[i];
+            } else {
+                uint32_t f = 0;
+                path_obs(a.cfg, SN, sp[0], sp[1], sp[2], f, po);
+                sh.rflags[lane] = f;
             }
         }
+        STAMP(4);
         flag_wait(sh.f_gs);
+        STAMP(5);
         if (valid && done && auto_reset) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) orow[19 + k] = (float)po[k];
         }
-        if (auto_reset && D2D_RC_FILL) rc_fill_path(a, SN, i, valid && !done && !(pst & RC_PATH), pst, sh.stop);
     }
     STAMP(2);
     __syncthreads();
@@ -662,6 +604,34 @@ __global__ __launch_bounds__(BLOCK) void d2d_reset_kernel(StepArgs a) {
 #pragma unroll
         for (int k = 0; k < D2D_OBS_DIM; ++k) a.obs[(size_t)i * D2D_OBS_DIM + k] = (float)obs[k];
     }
+}
+
+// ------------------------------------------------------------------------------ cache fill (K4)
+// one lane per env: an env whose entry does not belong to its current episode computes the
+// observation its next auto-reset will return (test-mode spawn of the next episode's scenario)
+template <bool LDS>
+__global__ __launch_bounds__(BLOCK) void d2d_fill_kernel(StepArgs a) {
+    extern __shared__ __attribute__((aligned(16))) Scn s_scn[];
+    const Scn* scns = stage_scenarios<LDS, BLOCK>(a, s_scn);
+    __syncthreads();
+    const int i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= a.n) return;
+    const int n = a.n;
+    const int32_t ep = fld(a.ist, D2D_I_EPISODE, n, i);
+    if (a.rc_tag[i] == ep) return;
+    const Scn& S = scns[next_scenario(a, i, (uint32_t)ep)];
+    double sp[7], so[19], o[8];
+    spawn_state(a, S, i, sp);
+    uint32_t f = 0;
+    sensor_obs(a.cfg, S, Body{sp[0], sp[1], sp[2], 0.0, 0.0, 0.0}, so);
+    path_obs(a.cfg, S, sp[0], sp[1], sp[2], f, o);
+    float* c = a.rc_obs + (size_t)i * D2D_OBS_DIM;
+#pragma unroll
+    for (int k = 0; k < 19; ++k) c[k] = (float)so[k];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) c[19 + k] = (float)o[k];
+    a.rc_rfl[i] = (int32_t)f;
+    a.rc_tag[i] = ep;
 }
 
 // ------------------------------------------------------------------------------------ self-test

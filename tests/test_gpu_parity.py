@@ -68,7 +68,7 @@ def test_vs_oracle_teacher_forced(d2, scn):
 
 
 def test_reset_cache_invalidation(d2):
-    """The auto-reset observation cache (filled ahead of time by the idle waves) must be dropped
+    """The auto-reset observation cache (filled ahead of time by the fill kernel) must be dropped
     by a full reset with a new seed and by set_state (episode counters may change)."""
     venv, orc = make_pair(d2, 2048, ["corridor"], seed=99, kwargs=_cfgkw())
     rng = np.random.default_rng(4)

@@ -4,8 +4,10 @@
     python tools/stamps.py build        # CPU container
     python tools/stamps.py run [--scenario S] [--envs N]   # GPU box
 
-Stamps per wave: 0 start, 1 after scenario staging, 2 end of phase-1 work, 3 after barrier 1,
-4 end of phase-2 work, 5 after barrier 2, 6 end.  Reported in shader cycles per role (wave 0..3).
+Stamps per wave: 0 start, 1 after scenario staging, 2 end of the role's work, 3 after the barrier,
+4/5 role-specific hand-off points (W0 physics done / CA received, W1 sensing done / joint sweep
+received, W2 search done / reward part received, W3 reset part done / joint sweep received), 6 end.
+Reported in shader cycles from stamp 1, per role (wave 0..3): [median, p95, max].
 """
 from __future__ import annotations
 
@@ -57,12 +59,17 @@ def run(scenario, n, steps_warm, lib=LIB):
     s = buf.cpu().numpy().reshape(-1, 4, 8).astype(np.int64)
     t0 = s[:, :, 0].min()
     res = {"scenario": scenario, "envs": n, "kernel_span_cycles": int(s[:, :, 6].max() - t0)}
-    names = ["stage", "phase1", "barrier1", "phase2", "barrier2", "phase3"]
+    # cumulative times from the wave's stamp 1 (after staging): [median, p95, max]
+    marks = {0: {"physics_done": 4, "ca_received": 5},
+             1: {"sensing_done": 4, "gs_received": 5},
+             2: {"search_done": 4, "pre_received": 5},
+             3: {"reset_part_done": 4, "gs_received": 5}}
     for w in range(4):
-        d = np.diff(s[:, w, :7], axis=1)
-        res[f"wave{w}"] = {nm: [int(np.median(d[:, k])), int(np.percentile(d[:, k], 95)), int(d[:, k].max())]
-                           for k, nm in enumerate(names)}
-        res[f"wave{w}"]["total"] = [int(np.median(s[:, w, 6] - s[:, w, 0])), int((s[:, w, 6] - s[:, w, 0]).max())]
+        r = {"stage": [int(np.median(s[:, w, 1] - s[:, w, 0]))]}
+        for nm, k in list(marks[w].items()) + [("role_done", 2), ("barrier", 3), ("end", 6)]:
+            d = s[:, w, k] - s[:, w, 1]
+            r[nm] = [int(np.median(d)), int(np.percentile(d, 95)), int(d.max())]
+        res[f"wave{w}"] = r
     # placement: slot 7 = XCC_ID << 32 | HW_ID (wave, simd [5:4], cu [11:8], sh [12], se [15:13])
     hw = s[:, :, 7]
     xcc = (hw >> 32) & 0xF
