@@ -206,7 +206,7 @@ def main():
                        "outputs": "obs f32[N,27], reward f32, terminated/truncated u8 (info rows off)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "d2d_step_kernel", "kernel_ms": kern_ms,
+                         "kernel": "d2d_step_kernel + d2d_fill_kernel/16 (per step)", "kernel_ms": kern_ms,
                          "bytes_per_env_step": BYTES_PER_ENV_STEP},
             "episodes": {"finished": float(st[1]), "mean_return": float(st[0] / max(st[1], 1)),
                          "success": float(st[2]), "collisions": float(st[4]),

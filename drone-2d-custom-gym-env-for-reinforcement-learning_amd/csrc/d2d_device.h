@@ -103,10 +103,10 @@ __device__ __forceinline__ double div_by_recip(double a, double b, double y) {
     const double r = fma(-q, b, a);
     return fma(r, y, q);
 }
-// Correctly rounded sqrt for x == 0 or 2^-767 <= x < inf: the device library's sequence (rsq
-// estimate + Goldschmidt/Newton refinement) without its range-scaling steps, which only act below
-// 2^-767.  Squared distances between fp64 points are 0 or far above that.  Checked bitwise against
-// sqrt() by d2d_selftest.
+// Correctly rounded sqrt for x = +-0, +inf, NaN or x >= 2^-767: the device library's sequence
+// (rsq estimate + Goldschmidt/Newton refinement) without its range-scaling steps, which only act
+// below 2^-767.  Squared distances between fp64 points are 0 or far above that.  Checked bitwise
+// against sqrt() by d2d_selftest.
 __device__ __forceinline__ double sqrt_nz(double x) {
     const double y = __builtin_amdgcn_rsq(x);
     double g = x * y;
@@ -118,8 +118,13 @@ __device__ __forceinline__ double sqrt_nz(double x) {
     g = fma(d, h, g);
     d = fma(-g, g, x);
     g = fma(d, h, g);
-    return (x == 0.0) ? x : g;
+    // +-0 and +inf return themselves (the refinement would give NaN for inf), NaN propagates
+    return __builtin_amdgcn_class(x, 0x260) ? x : g;
 }
+#ifndef D2D_SQRT_NZ
+#define D2D_SQRT_NZ 1   // distances: range-limited sqrt (squared fp64 distances are 0 or >= 2^-767)
+#endif
+__device__ __forceinline__ double sqrt_dist(double x) { return D2D_SQRT_NZ ? sqrt_nz(x) : sqrt(x); }
 // Correctly rounded a / b for normal operands with a normal quotient (no div_scale / div_fixup
 // range handling: results for zero / inf / NaN / extreme-exponent operands are unspecified).
 // Checked bitwise against '/' by d2d_selftest.
@@ -165,7 +170,7 @@ __device__ __forceinline__ double m1to1(double v, double lo, double hi) { return
 __device__ __forceinline__ double invm1to1(double v, double lo, double hi) { return (v + 1.0) * (hi - lo) / 2.0 + lo; }
 __device__ __forceinline__ double clipd(double x, double lo, double hi) { return x < lo ? lo : (x > hi ? hi : x); }
 // np.linalg.norm of a 2-vector == sqrt(OpenBLAS ddot) == sqrt(fma(dy, dy, dx*dx))
-__device__ __forceinline__ double norm2(double dx, double dy) { return sqrt(fma(dy, dy, dx * dx)); }
+__device__ __forceinline__ double norm2(double dx, double dy) { return sqrt_dist(fma(dy, dy, dx * dx)); }
 // np.sign(x) + (x == 0): 1 for x > 0 and +-0, -1 for x < 0, NaN for NaN (two selects)
 __device__ __forceinline__ double sgn_nz(double x) {
     const double s = (x < 0.0) ? -1.0 : 1.0;
@@ -243,9 +248,9 @@ __device__ __forceinline__ PathK path_k(const Scn& s) {
 // and the reference's case analysis picks the result with selects (same arithmetic per case).
 // first <=> n == 0 && u >= us[0];  last <=> u in [us[nw-2] - 0.001, L] or n == nw-1, and in every
 // first / last case the record's "B" quadratic is the one the reference uses (scn_build).
-__device__ __forceinline__ void path_eval(const Scn& s, const PathK& K, double u, double& x, double& y) {
+__device__ __forceinline__ void path_eval_n(const Scn& s, const PathK& K, double u, int n, double& x, double& y,
+                                            double& u1_out) {
     const int nw = K.nw;
-    const int n = u_index(s, u);
     double r[REC_N];
 #pragma unroll
     for (int f = 0; f < REC_N; ++f) r[f] = s.rec[f][n];
@@ -264,13 +269,19 @@ __device__ __forceinline__ void path_eval(const Scn& s, const PathK& K, double u
     const double xb = mu_r * xB + mu_f * xA, yb = mu_r * yB + mu_f * yA;
     x = blend ? xb : xB;
     y = blend ? yb : yB;
+    u1_out = u1;
+}
+__device__ __forceinline__ void path_eval(const Scn& s, const PathK& K, double u, double& x, double& y) {
+    double u1;
+    path_eval_n(s, K, u, u_index(s, u), x, y, u1);
 }
 __device__ __forceinline__ void path_eval(const Scn& s, double u, double& x, double& y) {
     path_eval(s, path_k(s), u, x, y);
 }
-__device__ __forceinline__ double path_dist(const Scn& s, const PathK& K, double u, double px, double py) {
+__device__ __forceinline__ double path_dist_n(const Scn& s, const PathK& K, double u, int n, double px, double py,
+                                              double& u1) {
     double x, y;
-    path_eval(s, K, u, x, y);
+    path_eval_n(s, K, u, n, x, y, u1);
     // (sqrt_nz measured slower here than the library sequence: tools/ubench_brent.py)
     return norm2(x - px, y - py);
 }
@@ -280,9 +291,15 @@ __device__ __forceinline__ double path_dist(const Scn& s, const PathK& K, double
 // The search state is explicit so that a search can be suspended and resumed bit-exactly (the
 // auto-reset observation cache runs it in slices across steps); xm / tol1 / tol2 are functions of
 // the state, recomputed exactly as scipy recomputes them at the end of each iteration.
+// Knot-interval tracking: u_index is monotone in u, so a probe u in [a, b] has
+// idx(a) <= idx(u) <= idx(b).  The state carries ia = idx(a), ib = idx(b), ixf = idx(xf) and the
+// knots ka = us[ia + 1], kxf = us[ixf + 1] (each taken from the record of the probe that set it);
+// once the bracket spans at most two intervals (ib <= ia + 1) a probe's index is
+// min(ia + !(u <= ka), nw - 1) -- one compare instead of the knot scan.  Exact: it is the same count.
 struct Brent {
     double a, b, fulc, ffulc, nfc, fnfc, xf, fx, rat, e;
-    int num;
+    double ka, kxf;
+    int num, ia, ib, ixf;
 };
 constexpr double BR_SQRT_EPS = 1.4832396974191326e-08;  // sqrt(2.2e-16)
 constexpr double BR_GOLDEN = 0.3819660112501051;        // 0.5*(3.0 - sqrt(5.0))
@@ -295,7 +312,11 @@ __device__ __forceinline__ void brent_init(const Scn& s, const PathK& K, double 
     B.xf = B.fulc;
     B.rat = 0.0;
     B.e = 0.0;
-    B.fx = path_dist(s, K, B.xf, px, py);
+    B.ia = u_index(s, B.a);
+    B.ib = u_index(s, B.b);
+    B.ka = s.rec[REC_U1][B.ia];
+    B.ixf = u_index(s, B.xf);
+    B.fx = path_dist_n(s, K, B.xf, B.ixf, px, py, B.kxf);
     B.num = 1;
     B.ffulc = B.fx;
     B.fnfc = B.fx;
@@ -329,16 +350,43 @@ __device__ __forceinline__ void brent_step(const Scn& s, const PathK& K, double 
     B.e = par ? B.rat : e_g;
     const double rat = par ? rat_p : rat_g;
     B.rat = rat;
-    const double ar = fabs(rat);
-    const double mx = (ar != ar) ? ar : (ar > tol1 ? ar : tol1);
-    const double x = xf + sgn_nz(rat) * mx;
-    const double fu = path_dist(s, K, x, px, py);
+    // x = xf + (sign(rat) + (rat == 0)) * max(|rat|, tol1).  rat is finite (a, b, xf are, and the
+    // parabolic step is taken only when |p/q| < |e|/2), so np.max's NaN rule never applies and the
+    // product is exactly -mx for rat < 0 and +mx otherwise
+    const double mx = fmax(fabs(rat), tol1);
+    const double x = xf + ((rat < 0.0) ? -mx : mx);
+    // knot interval of x: one compare once the bracket spans <= 2 intervals (wave-uniform choice)
+    const bool fast = (x >= a) & (x <= b) & (B.ib <= B.ia + 1);
+    int ix;
+    if (__ballot(!fast) == 0ull) {
+        ix = min(B.ia + ((x <= B.ka) ? 0 : 1), K.nw - 1);
+    } else {
+        // the knot scan re-reads the knots each time (an opaque pointer stops the compiler from
+        // keeping all 15 in registers across the loop: the fast path does not need them)
+        const Scn* sp = &s;
+        asm volatile("" : "+v"(sp));
+        ix = u_index(*sp, x);
+    }
+    double kx;
+    const double fu = path_dist_n(s, K, x, ix, px, py, kx);
     B.num += 1;
     const bool le = fu <= fx;
     const bool c1 = !le & ((fu <= B.fnfc) | (nfc == xf));
     const bool c2 = !le & !c1 & ((fu <= B.ffulc) | (fulc == xf) | (fulc == nfc));
-    B.a = le ? ((x >= xf) ? xf : a) : ((x < xf) ? x : a);
-    B.b = le ? ((x >= xf) ? b : xf) : ((x < xf) ? b : x);
+    // a <- (le ? xf : x) when le == (x >= xf), b <- the same value when le != (x >= xf): scipy's
+    // four cases (x, xf are finite, so x >= xf and x < xf are complements)
+    const bool ge = x >= xf;
+    const bool to_a = le == ge;
+    const double t = le ? xf : x;
+    const int ti = le ? B.ixf : ix;
+    const double tk = le ? B.kxf : kx;
+    B.a = to_a ? t : a;
+    B.b = to_a ? b : t;
+    B.ia = to_a ? ti : B.ia;
+    B.ka = to_a ? tk : B.ka;
+    B.ib = to_a ? B.ib : ti;
+    B.ixf = le ? ix : B.ixf;
+    B.kxf = le ? kx : B.kxf;
     const double nfulc = (le | c1) ? nfc : (c2 ? x : fulc);
     const double nffulc = (le | c1) ? B.fnfc : (c2 ? fu : B.ffulc);
     const double nnfc = le ? xf : (c1 ? x : nfc);
@@ -634,7 +682,7 @@ __device__ __forceinline__ void sensor_pos(const d2d_cfg& cfg, const Scn& s, dou
         q = (q1 < q) ? q1 : q;
         q = (q2 < q) ? q2 : q;
         q = (q3 < q) ? q3 : q;
-        const double d = sqrt(q) - s.cr[i];
+        const double d = sqrt_dist(q) - s.cr[i];
         // stable ascending insertion into the top-3 (equal keys keep index order)
         const bool l0 = (bi0 < 0) || d < bd0, l1 = (bi1 < 0) || d < bd1, l2 = (bi2 < 0) || d < bd2;
         bd2 = l1 ? bd1 : (l2 ? d : bd2);
@@ -706,39 +754,6 @@ __device__ __forceinline__ void path_obs(const d2d_cfg& cfg, const Scn& s, doubl
 
 // ------------------------------------------------------------------------------ reward
 // The reward decodes from the fp64 observation exactly as the reference does (drone_2d_env.py:423-572).
-struct CAPart {  // computed by the sensor role (obs 0..18 only)
-    double vel_ang, ca, lpa, lca, dclose;
-};
-__device__ __forceinline__ CAPart reward_ca_part(const d2d_cfg& cfg, const Scn& s, const double* o) {
-    const double W = cfg.screen_w, H = cfg.screen_h;
-    CAPart P;
-    P.vel_ang = pymod_2pi(atan2(o[17] * PI, o[18] * PI) + TWO_PI);
-    P.lpa = 1.0;
-    P.lca = 1.0;
-    P.ca = 0.0;
-    P.dclose = __builtin_inf();
-    if (s.n_circles > 0) {
-        const double diag = sqrt(W * W + H * H);
-        const double d = invm1to1(o[8], 0.0, diag);
-        P.dclose = d;
-        const double oa = pymod_2pi(atan2(o[9], o[10]) + TWO_PI);
-        const double adiff = fabs((pymod_2pi(oa - P.vel_ang + PI) - PI) * (180.0 / PI));
-        const double Rr = cfg.danger_range, A = cfg.danger_angle, k = cfg.abs_inv_ca_min_rew;
-        if (d < Rr && cfg.use_lambda) {
-            const double l = (d / Rr) / 2.0;
-            P.lpa = (l < 0.10) ? 0.10 : l;
-            P.lca = 1.0 - P.lpa;
-        }
-        if (d < Rr) {
-            double rr = -(((Rr + k * Rr) / (d + k * Rr)) - 1.0);
-            double ar = -(((A + k * A) / (adiff + k * A)) - 1.0);
-            ar = (ar > 0.0) ? 0.0 : ar;
-            rr = (rr > 0.0) ? 0.0 : rr;
-            P.ca = rr + ar;
-        }
-    }
-    return P;
-}
 // end conditions that need only the post-physics frame (drone_2d_env.py:543-571): collision,
 // reach-end (decoded target distance), AA (decoded alpha), time-up.  Known before the observation,
 // which lets the cooperative kernel start the auto-reset observation concurrently.
@@ -754,61 +769,46 @@ __device__ __forceinline__ int end_cause(const d2d_cfg& cfg, const Scn& s, const
     if (t == cfg.n_steps) cause |= D2D_END_TIMEUP;
     return cause;
 }
-struct Reward {
-    double reward, ca, pa, pp, coll, reach, aa, dclose, dist_path;
-    int cause;
+// reward_final split at its data dependencies, for the cooperative kernel (same arithmetic, same
+// summation order):
+//   CAStatic   obs 8..10 only (sensor role): closest distance, obstacle angle, lambdas, range term
+//   RewardPos  the post-position frame + end cause (path role, while it waits for the physics)
+//   RewardVel  the post-sweep velocity (physics role): speed term, velocity angle, CA total
+//   reward_path / reward_sum   the path-observation terms, then the sum (path role)
+struct CAStatic {
+    double d, oa, lpa, lca, rr, near;
 };
-// final combination (path-role results o19..26 = po[0..7], CA part from the sensor role)
-__device__ __forceinline__ Reward reward_final(const d2d_cfg& cfg, const Body& F, const double* po,
-                                               const CAPart& P, int cause) {
+__device__ __forceinline__ CAStatic ca_static(const d2d_cfg& cfg, const Scn& s, const double* o) {
     const double W = cfg.screen_w, H = cfg.screen_h;
-    Reward R;
-    const double vxd = invm1to1(m1to1(F.vx, -VEL_MAX, VEL_MAX), -VEL_MAX, VEL_MAX);
-    const double vyd = invm1to1(m1to1(F.vy, -VEL_MAX, VEL_MAX), -VEL_MAX, VEL_MAX);
-    const double alpha = (F.a / PI) * PI;
-    const double pxd = invm1to1(m1to1(F.px, 0.0, W), 0.0, W), pyd = invm1to1(m1to1(F.py, 0.0, H), 0.0, H);
-    const double cpx = invm1to1(po[0], 0.0, W), cpy = invm1to1(po[1], 0.0, H);
-    const double la_ang = pymod_2pi(atan2(po[4], po[5]) + TWO_PI);
-    const double dist = norm2(cpx - pxd, cpy - pyd);
-    R.dist_path = dist;
-    const double pa = -(2.0 * (clipd(dist, 0.0, cfg.pa_band_edge) / cfg.pa_band_edge) - 1.0) * cfg.pa_scale;
-    const double vel = sqrt(vxd * vxd + vyd * vyd);
-    const double sv = vel * cfg.pp_vel_scale;
-    const double vla = fabs(pymod_2pi(la_ang - P.vel_ang + PI) - PI);
-    const double pp = clipd(cos(vla) * sv, cfg.pp_rew_min, cfg.pp_rew_max);
-    const double coll = (cause & D2D_END_COLLISION) ? cfg.rew_collision : 0.0;
-    const double reach = (cause & D2D_END_REACH) ? cfg.rew_reach_end : 0.0;
-    double aa = 0.0;
-    if (alpha > cfg.aa_band) aa = -sin(alpha);
-    if (alpha < -cfg.aa_band) aa = sin(alpha);
-    if (cause & D2D_END_AA) aa = cfg.rew_aa;
-    R.reward = aa + pa * P.lpa + pp + coll + P.ca * P.lca + reach;
-    R.ca = P.ca * P.lca;
-    R.pa = pa * P.lpa;
-    R.pp = pp;
-    R.coll = coll;
-    R.reach = reach;
-    R.aa = aa;
-    R.dclose = P.dclose;
-    R.cause = cause;
-    return R;
+    CAStatic C{__builtin_inf(), 0.0, 1.0, 1.0, 0.0, 0.0};
+    if (s.n_circles > 0) {
+        const double diag = sqrt(W * W + H * H);
+        const double d = invm1to1(o[8], 0.0, diag);
+        C.d = d;
+        C.oa = pymod_2pi(atan2(o[9], o[10]) + TWO_PI);
+        const double Rr = cfg.danger_range, k = cfg.abs_inv_ca_min_rew;
+        if (d < Rr && cfg.use_lambda) {
+            const double l = (d / Rr) / 2.0;
+            C.lpa = (l < 0.10) ? 0.10 : l;
+            C.lca = 1.0 - C.lpa;
+        }
+        if (d < Rr) {
+            const double rr = -(((Rr + k * Rr) / (d + k * Rr)) - 1.0);
+            C.rr = (rr > 0.0) ? 0.0 : rr;
+            C.near = 1.0;
+        }
+    }
+    return C;
 }
-
-// reward_final split at its data dependencies, for the cooperative kernel: the part that needs only
-// the post-step frame and the CA part (known long before the path search ends) ...
-struct RewardPre {
-    double aa, lpa, coll, cal, reach, sv, vel_ang, pxd, pyd;
+struct RewardPos {
+    double aa, coll, reach, pxd, pyd;
 };
-__device__ __forceinline__ RewardPre reward_pre(const d2d_cfg& cfg, const Body& F, const CAPart& P, int cause) {
+__device__ __forceinline__ RewardPos reward_pos(const d2d_cfg& cfg, const Body& F, int cause) {
     const double W = cfg.screen_w, H = cfg.screen_h;
-    RewardPre R;
-    const double vxd = invm1to1(m1to1(F.vx, -VEL_MAX, VEL_MAX), -VEL_MAX, VEL_MAX);
-    const double vyd = invm1to1(m1to1(F.vy, -VEL_MAX, VEL_MAX), -VEL_MAX, VEL_MAX);
+    RewardPos R;
     const double alpha = (F.a / PI) * PI;
     R.pxd = invm1to1(m1to1(F.px, 0.0, W), 0.0, W);
     R.pyd = invm1to1(m1to1(F.py, 0.0, H), 0.0, H);
-    const double vel = sqrt(vxd * vxd + vyd * vyd);
-    R.sv = vel * cfg.pp_vel_scale;
     R.coll = (cause & D2D_END_COLLISION) ? cfg.rew_collision : 0.0;
     R.reach = (cause & D2D_END_REACH) ? cfg.rew_reach_end : 0.0;
     double aa = 0.0;
@@ -816,28 +816,53 @@ __device__ __forceinline__ RewardPre reward_pre(const d2d_cfg& cfg, const Body& 
     if (alpha < -cfg.aa_band) aa = sin(alpha);
     if (cause & D2D_END_AA) aa = cfg.rew_aa;
     R.aa = aa;
-    R.lpa = P.lpa;
-    R.cal = P.ca * P.lca;
-    R.vel_ang = P.vel_ang;
     return R;
 }
-// ... and the part that needs the path observation (po = obs 19..26).  Same arithmetic and the
-// same summation order as reward_final.
-struct RewardPost {
-    double reward, pa, pp, dist;
+struct RewardVel {
+    double sv, vel_ang, cal;
 };
-__device__ __forceinline__ RewardPost reward_post(const d2d_cfg& cfg, const RewardPre& R, const double* po) {
+// o = obs with entries 0, 1, 17, 18 filled (sensor_vel)
+__device__ __forceinline__ RewardVel reward_vel(const d2d_cfg& cfg, const double* o, const CAStatic& C) {
+    RewardVel R;
+    const double vxd = invm1to1(o[0], -VEL_MAX, VEL_MAX);
+    const double vyd = invm1to1(o[1], -VEL_MAX, VEL_MAX);
+    R.sv = sqrt(vxd * vxd + vyd * vyd) * cfg.pp_vel_scale;
+    R.vel_ang = pymod_2pi(atan2(o[17] * PI, o[18] * PI) + TWO_PI);
+    double ca = 0.0;
+    if (C.near != 0.0) {
+        const double A = cfg.danger_angle, k = cfg.abs_inv_ca_min_rew;
+        const double adiff = fabs((pymod_2pi(C.oa - R.vel_ang + PI) - PI) * (180.0 / PI));
+        double ar = -(((A + k * A) / (adiff + k * A)) - 1.0);
+        ar = (ar > 0.0) ? 0.0 : ar;
+        ca = C.rr + ar;
+    }
+    R.cal = ca * C.lca;
+    return R;
+}
+struct RewardPath {
+    double la_ang, dist, pa;
+};
+__device__ __forceinline__ RewardPath reward_path(const d2d_cfg& cfg, const RewardPos& P, const CAStatic& C,
+                                                  const double* po) {
     const double W = cfg.screen_w, H = cfg.screen_h;
-    RewardPost Q;
+    RewardPath Q;
     const double cpx = invm1to1(po[0], 0.0, W), cpy = invm1to1(po[1], 0.0, H);
-    const double la_ang = pymod_2pi(atan2(po[4], po[5]) + TWO_PI);
-    Q.dist = norm2(cpx - R.pxd, cpy - R.pyd);
+    Q.la_ang = pymod_2pi(atan2(po[4], po[5]) + TWO_PI);
+    Q.dist = norm2(cpx - P.pxd, cpy - P.pyd);
     const double pa = -(2.0 * (clipd(Q.dist, 0.0, cfg.pa_band_edge) / cfg.pa_band_edge) - 1.0) * cfg.pa_scale;
-    const double vla = fabs(pymod_2pi(la_ang - R.vel_ang + PI) - PI);
-    Q.pp = clipd(cos(vla) * R.sv, cfg.pp_rew_min, cfg.pp_rew_max);
-    Q.pa = pa * R.lpa;
-    Q.reward = R.aa + Q.pa + Q.pp + R.coll + R.cal + R.reach;
+    Q.pa = pa * C.lpa;
     return Q;
+}
+struct RewardSum {
+    double reward, pp;
+};
+__device__ __forceinline__ RewardSum reward_sum(const d2d_cfg& cfg, const RewardPos& P, const RewardVel& V,
+                                                const RewardPath& Q) {
+    RewardSum S;
+    const double vla = fabs(pymod_2pi(Q.la_ang - V.vel_ang + PI) - PI);
+    S.pp = clipd(cos(vla) * V.sv, cfg.pp_rew_min, cfg.pp_rew_max);
+    S.reward = P.aa + Q.pa + S.pp + P.coll + V.cal + P.reach;
+    return S;
 }
 
 // full single-lane observation (reset kernel)

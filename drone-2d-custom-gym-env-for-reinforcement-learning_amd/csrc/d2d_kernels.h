@@ -6,13 +6,14 @@
 // only on its pre-step position and velocity (forces act on velocities), so every wave derives it
 // from the state in HBM and no wave waits for another before its own chain:
 //
-//   W0  load state, thrust, 3-body position update, collision, end cause, 6-pivot joint sweep,
-//       store the state; velocity part of the observation (obs 0-2, 17-18); frame / CA part of
-//       the reward
+//   W0  load state, thrust, 3-body position update, collision, end cause (published to the other
+//       waves at once), 6-pivot joint sweep,
+//       store the state; velocity part of the observation (obs 0-2, 17-18) and of the reward
 //   W1  sensor part (obs 3..16, CA inputs); for envs that end: the spawn-state sensor part
-//   W2  path role: Brent closest point, obs 19..26, then the path part of the reward
-//   W3  end test first (for W2), then for envs that end: the spawn-state path part
-//   W1 and W3 then fill the auto-reset observation cache (below) while W2 is still searching.
+//   W2  path role: Brent closest point, obs 19..26, the position / path terms of the reward while
+//       the physics wave finishes, then the sum
+//   W3  for envs that end: the spawn-state path part
+//   (W1 and W3 take the spawn-state parts from the auto-reset observation cache when it is ready)
 //   epilogue (after the one barrier): the 64x27 f32 obs tile is stored as one contiguous span;
 //   W0 writes reward / flags / info / bookkeeping / auto-reset state.
 //
@@ -35,10 +36,10 @@ constexpr int K1_THREADS = 256; // K1: 4 waves
 // budget (160 KB / 4); larger sets are read from global memory (L1/L2 resident)
 constexpr size_t K1_LDS_BUDGET = 40 * 1024;
 constexpr size_t K2_LDS_BUDGET = 64 * 1024;
-// Wave priorities per role (s_setprio, 0..3) for phase A: the Brent waves win issue arbitration
-// on their SIMD over the other workgroups' physics / sensing waves.
+// Wave priorities per role (s_setprio, 0..3): the Brent waves win issue arbitration on their SIMD,
+// the physics waves come next (their 10-sweep joint chain must end before the search does).
 #ifndef D2D_PRIO_W0
-#define D2D_PRIO_W0 0
+#define D2D_PRIO_W0 2
 #endif
 #ifndef D2D_PRIO_W1
 #define D2D_PRIO_W1 0
@@ -92,12 +93,6 @@ struct StepArgs {
 #define D2D_ABL 0        // diagnostic builds only: bit r skips role r's compute, bit 4 = perfect
                          // reset cache (no fills, every entry taken as ready): timing ablations
 #endif
-#ifndef D2D_STOP_AFTER_PRE
-#define D2D_STOP_AFTER_PRE 0  // W2 raises `stop` after W0's reward part arrived (not right after its search)
-#endif
-#ifndef D2D_W3_FILL_FIRST
-#define D2D_W3_FILL_FIRST 0   // W3 fills the cache before waiting for the joint sweep (obs tile write after)
-#endif
 #ifndef D2D_FILL_PERIOD
 #define D2D_FILL_PERIOD 16  // K4 after every this many steps (0: never; every reset synchronous)
 #endif
@@ -145,17 +140,8 @@ __device__ __forceinline__ Body load_frame(const StepArgs& a, int i) {
     return Body{fld(a.st, 0, n, i), fld(a.st, 1, n, i), fld(a.st, 2, n, i),
                 fld(a.st, 3, n, i), fld(a.st, 4, n, i), fld(a.st, 5, n, i)};
 }
-// end cause of this step from the pre-step state: position update + contact + end tests
-__device__ __forceinline__ int step_cause(const StepArgs& a, const Scn& S, int i, Body& F) {
-    const int n = a.n;
-    const bool hit = frame_advance(S, F);
-    const uint32_t fl = (uint32_t)fld(a.ist, D2D_I_FLAGS, n, i);
-    const int t = fld(a.ist, D2D_I_T, n, i) + 1;
-    return end_cause(a.cfg, S, F, hit || (fl & D2D_FLAG_COLLIDED) != 0, t);
-}
 // next-episode spawn (test-mode reset, drone_2d_env.py:218-311, Drone.py:20-52)
-__device__ __forceinline__ void spawn_state(const StepArgs& a, const Scn& S, int i, double sp[7]) {
-    const uint32_t ep = (uint32_t)fld(a.ist, D2D_I_EPISODE, a.n, i);
+__device__ __forceinline__ void spawn_state(const StepArgs& a, const Scn& S, int i, uint32_t ep, double sp[7]) {
     double x, y, th;
     spawn_draw(S, a.seed, (uint32_t)a.cfg.env_id_base + (uint32_t)i, ep, x, y, th);
     double sl, cl, sr, cr;
@@ -173,10 +159,9 @@ __device__ __forceinline__ void spawn_state(const StepArgs& a, const Scn& S, int
 // wave-uniform read of an LDS flag written by another wave of the workgroup
 // (explicit LDS address space: a generic volatile access would become a flat load)
 using LdsU32 = __attribute__((address_space(3))) uint32_t;
-__device__ __forceinline__ bool stop_seen(const uint32_t& stop) {
-    return __builtin_amdgcn_readfirstlane(*(const volatile LdsU32*)&stop) != 0u;
+__device__ __forceinline__ bool flag_seen(const uint32_t& f) {
+    return __builtin_amdgcn_readfirstlane(*(const volatile LdsU32*)&f) != 0u;
 }
-__device__ __forceinline__ void stop_raise(uint32_t& stop) { *(volatile LdsU32*)&stop = 1u; }
 // scenario of the episode that follows episode counter `ep` of env j (curriculum pool: a fresh draw)
 __device__ __forceinline__ int next_scenario(const StepArgs& a, int j, uint32_t ep) {
     if (a.n_scn <= 1) return 0;
@@ -187,25 +172,24 @@ __device__ __forceinline__ int next_scenario(const StepArgs& a, int j, uint32_t 
 // ------------------------------------------------------------------------------------------ K1
 // Intra-workgroup hand-offs are LDS flags (raised after a release fence, polled with s_sleep), so
 // no wave waits at a barrier for work it does not depend on.  Dependencies (all acyclic):
-//   f_done  W3 -> W2        which envs end this step (W3 derives it first thing)
-//   f_ca    W1 -> W0        obs 8..10 for the CA reward part
+//   f_done  W0 -> W1,W2,W3  which envs end this step, cache readiness (right after the positions)
+//   f_ca    W1 -> W0,W2     CA inputs from obs 8..10 (CAStatic)
 //   f_gs    W0 -> W1,W2,W3  joint sweep finished: the jb region becomes the obs tile
-//   f_pre   W0 -> W2        frame/velocity/CA part of the reward
-//   stop    W2 -> W1,W3     own path search finished: cache fills stop
+//   f_pre   W0 -> W2        velocity part of the reward (RewardVel)
 struct K1Shared {
-    double sp[7][EPB];        // W3 -> W0: next-episode spawn of envs that end
-    double cao[3][EPB];       // W1 -> W0: obs 8, 9, 10 (fp64)
+    double acc[D2D_NSTATS][EPB];  // W3 -> W0: episode accumulators of envs that end (prefetched)
+    double cas[6][EPB];       // W1 -> W0, W2: CAStatic (d, oa, lpa, lca, rr, near)
     int scn[EPB];             // scenario index per env
-    uint32_t done[EPB];       // W3 -> W1, W2: env ends this step
-    uint32_t cvalid[EPB];     // W3 -> W1: the env's reset-cache entry is ready
+    uint32_t cause[EPB];      // W0 -> W1, W2, W3: end cause (0: the env keeps running)
+    uint32_t cvalid[EPB];     // W0 -> W1, W3: the env's reset-cache entry is ready
     uint32_t pflags[EPB];     // W2 -> W0: LA-lock bit after the path role
-    uint32_t rflags[EPB];     // W3 -> W0: flags of the reset observation
-    uint32_t f_done, f_ca, f_gs, f_pre, stop;
+    uint32_t ep[EPB];         // W0 -> W1, W3: episode counter (the state's copy changes at a reset)
+    uint32_t f_done, f_ca, f_gs, f_pre;
     union {
         double jb[6 * JB_PER_JOINT][EPB];  // W0's joint sweep: per-joint K^-1 + bias
         struct {
-            double pre[9][EPB];            // W0 -> W2: RewardPre
-            double post[4][EPB];           // W2 -> W0: RewardPost
+            double pre[3][EPB];            // W0 -> W2: RewardVel
+            double post[7][EPB];           // W2 -> W0: reward, pa, pp, dist, aa, coll, reach
             float obs[EPB * D2D_OBS_DIM];  // the workgroup's obs rows
         } p;                               // after f_gs
     } u;
@@ -216,7 +200,7 @@ __device__ __forceinline__ void flag_raise(uint32_t& f) {
     if ((threadIdx.x & 63) == 0) *(volatile LdsU32*)&f = 1u;
 }
 __device__ __forceinline__ void flag_wait(const uint32_t& f) {
-    while (!stop_seen(f)) __builtin_amdgcn_s_sleep(1);
+    while (!flag_seen(f)) __builtin_amdgcn_s_sleep(1);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
@@ -240,17 +224,10 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
         sh.f_ca = 0u;
         sh.f_gs = 0u;
         sh.f_pre = 0u;
-        sh.stop = 0u;
     }
     __syncthreads();
     STAMP(1);
     const Scn& S = scns[sh.scn[lane]];
-    // scenario of the episode an auto-reset would start (curriculum pool: a fresh draw)
-    const int nscn = (a.cfg.scn_pool && a.n_scn > 1 && valid)
-                         ? pool_pick(a.seed, (uint32_t)a.cfg.env_id_base + (uint32_t)i,
-                                     (uint32_t)fld(a.ist, D2D_I_EPISODE, n, i), a.n_scn)
-                         : sh.scn[lane];
-    const Scn& SN = scns[nscn];
     float* const trow = a.tobs ? a.tobs + (size_t)i * D2D_OBS_DIM : nullptr;
     float* const orow = &sh.u.p.obs[lane * D2D_OBS_DIM];
 
@@ -259,16 +236,16 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
     double path_err = 0.0, tot_rew = 0.0;
     int t = 0, cause = 0;
     uint32_t flags = 0;
-    RewardPre RP{};
+    RewardVel RV{};
     double dclose = 0.0;
     bool done = false;
     if (wave == 0) {
         // ---------------------------------------------------------------- physics
         D2D_SETPRIO(D2D_PRIO_W0);
         double ov[19];
+        Body B[3];
+        double j[12], cs[3], sn[3], fx = 0.0, fy = 0.0, tq = 0.0;
         if (valid && !(D2D_ABL & 1)) {
-            Body B[3];
-            double j[12];
 #pragma unroll
             for (int b = 0; b < 3; ++b) {
                 B[b].px = fld(a.st, 6 * b + 0, n, i);
@@ -289,15 +266,25 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
             const float fs = (float)a.cfg.force_scale;
             const float lf = __fmul_rn(__fadd_rn(act.x / 2.0f, 0.5f), fs);
             const float rf = __fmul_rn(__fadd_rn(act.y / 2.0f, 0.5f), fs);
-            double cs[3], sn[3], fx, fy, tq;
             if (phys_positions(S, B, (double)lf, (double)rf, cs, sn, fx, fy, tq)) flags |= D2D_FLAG_COLLIDED;
             t += 1;
             cause = end_cause(a.cfg, S, B[0], (flags & D2D_FLAG_COLLIDED) != 0, t);
+            done = cause != 0;
+            // which envs end (for W1, W2, W3) and whether their reset observation is cached
+            const int32_t ep = fld(a.ist, D2D_I_EPISODE, n, i);
+            const bool cv = done && auto_reset && ((D2D_ABL & 16) != 0 || a.rc_tag[i] == ep);
+            sh.ep[lane] = (uint32_t)ep;
+            sh.cause[lane] = (uint32_t)cause;
+            sh.cvalid[lane] = cv ? 1u : 0u;
+        }
+        flag_raise(sh.f_done);
+        if (valid && !(D2D_ABL & 1)) {
             const Arms A = make_arms(cs, sn);
             const double pos[6] = {B[0].px, B[0].py, B[1].px, B[1].py, B[2].px, B[2].py};
             double vel[9] = {B[0].vx, B[0].vy, B[0].w, B[1].vx, B[1].vy, B[1].w, B[2].vx, B[2].vy, B[2].w};
             phys_velocities<true>(A, pos, a.damping_dt, fx, fy, tq, vel, j, &sh.u.jb[0][lane], EPB);
-            // envs that end are overwritten with their spawn state in the epilogue
+            // envs that auto-reset get their spawn state from W3 instead
+            if (!(done && auto_reset)) {
 #pragma unroll
             for (int b = 0; b < 3; ++b) {
                 fld(a.st, 6 * b + 0, n, i) = B[b].px;
@@ -309,8 +296,8 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
             }
 #pragma unroll
             for (int k = 0; k < 12; ++k) fld(a.st, D2D_S_J + k, n, i) = j[k];
+            }
             F0 = Body{B[0].px, B[0].py, B[0].a, vel[0], vel[1], vel[2]};
-            done = cause != 0;
         }
         flag_raise(sh.f_gs);
         STAMP(4);
@@ -332,25 +319,22 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
                 trow[18] = (float)ov[18];
             }
         }
-        // frame / velocity / CA part of the reward, for W2
+        // velocity part of the reward (speed, velocity angle, CA total), for W2
         flag_wait(sh.f_ca);
         STAMP(5);
         if (valid) {
-            ov[8] = sh.cao[0][lane];
-            ov[9] = sh.cao[1][lane];
-            ov[10] = sh.cao[2][lane];
-            const CAPart P = reward_ca_part(a.cfg, S, ov);
-            RP = reward_pre(a.cfg, F0, P, cause);
-            sh.u.p.pre[0][lane] = RP.aa;
-            sh.u.p.pre[1][lane] = RP.lpa;
-            sh.u.p.pre[2][lane] = RP.coll;
-            sh.u.p.pre[3][lane] = RP.cal;
-            sh.u.p.pre[4][lane] = RP.reach;
-            sh.u.p.pre[5][lane] = RP.sv;
-            sh.u.p.pre[6][lane] = RP.vel_ang;
-            sh.u.p.pre[7][lane] = RP.pxd;
-            sh.u.p.pre[8][lane] = RP.pyd;
-            dclose = P.dclose;
+            CAStatic C;
+            C.d = sh.cas[0][lane];
+            C.oa = sh.cas[1][lane];
+            C.lpa = sh.cas[2][lane];
+            C.lca = sh.cas[3][lane];
+            C.rr = sh.cas[4][lane];
+            C.near = sh.cas[5][lane];
+            RV = reward_vel(a.cfg, ov, C);
+            sh.u.p.pre[0][lane] = RV.sv;
+            sh.u.p.pre[1][lane] = RV.vel_ang;
+            sh.u.p.pre[2][lane] = RV.cal;
+            dclose = C.d;
         }
         flag_raise(sh.f_pre);
     } else if (wave == 1) {
@@ -360,32 +344,41 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
         bool need = false;
         if (valid && !(D2D_ABL & 2)) {
             Body F = load_frame(a, i);
-            done = step_cause(a, S, i, F) != 0;
-            need = done && auto_reset;
+            advance_position(F);
             double so[19];
             sensor_pos(a.cfg, S, F.px, F.py, F.a, so);
-            sh.cao[0][lane] = so[8];
-            sh.cao[1][lane] = so[9];
-            sh.cao[2][lane] = so[10];
-            if (done && trow) {
-#pragma unroll
-                for (int k = 3; k < 17; ++k) trow[k] = (float)so[k];
-            }
+            const CAStatic C = ca_static(a.cfg, S, so);
+            sh.cas[0][lane] = C.d;
+            sh.cas[1][lane] = C.oa;
+            sh.cas[2][lane] = C.lpa;
+            sh.cas[3][lane] = C.lca;
+            sh.cas[4][lane] = C.rr;
+            sh.cas[5][lane] = C.near;
 #pragma unroll
             for (int k = 0; k < 19; ++k) row[k] = (float)so[k];
         }
         flag_raise(sh.f_ca);
-        // envs that end: the spawn-state sensor part, from the cache when its entry is ready
+        // envs that end (W0): terminal rows, and the spawn-state sensor part (cached when ready)
+        flag_wait(sh.f_done);
+        if (valid) {
+            done = sh.cause[lane] != 0u;
+            need = done && auto_reset;
+            if (done && trow) {
+#pragma unroll
+                for (int k = 3; k < 17; ++k) trow[k] = row[k];
+            }
+        }
         if (__ballot(need) != 0ull) {
-            flag_wait(sh.f_done);
             if (need) {
                 if (sh.cvalid[lane] != 0u) {
                     const float* c = a.rc_obs + (size_t)i * D2D_OBS_DIM;
 #pragma unroll
                     for (int k = 0; k < 19; ++k) row[k] = c[k];
                 } else {
+                    const uint32_t ep = sh.ep[lane];
+                    const Scn& SN = scns[next_scenario(a, i, ep)];
                     double sp[7], so[19];
-                    spawn_state(a, SN, i, sp);
+                    spawn_state(a, SN, i, ep, sp);
                     sensor_obs(a.cfg, SN, Body{sp[0], sp[1], sp[2], 0.0, 0.0, 0.0}, so);
 #pragma unroll
                     for (int k = 0; k < 19; ++k) row[k] = (float)so[k];
@@ -410,19 +403,31 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
         // the critical path, so it wins issue arbitration on its SIMD
         D2D_SETPRIO(D2D_PRIO_W2);
         double po[8];
+        Body F{};
         if (valid && !(D2D_ABL & 4)) {
-            Body F = load_frame(a, i);
+            F = load_frame(a, i);
             advance_position(F);
             uint32_t f = (uint32_t)fld(a.ist, D2D_I_FLAGS, n, i);
             path_obs(a.cfg, S, F.px, F.py, F.a, f, po);
             sh.pflags[lane] = f & D2D_FLAG_LA_LOCK;
         }
         STAMP(4);
-        if (!D2D_STOP_AFTER_PRE) stop_raise(sh.stop);
+        // the reward terms that do not need the joint sweep, while the physics wave finishes
         flag_wait(sh.f_done);
+        flag_wait(sh.f_ca);
+        RewardPos RP{};
+        RewardPath RQ{};
+        bool d = false;
+        if (valid) {
+            const int cause = (int)sh.cause[lane];
+            d = cause != 0;
+            CAStatic C;
+            C.lpa = sh.cas[2][lane];
+            RP = reward_pos(a.cfg, F, cause);
+            RQ = reward_path(a.cfg, RP, C, po);
+        }
         flag_wait(sh.f_gs);
         if (valid) {
-            const bool d = sh.done[lane] != 0u;
             if (!(d && auto_reset)) {
 #pragma unroll
                 for (int k = 0; k < 8; ++k) orow[19 + k] = (float)po[k];
@@ -433,53 +438,62 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
             }
         }
         flag_wait(sh.f_pre);
-        if (D2D_STOP_AFTER_PRE) stop_raise(sh.stop);
         STAMP(5);
         if (valid) {
-            RewardPre R;
-            R.aa = sh.u.p.pre[0][lane];
-            R.lpa = sh.u.p.pre[1][lane];
-            R.coll = sh.u.p.pre[2][lane];
-            R.cal = sh.u.p.pre[3][lane];
-            R.reach = sh.u.p.pre[4][lane];
-            R.sv = sh.u.p.pre[5][lane];
-            R.vel_ang = sh.u.p.pre[6][lane];
-            R.pxd = sh.u.p.pre[7][lane];
-            R.pyd = sh.u.p.pre[8][lane];
-            const RewardPost Q = reward_post(a.cfg, R, po);
+            RewardVel V;
+            V.sv = sh.u.p.pre[0][lane];
+            V.vel_ang = sh.u.p.pre[1][lane];
+            V.cal = sh.u.p.pre[2][lane];
+            const RewardSum Q = reward_sum(a.cfg, RP, V, RQ);
             sh.u.p.post[0][lane] = Q.reward;
-            sh.u.p.post[1][lane] = Q.pa;
+            sh.u.p.post[1][lane] = RQ.pa;
             sh.u.p.post[2][lane] = Q.pp;
-            sh.u.p.post[3][lane] = Q.dist;
+            sh.u.p.post[3][lane] = RQ.dist;
+            sh.u.p.post[4][lane] = RP.aa;
+            sh.u.p.post[5][lane] = RP.coll;
+            sh.u.p.post[6][lane] = RP.reach;
         }
     } else {
         // ---------------------------------------------------------------- auto-reset observation
         D2D_SETPRIO(D2D_PRIO_W3);
         double po[8];
-        bool cv = false;
-        if (valid && !(D2D_ABL & 8)) {
-            Body F = load_frame(a, i);
-            done = step_cause(a, S, i, F) != 0;
-            if (done && auto_reset) cv = (D2D_ABL & 16) != 0 || a.rc_tag[i] == fld(a.ist, D2D_I_EPISODE, n, i);
-            sh.done[lane] = done ? 1u : 0u;
-            sh.cvalid[lane] = cv ? 1u : 0u;
-        }
-        flag_raise(sh.f_done);
-        if (valid && done && auto_reset) {
-            double sp[7];
-            spawn_state(a, SN, i, sp);
+        flag_wait(sh.f_done);
+        const bool cv = valid && sh.cvalid[lane] != 0u;
+        if (valid) done = sh.cause[lane] != 0u;
+        if (valid && done) {
+            // finished-episode accumulators, read now so the epilogue does not wait on them
 #pragma unroll
-            for (int k = 0; k < 7; ++k) sh.sp[k][lane] = sp[k];
+            for (int k = 0; k < D2D_NSTATS; ++k) sh.acc[k][lane] = fld(a.acc, k, n, i);
+        }
+        if (valid && done && auto_reset && !(D2D_ABL & 8)) {
+            // the next episode: spawn state, reset observation (cached or computed), new state
+            const uint32_t ep = sh.ep[lane];
+            const int nscn = next_scenario(a, i, ep);
+            const Scn& SN = scns[nscn];
+            double sp[7];
+            spawn_state(a, SN, i, ep, sp);
+            uint32_t rfl = 0;
             if (cv) {
                 const float* c = a.rc_obs + (size_t)i * D2D_OBS_DIM + 19;
 #pragma unroll
                 for (int k = 0; k < 8; ++k) po[k] = (double)c[k];
-                sh.rflags[lane] = (uint32_t)a.rc_rfl[i];
+                rfl = (uint32_t)a.rc_rfl[i];
             } else {
-                uint32_t f = 0;
-                path_obs(a.cfg, SN, sp[0], sp[1], sp[2], f, po);
-                sh.rflags[lane] = f;
+                path_obs(a.cfg, SN, sp[0], sp[1], sp[2], rfl, po);
             }
+            const double th = sp[2];
+            const double bodies[18] = {sp[0], sp[1], th, 0.0, 0.0, 0.0, sp[3], sp[4], th, 0.0, 0.0, 0.0,
+                                       sp[5], sp[6], th, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int f = 0; f < 18; ++f) fld(a.st, f, n, i) = bodies[f];
+#pragma unroll
+            for (int k = 0; k < 12; ++k) fld(a.st, D2D_S_J + k, n, i) = 0.0;
+            fld(a.st, D2D_S_PATH_ERR, n, i) = 0.0;
+            fld(a.st, D2D_S_TOT_REW, n, i) = 0.0;
+            fld(a.ist, D2D_I_T, n, i) = 0;
+            fld(a.ist, D2D_I_FLAGS, n, i) = (int32_t)rfl;
+            fld(a.ist, D2D_I_EPISODE, n, i) = (int32_t)(ep + 1u);
+            if (a.cfg.scn_pool && a.env_scn) a.env_scn[i] = nscn;
         }
         STAMP(4);
         flag_wait(sh.f_gs);
@@ -517,12 +531,12 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
         a.trunc[i] = (uint8_t)trunc;
         if (a.info) {
             float* r = a.info + (size_t)i * D2D_INFO_DIM;
-            r[D2D_INFO_CA] = (float)RP.cal;
+            r[D2D_INFO_CA] = (float)RV.cal;
             r[D2D_INFO_PA] = (float)sh.u.p.post[1][lane];
             r[D2D_INFO_PP] = (float)sh.u.p.post[2][lane];
-            r[D2D_INFO_COLL] = (float)RP.coll;
-            r[D2D_INFO_REACH] = (float)RP.reach;
-            r[D2D_INFO_AA] = (float)RP.aa;
+            r[D2D_INFO_COLL] = (float)sh.u.p.post[5][lane];
+            r[D2D_INFO_REACH] = (float)sh.u.p.post[6][lane];
+            r[D2D_INFO_AA] = (float)sh.u.p.post[4][lane];
             r[D2D_INFO_DCLOSE] = (float)dclose;
             r[D2D_INFO_STEPS] = (float)t;
             r[D2D_INFO_CAUSE] = (float)cause;
@@ -534,29 +548,16 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
             // finished-episode accumulators (info counters of drone_2d_env.py:593-613)
             const bool c1 = cause & D2D_END_COLLISION, c2 = cause & D2D_END_REACH;
             const bool c4 = cause & D2D_END_TIMEUP, c5 = cause & D2D_END_AA;
-            fld(a.acc, D2D_ST_RETURN, n, i) += tot_rew;
-            fld(a.acc, D2D_ST_EPISODES, n, i) += 1.0;
-            fld(a.acc, D2D_ST_SUCCESS, n, i) += c2 ? 1.0 : 0.0;
-            fld(a.acc, D2D_ST_FAIL, n, i) += (c1 || c4 || c5) ? 1.0 : 0.0;
-            fld(a.acc, D2D_ST_COLLISION, n, i) += (c1 && !c2 && !c4 && !c5) ? 1.0 : 0.0;
-            fld(a.acc, D2D_ST_APE, n, i) += ape;
-            fld(a.acc, D2D_ST_LEN, n, i) += (double)t;
+            fld(a.acc, D2D_ST_RETURN, n, i) = sh.acc[D2D_ST_RETURN][lane] + tot_rew;
+            fld(a.acc, D2D_ST_EPISODES, n, i) = sh.acc[D2D_ST_EPISODES][lane] + 1.0;
+            fld(a.acc, D2D_ST_SUCCESS, n, i) = sh.acc[D2D_ST_SUCCESS][lane] + (c2 ? 1.0 : 0.0);
+            fld(a.acc, D2D_ST_FAIL, n, i) = sh.acc[D2D_ST_FAIL][lane] + ((c1 || c4 || c5) ? 1.0 : 0.0);
+            fld(a.acc, D2D_ST_COLLISION, n, i) =
+                sh.acc[D2D_ST_COLLISION][lane] + ((c1 && !c2 && !c4 && !c5) ? 1.0 : 0.0);
+            fld(a.acc, D2D_ST_APE, n, i) = sh.acc[D2D_ST_APE][lane] + ape;
+            fld(a.acc, D2D_ST_LEN, n, i) = sh.acc[D2D_ST_LEN][lane] + (double)t;
         }
-        if (done && auto_reset) {
-            const double x = sh.sp[0][lane], y = sh.sp[1][lane], th = sh.sp[2][lane];
-            const double bodies[18] = {x, y, th, 0.0, 0.0, 0.0, sh.sp[3][lane], sh.sp[4][lane], th, 0.0, 0.0, 0.0,
-                                       sh.sp[5][lane], sh.sp[6][lane], th, 0.0, 0.0, 0.0};
-#pragma unroll
-            for (int f = 0; f < 18; ++f) fld(a.st, f, n, i) = bodies[f];
-#pragma unroll
-            for (int k = 0; k < 12; ++k) fld(a.st, D2D_S_J + k, n, i) = 0.0;
-            fld(a.st, D2D_S_PATH_ERR, n, i) = 0.0;
-            fld(a.st, D2D_S_TOT_REW, n, i) = 0.0;
-            fld(a.ist, D2D_I_T, n, i) = 0;
-            fld(a.ist, D2D_I_FLAGS, n, i) = (int32_t)sh.rflags[lane];
-            fld(a.ist, D2D_I_EPISODE, n, i) += 1;
-            if (a.cfg.scn_pool && a.env_scn) a.env_scn[i] = nscn;
-        } else {
+        if (!(done && auto_reset)) {
             fld(a.st, D2D_S_PATH_ERR, n, i) = path_err;
             fld(a.st, D2D_S_TOT_REW, n, i) = tot_rew;
             fld(a.ist, D2D_I_T, n, i) = t;
@@ -584,7 +585,7 @@ __global__ __launch_bounds__(BLOCK) void d2d_reset_kernel(StepArgs a) {
     }
     const Scn& s = scns[si];
     double sp[7];
-    spawn_state(a, s, i, sp);
+    spawn_state(a, s, i, (uint32_t)fld(a.ist, D2D_I_EPISODE, n, i), sp);
     const double th = sp[2];
     const double bodies[18] = {sp[0], sp[1], th, 0.0, 0.0, 0.0, sp[3], sp[4], th, 0.0, 0.0, 0.0,
                                sp[5], sp[6], th, 0.0, 0.0, 0.0};
@@ -621,7 +622,7 @@ __global__ __launch_bounds__(BLOCK) void d2d_fill_kernel(StepArgs a) {
     if (a.rc_tag[i] == ep) return;
     const Scn& S = scns[next_scenario(a, i, (uint32_t)ep)];
     double sp[7], so[19], o[8];
-    spawn_state(a, S, i, sp);
+    spawn_state(a, S, i, (uint32_t)ep, sp);
     uint32_t f = 0;
     sensor_obs(a.cfg, S, Body{sp[0], sp[1], sp[2], 0.0, 0.0, 0.0}, so);
     path_obs(a.cfg, S, sp[0], sp[1], sp[2], f, o);
@@ -652,7 +653,8 @@ __global__ __launch_bounds__(256) void d2d_selftest_kernel(int which, long long 
         philox((uint32_t)k, (uint32_t)(k >> 32), 0x5E1F7E58u, (uint32_t)which, k0, k1, p);
         double got, want;
         if (which == D2D_SELFTEST_SQRT) {
-            const double x = ((p[0] & 63u) == 0u) ? 0.0 : st_rand(o[0], o[1], 1023 - 767, 2046, 0u);
+            const uint32_t sel = p[0] & 63u;  // 1/64 zeros, 1/64 +inf, the rest in [2^-767, max]
+            const double x = (sel == 0u) ? 0.0 : ((sel == 1u) ? __builtin_inf() : st_rand(o[0], o[1], 1023 - 767, 2046, 0u));
             got = sqrt_nz(x);
             want = sqrt(x);
         } else {

@@ -10,7 +10,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
 B="python3 $R/bench.py --no-cpu-baseline"
-KR="--kernel-include-regex d2d_step_kernel"
+KR="--kernel-include-regex d2d_(step|fill)_kernel"
 
 step() {  # step <name> <timeout> <cmd...>: stop on any failure
   local name=$1 lim=$2; shift 2

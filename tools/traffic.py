@@ -1,10 +1,13 @@
 #!/usr/bin/env python3
-"""Per-launch HBM-side traffic of the step kernel from rocprofv3 PMC passes (tools/profile.sh).
+"""Per-step HBM-side traffic of the step path from rocprofv3 PMC passes (tools/profile.sh).
 
     python tools/traffic.py gpurun_out/prof_TAG [--out profiles/traffic_corridor_65536.json]
 
-FETCH_SIZE / WRITE_SIZE are KB per dispatch.  MI355X_MICROARCH.md (HBM, gfx950): FETCH_SIZE reports
-half of the bytes of wide coalesced reads -> doubled; WRITE_SIZE is exact for streaming stores.
+One env step is one d2d_step_kernel launch plus its share of the periodic d2d_fill_kernel: the
+bytes of both kernels over the second half of the profiled dispatches, divided by the number of
+step-kernel launches there.  FETCH_SIZE / WRITE_SIZE are KB per dispatch.  MI355X_MICROARCH.md
+(HBM, gfx950): FETCH_SIZE reports half of the bytes of wide coalesced reads -> doubled; WRITE_SIZE
+is exact for streaming stores.
 """
 from __future__ import annotations
 
@@ -14,16 +17,25 @@ import glob
 import json
 import os
 
-import numpy as np
 
 
-def counter(d, name, kernel="d2d_step_kernel"):
-    vals = []
+def counter(d, name):
+    """[(dispatch id, kernel, value)] of the d2d kernels, in dispatch order"""
+    rows = []
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for row in csv.DictReader(open(f)):
-            if row["Counter_Name"] == name and kernel in row["Kernel_Name"]:
-                vals.append(float(row["Counter_Value"]))
-    return np.array(vals)
+            if row["Counter_Name"] == name and row["Kernel_Name"].startswith("d2d_"):
+                rows.append((int(row["Dispatch_Id"]), row["Kernel_Name"], float(row["Counter_Value"])))
+    return sorted(rows)
+
+
+def per_step(rows):
+    """bytes per step over the second half of the launches: (step + fill kernels) / step launches"""
+    rows = rows[len(rows) // 2:]
+    steps = sum(1 for _, k, _ in rows if k.startswith("d2d_step_kernel"))
+    step_b = sum(v for _, k, v in rows if k.startswith("d2d_step_kernel"))
+    fill_b = sum(v for _, k, v in rows if k.startswith("d2d_fill_kernel"))
+    return (step_b + fill_b) * 1024.0 / max(steps, 1), step_b * 1024.0 / max(steps, 1), steps
 
 
 def main():
@@ -34,14 +46,16 @@ def main():
     a = ap.parse_args()
     fetch = counter(os.path.join(a.prof_dir, "pmc_fetch"), "FETCH_SIZE")
     write = counter(os.path.join(a.prof_dir, "pmc_write"), "WRITE_SIZE")
-    assert len(fetch) and len(write), "no FETCH_SIZE / WRITE_SIZE rows for d2d_step_kernel"
-    # skip the first launches (episodes have not ended yet: no auto-reset traffic)
-    f = np.median(fetch[len(fetch) // 2:]) * 1024.0 * 2.0
-    w = np.median(write[len(write) // 2:]) * 1024.0
-    res = {"kernel": "d2d_step_kernel", "envs": a.envs, "bytes_per_launch": f + w,
+    assert len(fetch) and len(write), "no FETCH_SIZE / WRITE_SIZE rows for the d2d kernels"
+    # second half only: by then episodes end and the fill kernel runs (auto-reset traffic)
+    f, f_step, nf = per_step(fetch)
+    w, w_step, nw = per_step(write)
+    f, f_step = 2.0 * f, 2.0 * f_step
+    res = {"kernel": "d2d_step_kernel + d2d_fill_kernel share", "envs": a.envs, "bytes_per_launch": f + w,
            "fetch_bytes_corrected": f, "write_bytes": w, "bytes_per_env_step": (f + w) / a.envs,
-           "launches": [int(len(fetch)), int(len(write))],
-           "note": "median over the second half of the profiled launches; FETCH_SIZE x2 (gfx950)"}
+           "step_kernel_only_bytes": f_step + w_step, "step_launches": [nf, nw],
+           "note": "per step = (step + fill kernel bytes) / step launches over the second half of the "
+                   "profiled launches; FETCH_SIZE x2 (gfx950)"}
     print(json.dumps(res, indent=1))
     if a.out:
         json.dump(res, open(a.out, "w"), indent=1)
