@@ -460,6 +460,30 @@ __device__ __forceinline__ void arm(const Arms& A, int k, double& r1x, double& r
     r2y = (k < 3) ? -s : s;
 }
 
+// the same arms re-read from an LDS copy (JBUF mode: keeps the 14 values out of registers across the
+// 10-sweep loop); field order of Arms: m7c[2], m7s[2], f47c, f47s, f40c, f40s, f33c, f33s
+constexpr int ARMS_N = 14;
+__device__ __forceinline__ void arms_store(const Arms& A, double* ab, int stride) {
+    const double v[ARMS_N] = {A.m7c[0], A.m7c[1], A.m7s[0], A.m7s[1], A.f47c, A.f47s,
+                              A.f40c, A.f40s, A.f33c, A.f33s, 0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < 10; ++q) ab[q * stride] = v[q];
+}
+__device__ __forceinline__ void arm_lds(const double* ab, int stride, int k, double& r1x, double& r1y, double& r2x,
+                                        double& r2y) {
+    using LdsD = __attribute__((address_space(3))) double;
+    const volatile LdsD* v = (const volatile LdsD*)ab;
+    const int m = k < 3 ? 0 : 1;
+    const int q = k % 3;
+    const double mc = (q == 1) ? 0.0 : v[(0 + m) * stride], ms = (q == 1) ? 0.0 : v[(2 + m) * stride];
+    r1x = (q == 0) ? -mc : ((q == 1) ? 0.0 : mc);
+    r1y = (q == 0) ? -ms : ((q == 1) ? 0.0 : ms);
+    const int f = (k == 0 || k == 5) ? 4 : ((k == 1 || k == 4) ? 6 : 8);
+    const double c = v[f * stride], sn = v[(f + 1) * stride];
+    r2x = (k < 3) ? -c : c;
+    r2y = (k < 3) ? -sn : sn;
+}
+
 __device__ __forceinline__ void advance_position(Body& b) {
     b.px = b.px + (b.vx + 0.0) * DT;
     b.py = b.py + (b.vy + 0.0) * DT;
@@ -532,7 +556,8 @@ constexpr int JB_PER_JOINT = 5;  // K^-1 (a, b = c, d) + bias (x, y)
 template <bool JBUF>
 __device__ __forceinline__ void phys_velocities(const Arms& A, const double pos[6], double damping_dt, double fx,
                                                 double fy, double tq, double vel[9], double j[12], double* jb,
-                                                int stride) {
+                                                int stride, double* ab = nullptr) {
+    if (JBUF) arms_store(A, ab, stride);
     const double bias_coef = -(1.0 - 0.0) / DT;  // error_bias = 0 -> bias_coef(0, dt) = 1 - 0^dt = 1
     double kk[JBUF ? 1 : 6][5];
     // preStep
@@ -593,7 +618,8 @@ __device__ __forceinline__ void phys_velocities(const Arms& A, const double pos[
         for (int k = 0; k < 6; ++k) {
             const int m = k < 3 ? 1 : 2;
             double r1x, r1y, r2x, r2y;
-            arm(A, k, r1x, r1y, r2x, r2y);
+            if (JBUF) arm_lds(ab, stride, k, r1x, r1y, r2x, r2y);
+            else arm(A, k, r1x, r1y, r2x, r2y);
             double ka, kb, kd, bx, by;
             if (JBUF) {
                 // an explicit LDS (address_space 3) pointer: generic volatile loads would become flat

@@ -185,8 +185,12 @@ struct K1Shared {
     uint32_t pflags[EPB];     // W2 -> W0: LA-lock bit after the path role
     uint32_t ep[EPB];         // W0 -> W1, W3: episode counter (the state's copy changes at a reset)
     uint32_t f_done, f_ca, f_gs, f_pre;
+    double pe[2][EPB];        // W3 -> W0: path_err, total_reward (prefetched for the epilogue)
     union {
-        double jb[6 * JB_PER_JOINT][EPB];  // W0's joint sweep: per-joint K^-1 + bias
+        struct {
+            double jb[6 * JB_PER_JOINT][EPB];  // W0's joint sweep: per-joint K^-1 + bias
+            double arms[ARMS_N][EPB];          // ... and the rotated anchor arms
+        } g;
         struct {
             double pre[3][EPB];            // W0 -> W2: RewardVel
             double post[7][EPB];           // W2 -> W0: reward, pa, pp, dist, aa, coll, reach
@@ -257,8 +261,6 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
             }
 #pragma unroll
             for (int k = 0; k < 12; ++k) j[k] = fld(a.st, D2D_S_J + k, n, i);
-            path_err = fld(a.st, D2D_S_PATH_ERR, n, i);
-            tot_rew = fld(a.st, D2D_S_TOT_REW, n, i);
             t = fld(a.ist, D2D_I_T, n, i);
             flags = (uint32_t)fld(a.ist, D2D_I_FLAGS, n, i);
             // thrust in float32 exactly as SB3's float32 action hits drone_2d_env.py:400-401
@@ -276,20 +278,27 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
             sh.ep[lane] = (uint32_t)ep;
             sh.cause[lane] = (uint32_t)cause;
             sh.cvalid[lane] = cv ? 1u : 0u;
+            // positions and angles are final now (the sweep changes velocities only); envs that
+            // auto-reset get their spawn state from W3 instead
+            if (!(done && auto_reset)) {
+#pragma unroll
+                for (int b = 0; b < 3; ++b) {
+                    fld(a.st, 6 * b + 0, n, i) = B[b].px;
+                    fld(a.st, 6 * b + 1, n, i) = B[b].py;
+                    fld(a.st, 6 * b + 2, n, i) = B[b].a;
+                }
+            }
         }
         flag_raise(sh.f_done);
         if (valid && !(D2D_ABL & 1)) {
             const Arms A = make_arms(cs, sn);
             const double pos[6] = {B[0].px, B[0].py, B[1].px, B[1].py, B[2].px, B[2].py};
             double vel[9] = {B[0].vx, B[0].vy, B[0].w, B[1].vx, B[1].vy, B[1].w, B[2].vx, B[2].vy, B[2].w};
-            phys_velocities<true>(A, pos, a.damping_dt, fx, fy, tq, vel, j, &sh.u.jb[0][lane], EPB);
-            // envs that auto-reset get their spawn state from W3 instead
+            phys_velocities<true>(A, pos, a.damping_dt, fx, fy, tq, vel, j, &sh.u.g.jb[0][lane], EPB,
+                                  &sh.u.g.arms[0][lane]);
             if (!(done && auto_reset)) {
 #pragma unroll
             for (int b = 0; b < 3; ++b) {
-                fld(a.st, 6 * b + 0, n, i) = B[b].px;
-                fld(a.st, 6 * b + 1, n, i) = B[b].py;
-                fld(a.st, 6 * b + 2, n, i) = B[b].a;
                 fld(a.st, 6 * b + 3, n, i) = vel[3 * b + 0];
                 fld(a.st, 6 * b + 4, n, i) = vel[3 * b + 1];
                 fld(a.st, 6 * b + 5, n, i) = vel[3 * b + 2];
@@ -457,6 +466,11 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
         // ---------------------------------------------------------------- auto-reset observation
         D2D_SETPRIO(D2D_PRIO_W3);
         double po[8];
+        if (valid) {
+            // running path error / return for W0's epilogue
+            sh.pe[0][lane] = fld(a.st, D2D_S_PATH_ERR, n, i);
+            sh.pe[1][lane] = fld(a.st, D2D_S_TOT_REW, n, i);
+        }
         flag_wait(sh.f_done);
         const bool cv = valid && sh.cvalid[lane] != 0u;
         if (valid) done = sh.cause[lane] != 0u;
@@ -516,6 +530,8 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
         for (int k = threadIdx.x; k < words; k += K1_THREADS) dst[k] = sh.u.p.obs[k];
     }
     if (wave == 0 && valid) {
+        path_err = sh.pe[0][lane];
+        tot_rew = sh.pe[1][lane];
         flags = (flags & ~D2D_FLAG_LA_LOCK) | sh.pflags[lane];
         const double reward = sh.u.p.post[0][lane];
         path_err += sh.u.p.post[3][lane];
