@@ -60,7 +60,9 @@ struct Scn {
     double cx[D2D_MAX_CIRCLES], cy[D2D_MAX_CIRCLES], cr[D2D_MAX_CIRCLES];
     double wp_last_x, wp_last_y;
     double spawn_xmin, spawn_xmax, spawn_ymin, spawn_ymax, spawn_amin, spawn_amax;
+    double pad;  // sizeof(Scn) % 16 == 0: the probe tables staged after the scenarios stay 16-B aligned
 };
+static_assert(sizeof(Scn) % 16 == 0, "Scn size");
 // Returns false if the table is outside what the record form reproduces exactly: the last-segment
 // window us[nw-2] - 0.001 must not reach back past us[nw-3] (always true for real waypoints).
 inline bool scn_build(const d2d_scn& a, Scn& s) {
@@ -406,6 +408,205 @@ __device__ __forceinline__ double closest_u(const Scn& s, double px, double py) 
     return B.xf;
 }
 
+// ------------------------------------------------------------------ Brent golden-march tables
+// Two probe sequences of fminbound do not depend on the point at all as long as its decisions are
+// "golden step, the new probe is not worse" (after the first step):
+//   kind 0 (golden-left):  step 0 worse, then every step better -> converges to u = -10
+//                          (points behind the path start; 66 % of the bench's searches)
+//   kind 1 (golden-right): every step better                 -> converges to u = L + 10
+// In that regime a, b, the probes, e, rat and tol1 are functions of the step number only; the
+// distances enter only the decisions.  So for each scenario a forced run (d2d_brtab_kernel, the
+// same device arithmetic as brent_step) records per step k: the probe's path point (X, Y) and the
+// f-independent operands of the parabolic-acceptance test, plus the whole search state before
+// the step (the snapshot).  A search then (closest_u_tab):
+//   1. evaluates the distances at the recorded probes and re-checks every decision with its own
+//      distances: `par` (the parabolic acceptance test, same operations as brent_step) must be
+//      false and `fu <= fx` true -- ~35 instructions per step, no path evaluation, no selects;
+//   2. at the first step d whose decision differs (if any), restores the snapshot before step d
+//      (its fx / fnfc / ffulc are the distances at recorded probes) and continues with brent_step.
+// Both stages perform exactly the operations brent_step performs on the same operands, so the
+// result is bit-identical to closest_u for every point (tests/test_gpu_parity.py grid test).
+constexpr int BT_K = 48;    // recorded steps per kind (longer marches continue in brent_step)
+constexpr int BT_HOT = BT_K + 4;  // probe entries per kind: 0..BT_K, plus zero entries the 3-step
+                                  // unrolled check may read past a table's end
+struct BtIt {             // probe j (0: the initial point; k + 1: the probe of step k) + step k's operands
+    double X, Y;          // path(probe)
+    double dxn, dxf;      // xf - nfc, xf - fulc before step k
+    double e;             // e before step k if |e| > tol1 (parabolic step tried), else 0 (never accepted)
+    double am, bm;        // a - xf, b - xf before step k
+    double pad;
+};
+struct BtSnap {           // search state before step k (the f values are distances at probes j_*)
+    double a, b, fulc, nfc, xf, rat, e, ka, kxf;
+    int32_t num, ia, ib, ixf;
+    int32_t j_fulc, j_nfc, j_xf, pad;
+};
+struct BtHot {
+    BtIt it[2][BT_HOT];   // [kind][probe]
+};
+static_assert(sizeof(BtIt) == 64, "BtIt size");
+struct BrTab {
+    BtHot hot;            // first member: staged into LDS as one block
+    BtSnap snap[2][BT_K + 1];
+    int32_t len[2];       // recorded steps of each kind (the march's length, at most BT_K)
+    int32_t pad[2];
+};
+
+// forced run of kind `kind` (one thread per scenario and kind; table generation, not on the step path)
+__device__ __forceinline__ void brtab_build(const Scn& s, int kind, BrTab& T) {
+    const PathK K = path_k(s);
+    Brent B;
+    B.a = 0.0 - 10.0;
+    B.b = K.L + 10.0;
+    B.fulc = B.a + BR_GOLDEN * (B.b - B.a);
+    B.nfc = B.fulc;
+    B.xf = B.fulc;
+    B.rat = 0.0;
+    B.e = 0.0;
+    B.ia = u_index(s, B.a);
+    B.ib = u_index(s, B.b);
+    B.ka = s.rec[REC_U1][B.ia];
+    B.ixf = u_index(s, B.xf);
+    B.num = 1;
+    B.fx = B.ffulc = B.fnfc = 0.0;
+    BtIt& h0 = T.hot.it[kind][0];
+    path_eval_n(s, K, B.xf, B.ixf, h0.X, h0.Y, B.kxf);
+    h0.dxn = h0.dxf = h0.e = h0.am = h0.bm = h0.pad = 0.0;
+    int jf = 0, jn = 0, jx = 0;  // probe indices of fulc, nfc, xf
+    int k = 0;
+    for (; k < BT_K && brent_active(B); ++k) {
+        BtSnap& S = T.snap[kind][k];
+        S = BtSnap{B.a, B.b, B.fulc, B.nfc, B.xf, B.rat, B.e, B.ka, B.kxf, B.num, B.ia, B.ib, B.ixf, jf, jn, jx, 0};
+        const double a = B.a, b = B.b, xf = B.xf, nfc = B.nfc, fulc = B.fulc;
+        const double xm = 0.5 * (a + b);
+        const double tol1 = BR_SQRT_EPS * fabs(xf) + BR_XATOL3;
+        BtIt& h = T.hot.it[kind][k + 1];
+        h.dxn = xf - nfc;
+        h.dxf = xf - fulc;
+        h.e = (fabs(B.e) > tol1) ? B.e : 0.0;
+        h.am = a - xf;
+        h.bm = b - xf;
+        h.pad = 0.0;
+        // golden step (brent_step with par == false)
+        const double e_g = (xf >= xm) ? a - xf : b - xf;
+        const double rat = BR_GOLDEN * e_g;
+        B.e = e_g;
+        B.rat = rat;
+        const double mx = fmax(fabs(rat), tol1);
+        const double x = xf + ((rat < 0.0) ? -mx : mx);
+        const int ix = u_index(s, x);
+        double kx;
+        path_eval_n(s, K, x, ix, h.X, h.Y, kx);
+        B.num += 1;
+        // forced decision: kind 0 step 0 is worse (c1 holds: nfc == xf), every other step better
+        const bool le = !(kind == 0 && k == 0);
+        const bool c1 = !le;
+        const bool ge = x >= xf;
+        const bool to_a = le == ge;
+        const double t = le ? xf : x;
+        const int ti = le ? B.ixf : ix;
+        const double tk = le ? B.kxf : kx;
+        B.a = to_a ? t : a;
+        B.b = to_a ? b : t;
+        B.ia = to_a ? ti : B.ia;
+        B.ka = to_a ? tk : B.ka;
+        B.ib = to_a ? B.ib : ti;
+        B.ixf = le ? ix : B.ixf;
+        B.kxf = le ? kx : B.kxf;
+        const int j = k + 1;
+        const double nfulc = (le | c1) ? nfc : fulc;
+        const int njf = (le | c1) ? jn : jf;
+        const double nnfc = le ? xf : (c1 ? x : nfc);
+        const int njn = le ? jx : (c1 ? j : jn);
+        B.fulc = nfulc;
+        B.nfc = nnfc;
+        B.xf = le ? x : xf;
+        jf = njf;
+        jn = njn;
+        jx = le ? j : jx;
+    }
+    T.snap[kind][k] = BtSnap{B.a, B.b, B.fulc, B.nfc, B.xf, B.rat, B.e, B.ka, B.kxf, B.num, B.ia, B.ib, B.ixf,
+                             jf, jn, jx, 0};
+    T.len[kind] = k;
+}
+
+// one recorded step re-checked with this point's distances (the operations of brent_step on the
+// same operands): returns the probe's distance; dev <- k if the decision differs.  The window
+// (ffulc, fnfc, fx) is the distances at fulc, nfc, xf before the step.
+__device__ __forceinline__ double bt_check(const BtIt& h, int k, double px, double py, double ffulc, double fnfc,
+                                           double fx, int& dev) {
+    const double fu = norm2(h.X - px, h.Y - py);
+    const double r = h.dxn * (fx - ffulc);
+    double q = h.dxf * (fx - fnfc);
+    double p = h.dxf * q - h.dxn * r;
+    q = 2.0 * (q - r);
+    p = (q > 0.0) ? -p : p;
+    q = fabs(q);
+    const bool par = (fabs(p) < fabs(0.5 * q * h.e)) & (p > q * h.am) & (p < q * h.bm);
+    const bool ok = !par & (fu <= fx);
+    dev = min(dev, ok ? BT_HOT : k);
+    return fu;
+}
+
+// get_closest_u through the golden-march tables (bit-identical to closest_u, see above).
+// `hot` is the scenario's probe table: LDS (address space 3) when LT, else global memory.
+template <bool LT>
+__device__ __forceinline__ double closest_u_tab(const Scn& s, const BrTab& T, const BtHot* hot, double px,
+                                                double py) {
+    using HL = __attribute__((address_space(3))) const double;
+    const auto H = [&](int kind, int j) -> BtIt {
+        if (!LT) return hot->it[kind][j];
+        const HL* q = (const HL*)&hot->it[kind][j];
+        return BtIt{q[0], q[1], q[2], q[3], q[4], q[5], q[6], q[7]};
+    };
+    // the initial point and step 0's probe are the same in both kinds; step 0's decision picks the kind
+    const BtIt h0 = H(0, 0), h1 = H(0, 1);
+    const double f0 = norm2(h0.X - px, h0.Y - py);
+    const double f1 = norm2(h1.X - px, h1.Y - py);
+    const int kind = (f1 <= f0) ? 1 : 0;
+    const int len = T.len[kind];
+    // distances at fulc, nfc, xf after step 0
+    double fa = f0, fb = kind ? f0 : f1, fc = kind ? f1 : f0;
+    int dev = len;  // first step whose decision differs from the table (len: none)
+    // steps 1, 2, ... three per pass (independent distance evaluations; the window rotates by name)
+    for (int k = 1; __ballot(k < dev) != 0ull; k += 3) {
+        const BtIt ha = H(kind, k + 1), hb = H(kind, k + 2), hc = H(kind, k + 3);
+        const double fd = bt_check(ha, k, px, py, fa, fb, fc, dev);
+        const double fe = bt_check(hb, k + 1, px, py, fb, fc, fd, dev);
+        const double ff = bt_check(hc, k + 2, px, py, fc, fd, fe, dev);
+        fa = fd;
+        fb = fe;
+        fc = ff;
+    }
+    dev = min(dev, len);
+    // resume brent_step from the snapshot before the first differing step (a search that followed
+    // the table restores its final state, which is inactive unless the march is longer than BT_K)
+    const BtSnap& S = T.snap[kind][dev];
+    Brent B;
+    B.a = S.a;
+    B.b = S.b;
+    B.fulc = S.fulc;
+    B.nfc = S.nfc;
+    B.xf = S.xf;
+    B.rat = S.rat;
+    B.e = S.e;
+    B.ka = S.ka;
+    B.kxf = S.kxf;
+    B.num = S.num;
+    B.ia = S.ia;
+    B.ib = S.ib;
+    B.ixf = S.ixf;
+    if (__ballot(brent_active(B)) != 0ull) {
+        const PathK K = path_k(s);
+        const BtIt pf = H(kind, S.j_fulc), pn = H(kind, S.j_nfc), px_ = H(kind, S.j_xf);
+        B.ffulc = norm2(pf.X - px, pf.Y - py);
+        B.fnfc = norm2(pn.X - px, pn.Y - py);
+        B.fx = norm2(px_.X - px, px_.Y - py);
+        while (brent_active(B)) brent_step(s, K, px, py, B);
+    }
+    return B.xf;
+}
+
 // ------------------------------------------------------------------------------ bodies / physics
 // One cpSpaceStep(1/60) of the Drone.py body/joint configuration, split in
 // two stages so that a caller can retire the positions before the Gauss-Seidel sweep:
@@ -462,10 +663,10 @@ __device__ __forceinline__ void arm(const Arms& A, int k, double& r1x, double& r
 
 // the same arms re-read from an LDS copy (JBUF mode: keeps the 14 values out of registers across the
 // 10-sweep loop); field order of Arms: m7c[2], m7s[2], f47c, f47s, f40c, f40s, f33c, f33s
-constexpr int ARMS_N = 14;
+constexpr int ARMS_N = 10;
 __device__ __forceinline__ void arms_store(const Arms& A, double* ab, int stride) {
     const double v[ARMS_N] = {A.m7c[0], A.m7c[1], A.m7s[0], A.m7s[1], A.f47c, A.f47s,
-                              A.f40c, A.f40s, A.f33c, A.f33s, 0.0, 0.0, 0.0, 0.0};
+                              A.f40c, A.f40s, A.f33c, A.f33s};
 #pragma unroll
     for (int q = 0; q < 10; ++q) ab[q * stride] = v[q];
 }
@@ -772,9 +973,14 @@ __device__ __forceinline__ void path_obs_u(const d2d_cfg& cfg, const Scn& s, dou
     sincos_d(laa, o[4], o[5]);
     sincos_d(cpa, o[6], o[7]);
 }
-__device__ __forceinline__ void path_obs(const d2d_cfg& cfg, const Scn& s, double x, double y, double al,
-                                         uint32_t& flags, double o[8]) {
-    const double u = (D2D_ABLATE & 1) ? clipd(x - 100.0, -10.0, s.us[s.n_wps - 1]) : closest_u(s, x, y);
+// T: the scenario's golden-march tables (null: plain search); hot: their probe table staged in LDS
+// (LT) or null (read from T in global memory)
+template <bool LT = false>
+__device__ __forceinline__ void path_obs(const d2d_cfg& cfg, const Scn& s, const BrTab* T, double x, double y,
+                                         double al, uint32_t& flags, double o[8], const BtHot* hot = nullptr) {
+    const double u = (D2D_ABLATE & 1) ? clipd(x - 100.0, -10.0, s.us[s.n_wps - 1])
+                     : (T ? (LT ? closest_u_tab<true>(s, *T, hot, x, y) : closest_u_tab<false>(s, *T, &T->hot, x, y))
+                          : closest_u(s, x, y));
     path_obs_u(cfg, s, x, y, al, u, flags, o);
 }
 
@@ -892,10 +1098,10 @@ __device__ __forceinline__ RewardSum reward_sum(const d2d_cfg& cfg, const Reward
 }
 
 // full single-lane observation (reset kernel)
-__device__ __forceinline__ void observe(const d2d_cfg& cfg, const Scn& s, const Body& F, uint32_t& flags,
-                                        double obs[D2D_OBS_DIM]) {
+__device__ __forceinline__ void observe(const d2d_cfg& cfg, const Scn& s, const BrTab* T, const Body& F,
+                                        uint32_t& flags, double obs[D2D_OBS_DIM]) {
     sensor_obs(cfg, s, F, obs);
-    path_obs(cfg, s, F.px, F.py, F.a, flags, obs + 19);
+    path_obs(cfg, s, T, F.px, F.py, F.a, flags, obs + 19);
 }
 
 }  // namespace d2d

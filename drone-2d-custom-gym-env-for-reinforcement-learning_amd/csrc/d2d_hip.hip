@@ -15,6 +15,10 @@
 
 using namespace d2dk;
 
+#ifndef D2D_BRTAB
+#define D2D_BRTAB 1  // 0: searches without the golden-march tables (diagnostic A/B builds only)
+#endif
+
 namespace {
 thread_local std::string g_err;
 
@@ -37,6 +41,7 @@ struct d2d_handle {
     int32_t* ist = nullptr;
     double* acc = nullptr;
     d2d::Scn* scn = nullptr;    // device table: ABI scenarios + derived fields
+    d2d::BrTab* brt = nullptr;  // golden-march tables of the scenarios (d2d_brtab_kernel)
     int32_t* env_scn = nullptr;
     uint64_t seed = 0;
     bool reset_done = false;
@@ -59,6 +64,7 @@ StepArgs make_args(const d2d_t* h) {
     a.ist = h->ist;
     a.acc = h->acc;
     a.scn = h->scn;
+    a.brt = D2D_BRTAB ? h->brt : nullptr;
     a.env_scn = h->env_scn;
     a.cfg = h->cfg;
     a.damping_dt = std::pow(h->cfg.damping, 1.0 / 60.0);
@@ -150,6 +156,7 @@ void d2d_destroy(d2d_t* h) {
     if (h->ist) (void)hipFree(h->ist);
     if (h->acc) (void)hipFree(h->acc);
     if (h->scn) (void)hipFree(h->scn);
+    if (h->brt) (void)hipFree(h->brt);
     if (h->env_scn) (void)hipFree(h->env_scn);
     if (h->rc_obs) (void)hipFree(h->rc_obs);
     if (h->rc_rfl) (void)hipFree(h->rc_rfl);
@@ -188,6 +195,10 @@ int32_t d2d_set_scenarios(d2d_t* h, const d2d_scn* scns, int32_t n_scn, const in
         (void)hipFree(h->scn);
         h->scn = nullptr;
     }
+    if (h->brt) {
+        (void)hipFree(h->brt);
+        h->brt = nullptr;
+    }
     std::vector<d2d::Scn> tab((size_t)n_scn);
     for (int k = 0; k < n_scn; ++k) {
         if (!d2d::scn_build(scns[k], tab[k]))
@@ -197,6 +208,13 @@ int32_t d2d_set_scenarios(d2d_t* h, const d2d_scn* scns, int32_t n_scn, const in
     if ((e = hipMalloc(&h->scn, bytes)) != hipSuccess) return hip_fail(e, "hipMalloc scn");
     if ((e = hipMemcpy(h->scn, tab.data(), bytes, hipMemcpyHostToDevice)) != hipSuccess)
         return hip_fail(e, "hipMemcpy scn");
+    // golden-march tables: forced searches on the device (same arithmetic as the step kernels)
+    const size_t tbytes = sizeof(d2d::BrTab) * (size_t)n_scn;
+    if ((e = hipMalloc(&h->brt, tbytes)) != hipSuccess) return hip_fail(e, "hipMalloc brt");
+    if ((e = hipMemset(h->brt, 0, tbytes)) != hipSuccess) return hip_fail(e, "hipMemset brt");
+    hipLaunchKernelGGL(d2d_brtab_kernel, dim3((2 * n_scn + 63) / 64), dim3(64), 0, 0, h->scn, n_scn, h->brt);
+    if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "d2d_brtab_kernel launch");
+    if ((e = hipDeviceSynchronize()) != hipSuccess) return hip_fail(e, "d2d_brtab_kernel");
     if (env_scn_host) {
         if ((e = hipMemcpy(h->env_scn, env_scn_host, sizeof(int32_t) * (size_t)h->n, hipMemcpyHostToDevice)) !=
             hipSuccess)
@@ -249,10 +267,13 @@ int32_t d2d_step(d2d_t* h, const float* act_dev, float* obs_dev, float* rew_dev,
     a.info = info_dev;
     a.tobs = term_obs_dev;
     const dim3 grid((h->n + EPB - 1) / EPB);
-    if (sizeof(d2d::Scn) * (size_t)h->n_scn + sizeof(K1Shared) <= K1_LDS_BUDGET)
-        hipLaunchKernelGGL(d2d_step_kernel<true>, grid, dim3(K1_THREADS), sizeof(d2d::Scn) * h->n_scn, (hipStream_t)stream, a);
+    const size_t lds_scn = sizeof(d2d::Scn) * (size_t)h->n_scn, lds_hot = sizeof(d2d::BtHot) * (size_t)h->n_scn;
+    if (a.brt && lds_scn + lds_hot + sizeof(K1Shared) <= K1_LDS_BUDGET)
+        hipLaunchKernelGGL((d2d_step_kernel<true, true>), grid, dim3(K1_THREADS), lds_scn + lds_hot, (hipStream_t)stream, a);
+    else if (lds_scn + sizeof(K1Shared) <= K1_LDS_BUDGET)
+        hipLaunchKernelGGL((d2d_step_kernel<true, false>), grid, dim3(K1_THREADS), lds_scn, (hipStream_t)stream, a);
     else
-        hipLaunchKernelGGL(d2d_step_kernel<false>, grid, dim3(K1_THREADS), 0, (hipStream_t)stream, a);
+        hipLaunchKernelGGL((d2d_step_kernel<false, false>), grid, dim3(K1_THREADS), 0, (hipStream_t)stream, a);
     e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "d2d_step launch");
     if (D2D_FILL_PERIOD > 0 && h->cfg.auto_reset && ++h->n_steps % D2D_FILL_PERIOD == 0 &&

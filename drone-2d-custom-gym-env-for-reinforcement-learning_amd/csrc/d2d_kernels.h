@@ -62,6 +62,7 @@ struct StepArgs {
     int32_t* ist;            // [NISTATE][n]
     double* acc;             // [NSTATS][n]
     const Scn* scn;          // [n_scn]
+    const BrTab* brt;        // [n_scn] golden-march tables (d2d_brtab_kernel), or null
     int32_t* env_scn;        // [n] or null (all scenario 0); rewritten at resets in pool mode
     d2d_cfg cfg;
     double damping_dt;       // pow(cfg.damping, dt), host glibc
@@ -115,6 +116,8 @@ struct StepArgs {
     } while (0)
 #endif
 
+__device__ __forceinline__ const BrTab* brtab(const StepArgs& a, int si) { return a.brt ? a.brt + si : nullptr; }
+
 template <bool LDS, int NT>
 __device__ __forceinline__ const Scn* stage_scenarios(const StepArgs& a, Scn* lds) {
     if (!LDS) return a.scn;
@@ -122,6 +125,16 @@ __device__ __forceinline__ const Scn* stage_scenarios(const StepArgs& a, Scn* ld
     const double* src = reinterpret_cast<const double*>(a.scn);
     double* dst = reinterpret_cast<double*>(lds);
     for (int k = threadIdx.x; k < words; k += NT) dst[k] = src[k];
+    return lds;
+}
+// the probe tables of the golden-march tables (BrTab::hot), staged after the scenarios
+template <int NT>
+__device__ __forceinline__ const BtHot* stage_hot(const StepArgs& a, BtHot* lds) {
+    const int per = (int)(sizeof(BtHot) / 16);
+    for (int k = threadIdx.x; k < a.n_scn * per; k += NT) {
+        const double2* src = reinterpret_cast<const double2*>(&a.brt[k / per].hot) + (k % per);
+        reinterpret_cast<double2*>(lds)[k] = *src;
+    }
     return lds;
 }
 
@@ -208,9 +221,10 @@ __device__ __forceinline__ void flag_wait(const uint32_t& f) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-template <bool LDS>
+// LDS: scenario tables in LDS; LTAB: the golden-march probe tables too (after the scenarios)
+template <bool LDS, bool LTAB>
 __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
-    // dynamic LDS: n_scn scenario tables (sized at launch)
+    // dynamic LDS: n_scn scenario tables [+ n_scn probe tables] (sized at launch)
     extern __shared__ __attribute__((aligned(16))) Scn s_scn[];
     __shared__ __attribute__((aligned(16))) K1Shared sh;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -222,6 +236,7 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
     const bool auto_reset = a.cfg.auto_reset != 0;
     STAMP(0);
     const Scn* scns = stage_scenarios<LDS, K1_THREADS>(a, s_scn);
+    const BtHot* hots = LTAB ? stage_hot<K1_THREADS>(a, reinterpret_cast<BtHot*>(s_scn + a.n_scn)) : nullptr;
     if (wave == 0) sh.scn[lane] = (valid && a.env_scn && a.n_scn > 1) ? a.env_scn[i] : 0;
     if (threadIdx.x == 0) {
         sh.f_done = 0u;
@@ -417,7 +432,8 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
             F = load_frame(a, i);
             advance_position(F);
             uint32_t f = (uint32_t)fld(a.ist, D2D_I_FLAGS, n, i);
-            path_obs(a.cfg, S, F.px, F.py, F.a, f, po);
+            path_obs<LTAB>(a.cfg, S, brtab(a, sh.scn[lane]), F.px, F.py, F.a, f, po,
+                           LTAB ? hots + sh.scn[lane] : nullptr);
             sh.pflags[lane] = f & D2D_FLAG_LA_LOCK;
         }
         STAMP(4);
@@ -493,7 +509,7 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
                 for (int k = 0; k < 8; ++k) po[k] = (double)c[k];
                 rfl = (uint32_t)a.rc_rfl[i];
             } else {
-                path_obs(a.cfg, SN, sp[0], sp[1], sp[2], rfl, po);
+                path_obs(a.cfg, SN, brtab(a, nscn), sp[0], sp[1], sp[2], rfl, po);
             }
             const double th = sp[2];
             const double bodies[18] = {sp[0], sp[1], th, 0.0, 0.0, 0.0, sp[3], sp[4], th, 0.0, 0.0, 0.0,
@@ -607,7 +623,7 @@ __global__ __launch_bounds__(BLOCK) void d2d_reset_kernel(StepArgs a) {
                                sp[5], sp[6], th, 0.0, 0.0, 0.0};
     uint32_t flags = 0;
     double obs[D2D_OBS_DIM];
-    observe(a.cfg, s, Body{sp[0], sp[1], th, 0.0, 0.0, 0.0}, flags, obs);
+    observe(a.cfg, s, brtab(a, si), Body{sp[0], sp[1], th, 0.0, 0.0, 0.0}, flags, obs);
 #pragma unroll
     for (int f = 0; f < 18; ++f) fld(a.st, f, n, i) = bodies[f];
 #pragma unroll
@@ -636,12 +652,13 @@ __global__ __launch_bounds__(BLOCK) void d2d_fill_kernel(StepArgs a) {
     const int n = a.n;
     const int32_t ep = fld(a.ist, D2D_I_EPISODE, n, i);
     if (a.rc_tag[i] == ep) return;
-    const Scn& S = scns[next_scenario(a, i, (uint32_t)ep)];
+    const int si = next_scenario(a, i, (uint32_t)ep);
+    const Scn& S = scns[si];
     double sp[7], so[19], o[8];
     spawn_state(a, S, i, (uint32_t)ep, sp);
     uint32_t f = 0;
     sensor_obs(a.cfg, S, Body{sp[0], sp[1], sp[2], 0.0, 0.0, 0.0}, so);
-    path_obs(a.cfg, S, sp[0], sp[1], sp[2], f, o);
+    path_obs(a.cfg, S, brtab(a, si), sp[0], sp[1], sp[2], f, o);
     float* c = a.rc_obs + (size_t)i * D2D_OBS_DIM;
 #pragma unroll
     for (int k = 0; k < 19; ++k) c[k] = (float)so[k];
@@ -649,6 +666,14 @@ __global__ __launch_bounds__(BLOCK) void d2d_fill_kernel(StepArgs a) {
     for (int k = 0; k < 8; ++k) c[19 + k] = (float)o[k];
     a.rc_rfl[i] = (int32_t)f;
     a.rc_tag[i] = ep;
+}
+
+// ------------------------------------------------------------------------- golden-march tables
+// one thread per (scenario, kind): the forced runs of brtab_build (d2d_device.h)
+__global__ __launch_bounds__(64) void d2d_brtab_kernel(const Scn* scn, int n_scn, BrTab* out) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= 2 * n_scn) return;
+    brtab_build(scn[t >> 1], t & 1, out[t >> 1]);
 }
 
 // ------------------------------------------------------------------------------------ self-test

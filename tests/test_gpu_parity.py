@@ -294,3 +294,42 @@ def test_device_math_selftest(d2, which):
     bad = C.c_uint64(123)
     assert lib.d2d_selftest(which, 1 << 26, 2024 + which, C.byref(bad)) == 0
     assert bad.value == 0
+
+
+def test_closest_point_grid_bitwise(d2):
+    """Brent closest-point search over the whole plane and around every path, all 7 scenarios:
+    the golden-march tables (golden-left / golden-right prefixes, resume at the first differing
+    step) must give exactly the probe sequence of the plain search, so the closest / lookahead
+    points (obs 19..22) and the accumulated path error are bit-identical to the C oracle."""
+    from drone2d_amd import abi
+
+    per = 8192
+    n = per * len(SCENARIOS)
+    venv, orc = make_pair(d2, n, SCENARIOS, seed=5, kwargs=_cfgkw(), env_scenario=np.repeat(np.arange(7), per),
+                          auto_reset=False)
+    rng = np.random.default_rng(11)
+    pts = []
+    for s in venv.scenarios:
+        g = np.linspace(-600.0, 1900.0, 64)
+        grid = np.stack(np.meshgrid(g, g), -1).reshape(-1, 2)  # 4096: behind, beyond, around the path
+        L = float(s.path.us[-1])
+        u = rng.uniform(-10.0, L + 10.0, per - len(grid))
+        near = np.array([s.path(x) for x in u]) + rng.normal(0.0, 40.0, (len(u), 2))  # parabolic searches
+        pts.append(np.concatenate([grid, near]))
+    pts = np.concatenate(pts)
+    st = np.zeros((abi.NSTATE, n))
+    st[0], st[1] = pts[:, 0], pts[:, 1]
+    st[6], st[7] = pts[:, 0] - 40.0, pts[:, 1]   # motors at frame -+ 40 (theta = 0, Drone.py:37,51)
+    st[12], st[13] = pts[:, 0] + 40.0, pts[:, 1]
+    ist = np.zeros((abi.NISTATE, n), np.int32)
+    venv.set_state(torch.as_tensor(st), torch.as_tensor(ist))
+    orc.set_state(st, ist)
+    act = np.zeros((n, 2), np.float32)
+    obs, rew, term, trunc, info = (x.cpu().numpy() for x in venv.step(torch.as_tensor(act, device=venv.device)))
+    o_obs, o_rew, _, _, _ = orc.step(act)
+    np.testing.assert_array_equal(obs[:, 19:23], o_obs[:, 19:23])
+    np.testing.assert_allclose(obs, o_obs, rtol=0, atol=OBS_ATOL)
+    st2 = venv.get_state()[0].cpu().numpy()
+    o_st2 = orc.get_state()[0]
+    np.testing.assert_array_equal(st2[abi.S_PATH_ERR], o_st2[abi.S_PATH_ERR])
+    venv.close()
