@@ -880,12 +880,41 @@ __device__ __forceinline__ bool space_step(const Scn& s, double damping_dt, Body
 // sqrt is monotone and correctly rounded, so sqrt(min d^2) - r == min(sqrt(d^2) - r) bitwise.
 // Split in the velocity-dependent entries (0, 1, 2, 17, 18: need the joint sweep's output) and the
 // position-dependent ones (3..16: known right after the position update).
-__device__ __forceinline__ void sensor_vel(const Body& F, double o[19]) {
+//
+// Bearing observations.  The reference turns a direction vector (x, y) into an angle, subtracts
+// the frame angle, wraps it (ssa) and stores its sin / cos (obs 9-16, 17-18, 23-26).  For a
+// nonzero finite vector that is the unit vector rotated by -al; rel_dir computes it with one sqrt
+// and one division instead of atan2 + fmod + sincos (~200 fp64 instructions each).  It differs from
+// the reference sequence by a few ulp (|diff| <~ 1e-15 before the float32 rounding of the
+// observation); zero / tiny / non-finite vectors, where atan2's signed-zero cases decide, take the
+// reference sequence itself.  `ref` is that sequence (called only on the rare fallback lanes).
+template <typename Ref>
+__device__ __forceinline__ void rel_dir(double y, double x, double sa, double ca, double& s, double& c,
+                                        const Ref& ref) {
+    const double r2 = fma(y, y, x * x);
+    if ((r2 > 1e-200) & (r2 < 1e300)) {
+        const double ir = 1.0 / sqrt_nz(r2);
+        const double ux = x * ir, uy = y * ir;
+        s = uy * ca - ux * sa;  // sin(phi - al)
+        c = ux * ca + uy * sa;  // cos(phi - al)
+    } else {
+        ref(s, c);
+    }
+}
+// velocity part of obs (0-2, 17-18) for frame state F; sa, ca = sin / cos of F.a
+__device__ __forceinline__ void sensor_vel(const Body& F, double sa, double ca, double o[19]) {
     o[0] = m1to1(F.vx, -VEL_MAX, VEL_MAX);
     o[1] = m1to1(F.vy, -VEL_MAX, VEL_MAX);
     o[2] = clipd(F.w / 11.7, -1.0, 1.0);
-    const double vab = ssa(atan2(F.vy, F.vx) - F.a);
-    sincos_d(vab, o[17], o[18]);
+    rel_dir(F.vy, F.vx, sa, ca, o[17], o[18], [&](double& s, double& c) {
+        const double vab = ssa(atan2(F.vy, F.vx) - F.a);
+        sincos_d(vab, s, c);
+    });
+}
+__device__ __forceinline__ void sensor_vel(const Body& F, double o[19]) {
+    double sa, ca;
+    sincos_d(F.a, sa, ca);
+    sensor_vel(F, sa, ca, o);
 }
 __device__ __forceinline__ void sensor_pos(const d2d_cfg& cfg, const Scn& s, double x, double y, double al,
                                            double o[19]) {
@@ -922,12 +951,22 @@ __device__ __forceinline__ void sensor_pos(const d2d_cfg& cfg, const Scn& s, dou
     const double diag = sqrt(W * W + H * H);
     const double bd[3] = {bd0, bd1, bd2};
     const int bi[3] = {bi0, bi1, bi2};
+    double sal, cal;
+    sincos_d(al, sal, cal);
 #pragma unroll
-    for (int jj = 0; jj < 3; ++jj) {  // three independent atan2/sincos chains
+    for (int jj = 0; jj < 3; ++jj) {
         const int idx = bi[jj] < 0 ? 0 : bi[jj];
-        const double ang = ssa(atan2(y - s.cy[idx], x - s.cx[idx]) - al - PI);
+        const double dy = y - s.cy[idx], dx = x - s.cx[idx];
         double sa, ca;
-        sincos_d(ang, sa, ca);
+        // ssa(atan2(dy, dx) - al - pi): the rotated unit vector, negated
+        rel_dir(dy, dx, sal, cal, sa, ca, [&](double& rs, double& rc) {
+            const double ang = ssa(atan2(dy, dx) - al - PI);
+            sincos_d(ang, rs, rc);
+            rs = -rs;
+            rc = -rc;
+        });
+        sa = -sa;
+        ca = -ca;
         const bool have = bi[jj] >= 0;
         o[8 + 3 * jj] = have ? m1to1(bd[jj], 0.0, diag) : 1.0;
         o[9 + 3 * jj] = have ? sa : 0.0;
@@ -960,18 +999,18 @@ __device__ __forceinline__ void path_obs_u(const d2d_cfg& cfg, const Scn& s, dou
     o[1] = m1to1(cpy, 0.0, H);
     o[2] = m1to1(lax, 0.0, W);
     o[3] = m1to1(lay, 0.0, H);
-    double sa, ca;
-    sincos_d(al, sa, ca);
+    // ssa(atan2(R_w_b(alpha) d) - alpha): R_w_b rotates by +alpha, so this is the world bearing of
+    // d itself (rel_dir with the identity rotation); the reference sequence on fallback lanes:
     // np.matmul(R_w_b(alpha), d): row r = fma(R[r][0], d0, R[r][1] * d1)
-    double dx = lax - x, dy = lay - y;
-    const double bx1 = fma(ca, dx, (-sa) * dy), by1 = fma(sa, dx, ca * dy);
-    dx = cpx - x;
-    dy = cpy - y;
-    const double bx2 = fma(ca, dx, (-sa) * dy), by2 = fma(sa, dx, ca * dy);
-    const double laa = ssa(atan2(by1, bx1) - al);  // two independent chains
-    const double cpa = ssa(atan2(by2, bx2) - al);
-    sincos_d(laa, o[4], o[5]);
-    sincos_d(cpa, o[6], o[7]);
+    const auto ref = [&](double dx, double dy, double& rs, double& rc) {
+        double sa, ca;
+        sincos_d(al, sa, ca);
+        const double bx = fma(ca, dx, (-sa) * dy), by = fma(sa, dx, ca * dy);
+        sincos_d(ssa(atan2(by, bx) - al), rs, rc);
+    };
+    const double ldx = lax - x, ldy = lay - y, cdx = cpx - x, cdy = cpy - y;
+    rel_dir(ldy, ldx, 0.0, 1.0, o[4], o[5], [&](double& rs, double& rc) { ref(ldx, ldy, rs, rc); });
+    rel_dir(cdy, cdx, 0.0, 1.0, o[6], o[7], [&](double& rs, double& rc) { ref(cdx, cdy, rs, rc); });
 }
 // T: the scenario's golden-march tables (null: plain search); hot: their probe table staged in LDS
 // (LT) or null (read from T in global memory)
@@ -1007,17 +1046,22 @@ __device__ __forceinline__ int end_cause(const d2d_cfg& cfg, const Scn& s, const
 //   RewardPos  the post-position frame + end cause (path role, while it waits for the physics)
 //   RewardVel  the post-sweep velocity (physics role): speed term, velocity angle, CA total
 //   reward_path / reward_sum   the path-observation terms, then the sum (path role)
+// Angles the reward decodes from the observation (atan2 of a sin / cos pair, drone_2d_env.py:
+// 438-445) enter it only through their differences: the PP term's cos(|wrap(LA - vel)|) is the dot
+// product of the two (sin, cos) pairs, the CA term's |wrap(obst - vel)| the atan2 of their cross and
+// dot products (one atan2 instead of two + two fmods; a few ulp from the reference sequence).
 struct CAStatic {
-    double d, oa, lpa, lca, rr, near;
+    double d, os, oc, lpa, lca, rr;   // closest obstacle: distance, bearing (sin, cos) = obs 9, 10
 };
 __device__ __forceinline__ CAStatic ca_static(const d2d_cfg& cfg, const Scn& s, const double* o) {
     const double W = cfg.screen_w, H = cfg.screen_h;
-    CAStatic C{__builtin_inf(), 0.0, 1.0, 1.0, 0.0, 0.0};
+    CAStatic C{__builtin_inf(), 0.0, 1.0, 1.0, 1.0, 0.0};
     if (s.n_circles > 0) {
         const double diag = sqrt(W * W + H * H);
         const double d = invm1to1(o[8], 0.0, diag);
         C.d = d;
-        C.oa = pymod_2pi(atan2(o[9], o[10]) + TWO_PI);
+        C.os = o[9];
+        C.oc = o[10];
         const double Rr = cfg.danger_range, k = cfg.abs_inv_ca_min_rew;
         if (d < Rr && cfg.use_lambda) {
             const double l = (d / Rr) / 2.0;
@@ -1027,7 +1071,6 @@ __device__ __forceinline__ CAStatic ca_static(const d2d_cfg& cfg, const Scn& s, 
         if (d < Rr) {
             const double rr = -(((Rr + k * Rr) / (d + k * Rr)) - 1.0);
             C.rr = (rr > 0.0) ? 0.0 : rr;
-            C.near = 1.0;
         }
     }
     return C;
@@ -1051,7 +1094,7 @@ __device__ __forceinline__ RewardPos reward_pos(const d2d_cfg& cfg, const Body& 
     return R;
 }
 struct RewardVel {
-    double sv, vel_ang, cal;
+    double sv, vs, vc, cal;   // speed term, velocity bearing (sin, cos) = obs 17, 18, CA total
 };
 // o = obs with entries 0, 1, 17, 18 filled (sensor_vel)
 __device__ __forceinline__ RewardVel reward_vel(const d2d_cfg& cfg, const double* o, const CAStatic& C) {
@@ -1059,11 +1102,13 @@ __device__ __forceinline__ RewardVel reward_vel(const d2d_cfg& cfg, const double
     const double vxd = invm1to1(o[0], -VEL_MAX, VEL_MAX);
     const double vyd = invm1to1(o[1], -VEL_MAX, VEL_MAX);
     R.sv = sqrt(vxd * vxd + vyd * vyd) * cfg.pp_vel_scale;
-    R.vel_ang = pymod_2pi(atan2(o[17] * PI, o[18] * PI) + TWO_PI);
+    R.vs = o[17];
+    R.vc = o[18];
     double ca = 0.0;
-    if (C.near != 0.0) {
+    if (C.d < cfg.danger_range) {
         const double A = cfg.danger_angle, k = cfg.abs_inv_ca_min_rew;
-        const double adiff = fabs((pymod_2pi(C.oa - R.vel_ang + PI) - PI) * (180.0 / PI));
+        // |wrap(obstacle angle - velocity angle)| in degrees
+        const double adiff = fabs(atan2(C.os * R.vc - C.oc * R.vs, C.oc * R.vc + C.os * R.vs) * (180.0 / PI));
         double ar = -(((A + k * A) / (adiff + k * A)) - 1.0);
         ar = (ar > 0.0) ? 0.0 : ar;
         ca = C.rr + ar;
@@ -1072,14 +1117,15 @@ __device__ __forceinline__ RewardVel reward_vel(const d2d_cfg& cfg, const double
     return R;
 }
 struct RewardPath {
-    double la_ang, dist, pa;
+    double ls, lc, dist, pa;   // LA bearing (sin, cos) = obs 23, 24
 };
 __device__ __forceinline__ RewardPath reward_path(const d2d_cfg& cfg, const RewardPos& P, const CAStatic& C,
                                                   const double* po) {
     const double W = cfg.screen_w, H = cfg.screen_h;
     RewardPath Q;
     const double cpx = invm1to1(po[0], 0.0, W), cpy = invm1to1(po[1], 0.0, H);
-    Q.la_ang = pymod_2pi(atan2(po[4], po[5]) + TWO_PI);
+    Q.ls = po[4];
+    Q.lc = po[5];
     Q.dist = norm2(cpx - P.pxd, cpy - P.pyd);
     const double pa = -(2.0 * (clipd(Q.dist, 0.0, cfg.pa_band_edge) / cfg.pa_band_edge) - 1.0) * cfg.pa_scale;
     Q.pa = pa * C.lpa;
@@ -1091,8 +1137,9 @@ struct RewardSum {
 __device__ __forceinline__ RewardSum reward_sum(const d2d_cfg& cfg, const RewardPos& P, const RewardVel& V,
                                                 const RewardPath& Q) {
     RewardSum S;
-    const double vla = fabs(pymod_2pi(Q.la_ang - V.vel_ang + PI) - PI);
-    S.pp = clipd(cos(vla) * V.sv, cfg.pp_rew_min, cfg.pp_rew_max);
+    // cos(|wrap(LA angle - velocity angle)|)
+    const double cvla = Q.lc * V.vc + Q.ls * V.vs;
+    S.pp = clipd(cvla * V.sv, cfg.pp_rew_min, cfg.pp_rew_max);
     S.reward = P.aa + Q.pa + S.pp + P.coll + V.cal + P.reach;
     return S;
 }

@@ -191,7 +191,7 @@ __device__ __forceinline__ int next_scenario(const StepArgs& a, int j, uint32_t 
 //   f_pre   W0 -> W2        velocity part of the reward (RewardVel)
 struct K1Shared {
     double acc[D2D_NSTATS][EPB];  // W3 -> W0: episode accumulators of envs that end (prefetched)
-    double cas[6][EPB];       // W1 -> W0, W2: CAStatic (d, oa, lpa, lca, rr, near)
+    double cas[6][EPB];       // W1 -> W0, W2: CAStatic (d, os, oc, lpa, lca, rr)
     int scn[EPB];             // scenario index per env
     uint32_t cause[EPB];      // W0 -> W1, W2, W3: end cause (0: the env keeps running)
     uint32_t cvalid[EPB];     // W0 -> W1, W3: the env's reset-cache entry is ready
@@ -205,7 +205,7 @@ struct K1Shared {
             double arms[ARMS_N][EPB];          // ... and the rotated anchor arms
         } g;
         struct {
-            double pre[3][EPB];            // W0 -> W2: RewardVel
+            double pre[4][EPB];            // W0 -> W2: RewardVel
             double post[7][EPB];           // W2 -> W0: reward, pa, pp, dist, aa, coll, reach
             float obs[EPB * D2D_OBS_DIM];  // the workgroup's obs rows
         } p;                               // after f_gs
@@ -327,7 +327,7 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
         STAMP(4);
         // velocity part of the observation (obs 0-2, 17-18) into the tile / terminal obs
         if (valid) {
-            sensor_vel(F0, ov);
+            sensor_vel(F0, sn[0], cs[0], ov);
             if (!(done && auto_reset)) {
                 orow[0] = (float)ov[0];
                 orow[1] = (float)ov[1];
@@ -349,15 +349,16 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
         if (valid) {
             CAStatic C;
             C.d = sh.cas[0][lane];
-            C.oa = sh.cas[1][lane];
-            C.lpa = sh.cas[2][lane];
-            C.lca = sh.cas[3][lane];
-            C.rr = sh.cas[4][lane];
-            C.near = sh.cas[5][lane];
+            C.os = sh.cas[1][lane];
+            C.oc = sh.cas[2][lane];
+            C.lpa = sh.cas[3][lane];
+            C.lca = sh.cas[4][lane];
+            C.rr = sh.cas[5][lane];
             RV = reward_vel(a.cfg, ov, C);
             sh.u.p.pre[0][lane] = RV.sv;
-            sh.u.p.pre[1][lane] = RV.vel_ang;
-            sh.u.p.pre[2][lane] = RV.cal;
+            sh.u.p.pre[1][lane] = RV.vs;
+            sh.u.p.pre[2][lane] = RV.vc;
+            sh.u.p.pre[3][lane] = RV.cal;
             dclose = C.d;
         }
         flag_raise(sh.f_pre);
@@ -373,11 +374,11 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
             sensor_pos(a.cfg, S, F.px, F.py, F.a, so);
             const CAStatic C = ca_static(a.cfg, S, so);
             sh.cas[0][lane] = C.d;
-            sh.cas[1][lane] = C.oa;
-            sh.cas[2][lane] = C.lpa;
-            sh.cas[3][lane] = C.lca;
-            sh.cas[4][lane] = C.rr;
-            sh.cas[5][lane] = C.near;
+            sh.cas[1][lane] = C.os;
+            sh.cas[2][lane] = C.oc;
+            sh.cas[3][lane] = C.lpa;
+            sh.cas[4][lane] = C.lca;
+            sh.cas[5][lane] = C.rr;
 #pragma unroll
             for (int k = 0; k < 19; ++k) row[k] = (float)so[k];
         }
@@ -447,7 +448,7 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
             const int cause = (int)sh.cause[lane];
             d = cause != 0;
             CAStatic C;
-            C.lpa = sh.cas[2][lane];
+            C.lpa = sh.cas[3][lane];
             RP = reward_pos(a.cfg, F, cause);
             RQ = reward_path(a.cfg, RP, C, po);
         }
@@ -467,8 +468,9 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
         if (valid) {
             RewardVel V;
             V.sv = sh.u.p.pre[0][lane];
-            V.vel_ang = sh.u.p.pre[1][lane];
-            V.cal = sh.u.p.pre[2][lane];
+            V.vs = sh.u.p.pre[1][lane];
+            V.vc = sh.u.p.pre[2][lane];
+            V.cal = sh.u.p.pre[3][lane];
             const RewardSum Q = reward_sum(a.cfg, RP, V, RQ);
             sh.u.p.post[0][lane] = Q.reward;
             sh.u.p.post[1][lane] = RQ.pa;
