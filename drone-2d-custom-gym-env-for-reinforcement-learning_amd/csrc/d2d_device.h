@@ -400,11 +400,13 @@ __device__ __forceinline__ void brent_step(const Scn& s, const PathK& K, double 
     B.xf = le ? x : xf;
     B.fx = le ? fu : fx;
 }
-__device__ __forceinline__ double closest_u(const Scn& s, double px, double py) {
+// (iu: the knot interval of the result, u_index(s, result), tracked by the search)
+__device__ __forceinline__ double closest_u(const Scn& s, double px, double py, int& iu) {
     const PathK K = path_k(s);
     Brent B;
     brent_init(s, K, px, py, B);
     while (brent_active(B)) brent_step(s, K, px, py, B);
+    iu = B.ixf;
     return B.xf;
 }
 
@@ -552,7 +554,7 @@ __device__ __forceinline__ double bt_check(const BtIt& h, int k, double px, doub
 // `hot` is the scenario's probe table: LDS (address space 3) when LT, else global memory.
 template <bool LT>
 __device__ __forceinline__ double closest_u_tab(const Scn& s, const BrTab& T, const BtHot* hot, double px,
-                                                double py) {
+                                                double py, int& iu) {
     using HL = __attribute__((address_space(3))) const double;
     const auto H = [&](int kind, int j) -> BtIt {
         if (!LT) return hot->it[kind][j];
@@ -604,6 +606,7 @@ __device__ __forceinline__ double closest_u_tab(const Scn& s, const BrTab& T, co
         B.fx = norm2(px_.X - px, px_.Y - py);
         while (brent_active(B)) brent_step(s, K, px, py, B);
     }
+    iu = B.ixf;
     return B.xf;
 }
 
@@ -725,9 +728,23 @@ __device__ __forceinline__ bool phys_positions(const Scn& s, Body B[3], double f
     }
     // 1. cpBodyUpdatePosition (v_bias = 0)
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        advance_position(B[i]);
-        sincos_d(B[i].a, sn[i], cs[i]);
+    for (int i = 0; i < 3; ++i) advance_position(B[i]);
+    sincos_d(B[0].a, sn[0], cs[0]);
+    // the motors' rotations (cpBodySetAngle -> cos, sin) from the frame's: the pivot triples keep
+    // d = angle - frame angle tiny, so sin / cos(frame + d) by the addition formula with d's series
+    // (truncation < 1e-20 for |d| < 1e-2; a few ulp from sincos); larger d calls sincos
+#pragma unroll
+    for (int i = 1; i < 3; ++i) {
+        const double d = B[i].a - B[0].a;
+        if (fabs(d) < 1e-2) {
+            const double d2 = d * d;
+            const double sd = d * fma(d2, fma(d2, fma(d2, -1.0 / 5040.0, 1.0 / 120.0), -1.0 / 6.0), 1.0);
+            const double cdm1 = d2 * fma(d2, fma(d2, fma(d2, 1.0 / 40320.0, -1.0 / 720.0), 1.0 / 24.0), -0.5);
+            sn[i] = fma(sn[0], cdm1, fma(cs[0], sd, sn[0]));   // sin0 * cos d + cos0 * sin d
+            cs[i] = fma(cs[0], cdm1, fma(-sn[0], sd, cs[0]));  // cos0 * cos d - sin0 * sin d
+        } else {
+            sincos_d(B[i].a, sn[i], cs[i]);
+        }
     }
     // 2. collision: CircleToPoly(circle, frame box) contact iff dist(center, box) <= r
     return frame_hits(s, B[0], cs[0], sn[0]);
@@ -982,11 +999,12 @@ __device__ __forceinline__ void sensor_obs(const d2d_cfg& cfg, const Scn& s, con
 // reference calls it twice with identical input, predef_path.py:255 and :261).  Updates the
 // sticky LA lock in `flags`; returns the closest point (cpx, cpy) for the path-adherence reward.
 // the part after the closest-point search, for a given u
+// (iu: u's knot interval if known, else -1)
 __device__ __forceinline__ void path_obs_u(const d2d_cfg& cfg, const Scn& s, double x, double y, double al,
-                                           double u, uint32_t& flags, double o[8]) {
+                                           double u, uint32_t& flags, double o[8], int iu = -1) {
     const double W = cfg.screen_w, H = cfg.screen_h;
-    double cpx, cpy;
-    path_eval(s, u, cpx, cpy);
+    double cpx, cpy, u1;
+    path_eval_n(s, path_k(s), u, (iu >= 0) ? iu : u_index(s, u), cpx, cpy, u1);
     const double L = s.us[s.n_wps - 1];
     const double ula = (u + cfg.lookahead > L) ? L : u + cfg.lookahead;
     double lax, lay;
@@ -1017,10 +1035,12 @@ __device__ __forceinline__ void path_obs_u(const d2d_cfg& cfg, const Scn& s, dou
 template <bool LT = false>
 __device__ __forceinline__ void path_obs(const d2d_cfg& cfg, const Scn& s, const BrTab* T, double x, double y,
                                          double al, uint32_t& flags, double o[8], const BtHot* hot = nullptr) {
+    int iu = -1;
     const double u = (D2D_ABLATE & 1) ? clipd(x - 100.0, -10.0, s.us[s.n_wps - 1])
-                     : (T ? (LT ? closest_u_tab<true>(s, *T, hot, x, y) : closest_u_tab<false>(s, *T, &T->hot, x, y))
-                          : closest_u(s, x, y));
-    path_obs_u(cfg, s, x, y, al, u, flags, o);
+                     : (T ? (LT ? closest_u_tab<true>(s, *T, hot, x, y, iu)
+                                : closest_u_tab<false>(s, *T, &T->hot, x, y, iu))
+                          : closest_u(s, x, y, iu));
+    path_obs_u(cfg, s, x, y, al, u, flags, o, iu);
 }
 
 // ------------------------------------------------------------------------------ reward
@@ -1078,7 +1098,9 @@ __device__ __forceinline__ CAStatic ca_static(const d2d_cfg& cfg, const Scn& s, 
 struct RewardPos {
     double aa, coll, reach, pxd, pyd;
 };
-__device__ __forceinline__ RewardPos reward_pos(const d2d_cfg& cfg, const Body& F, int cause) {
+// sin_a: sin(F.a) (the physics wave's sincos of the frame angle); the reference takes sin(alpha) of
+// alpha = (F.a / pi) * pi, within an ulp of F.a
+__device__ __forceinline__ RewardPos reward_pos(const d2d_cfg& cfg, const Body& F, int cause, double sin_a) {
     const double W = cfg.screen_w, H = cfg.screen_h;
     RewardPos R;
     const double alpha = (F.a / PI) * PI;
@@ -1087,8 +1109,8 @@ __device__ __forceinline__ RewardPos reward_pos(const d2d_cfg& cfg, const Body& 
     R.coll = (cause & D2D_END_COLLISION) ? cfg.rew_collision : 0.0;
     R.reach = (cause & D2D_END_REACH) ? cfg.rew_reach_end : 0.0;
     double aa = 0.0;
-    if (alpha > cfg.aa_band) aa = -sin(alpha);
-    if (alpha < -cfg.aa_band) aa = sin(alpha);
+    if (alpha > cfg.aa_band) aa = -sin_a;
+    if (alpha < -cfg.aa_band) aa = sin_a;
     if (cause & D2D_END_AA) aa = cfg.rew_aa;
     R.aa = aa;
     return R;

@@ -197,6 +197,7 @@ struct K1Shared {
     uint32_t cvalid[EPB];     // W0 -> W1, W3: the env's reset-cache entry is ready
     uint32_t pflags[EPB];     // W2 -> W0: LA-lock bit after the path role
     uint32_t ep[EPB];         // W0 -> W1, W3: episode counter (the state's copy changes at a reset)
+    double sina[EPB];         // W0 -> W2: sin of the post-step frame angle (AA reward)
     uint32_t f_done, f_ca, f_gs, f_pre;
     double pe[2][EPB];        // W3 -> W0: path_err, total_reward (prefetched for the epilogue)
     union {
@@ -292,6 +293,7 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
             const bool cv = done && auto_reset && ((D2D_ABL & 16) != 0 || a.rc_tag[i] == ep);
             sh.ep[lane] = (uint32_t)ep;
             sh.cause[lane] = (uint32_t)cause;
+            sh.sina[lane] = sn[0];
             sh.cvalid[lane] = cv ? 1u : 0u;
             // positions and angles are final now (the sweep changes velocities only); envs that
             // auto-reset get their spawn state from W3 instead
@@ -449,7 +451,7 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
             d = cause != 0;
             CAStatic C;
             C.lpa = sh.cas[3][lane];
-            RP = reward_pos(a.cfg, F, cause);
+            RP = reward_pos(a.cfg, F, cause, sh.sina[lane]);
             RQ = reward_path(a.cfg, RP, C, po);
         }
         flag_wait(sh.f_gs);
