@@ -42,6 +42,8 @@ SCENARIO = "corridor"
 BYTES_PER_ENV_STEP = 650   # DESIGN.md "Algorithmic bytes": 272 read + 378 written, info off
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec)
 ACTION_BANK = 16
+# BASELINE.json configs[4]: env i gets scenario i mod 7 in this order
+MIXED = ["perpendicular", "parallel", "S_parallel", "corridor", "S_corridor", "large", "impossible"]
 
 
 def parse():
@@ -50,7 +52,8 @@ def parse():
     p.add_argument("--steps", type=int, default=1000)
     p.add_argument("--warmup", type=int, default=50)
     p.add_argument("--envs", type=int, default=ENVS_PER_GPU)
-    p.add_argument("--scenario", default=SCENARIO)
+    p.add_argument("--scenario", default=SCENARIO,
+                   help="test scenario name, NAME_free (no obstacles: configs[1]) or 'mixed' (configs[4])")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (s)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--eager", action="store_true",
@@ -113,7 +116,7 @@ def main():
 
     rank, world, local = setup_dist(args)
 
-    kwargs = dict(ENV_TRAIN_CONFIG, scenario=args.scenario)
+    kwargs = dict(ENV_TRAIN_CONFIG, scenario=MIXED if args.scenario == "mixed" else args.scenario)
     dev = torch.device("cuda", torch.cuda.current_device())
     n = args.envs
     # this rank's block of a global batch of world x n envs (global env ids, no step collective)

@@ -550,29 +550,58 @@ __device__ __forceinline__ double bt_check(const BtIt& h, int k, double px, doub
     return fu;
 }
 
-// get_closest_u through the golden-march tables (bit-identical to closest_u, see above).
+// get_closest_u through the golden-march tables (bit-identical to closest_u, see above), in three
+// pieces so that two waves can split the re-checks: bt_start (step 0, the kind), bt_verify (steps
+// [k0, k1)), bt_finish (resume brent_step at the first differing step).
 // `hot` is the scenario's probe table: LDS (address space 3) when LT, else global memory.
 template <bool LT>
-__device__ __forceinline__ double closest_u_tab(const Scn& s, const BrTab& T, const BtHot* hot, double px,
-                                                double py, int& iu) {
+__device__ __forceinline__ BtIt bt_hot(const BtHot* hot, int kind, int j) {
+    if (!LT) return hot->it[kind][j];
     using HL = __attribute__((address_space(3))) const double;
-    const auto H = [&](int kind, int j) -> BtIt {
-        if (!LT) return hot->it[kind][j];
-        const HL* q = (const HL*)&hot->it[kind][j];
-        return BtIt{q[0], q[1], q[2], q[3], q[4], q[5], q[6], q[7]};
-    };
-    // the initial point and step 0's probe are the same in both kinds; step 0's decision picks the kind
-    const BtIt h0 = H(0, 0), h1 = H(0, 1);
-    const double f0 = norm2(h0.X - px, h0.Y - py);
-    const double f1 = norm2(h1.X - px, h1.Y - py);
-    const int kind = (f1 <= f0) ? 1 : 0;
-    const int len = T.len[kind];
-    // distances at fulc, nfc, xf after step 0
-    double fa = f0, fb = kind ? f0 : f1, fc = kind ? f1 : f0;
-    int dev = len;  // first step whose decision differs from the table (len: none)
-    // steps 1, 2, ... three per pass (independent distance evaluations; the window rotates by name)
-    for (int k = 1; __ballot(k < dev) != 0ull; k += 3) {
-        const BtIt ha = H(kind, k + 1), hb = H(kind, k + 2), hc = H(kind, k + 3);
+    const HL* q = (const HL*)&hot->it[kind][j];
+    return BtIt{q[0], q[1], q[2], q[3], q[4], q[5], q[6], q[7]};
+}
+template <bool LT>
+__device__ __forceinline__ double bt_dist(const BtHot* hot, int kind, int j, double px, double py) {
+    const BtIt h = bt_hot<LT>(hot, kind, j);
+    return norm2(h.X - px, h.Y - py);
+}
+struct BtLane {
+    int kind, len, dev;   // dev: first step whose decision differs from the table (len: none)
+    double fa, fb, fc;    // distances at fulc, nfc, xf before the next step to check
+};
+// step 0: the initial point and step 0's probe are the same in both kinds; its decision picks the kind
+template <bool LT>
+__device__ __forceinline__ BtLane bt_start(const BrTab& T, const BtHot* hot, double px, double py) {
+    const double f0 = bt_dist<LT>(hot, 0, 0, px, py);
+    const double f1 = bt_dist<LT>(hot, 0, 1, px, py);
+    BtLane L;
+    L.kind = (f1 <= f0) ? 1 : 0;
+    L.len = T.len[L.kind];
+    L.dev = L.len;
+    L.fa = f0;
+    L.fb = L.kind ? f0 : f1;
+    L.fc = L.kind ? f1 : f0;
+    return L;
+}
+// the window before step k >= 3 when steps 1 .. k-1 followed the table: fulc, nfc, xf are the probes
+// of steps k-3, k-2, k-1 (probe indices k-2, k-1, k)
+template <bool LT>
+__device__ __forceinline__ void bt_window(const BtHot* hot, BtLane& L, int k, double px, double py) {
+    L.fa = bt_dist<LT>(hot, L.kind, k - 2, px, py);
+    L.fb = bt_dist<LT>(hot, L.kind, k - 1, px, py);
+    L.fc = bt_dist<LT>(hot, L.kind, k, px, py);
+}
+// re-check steps [k0, min(k1, len)) (three per pass: independent distance evaluations, the window
+// rotates by name); L.dev <- the first differing step among them
+template <bool LT>
+__device__ __forceinline__ void bt_verify(const BtHot* hot, BtLane& L, int k0, int k1, double px, double py) {
+    double fa = L.fa, fb = L.fb, fc = L.fc;
+    int dev = L.dev;
+    const int kind = L.kind;
+    for (int k = k0; __ballot(k < min(dev, k1)) != 0ull; k += 3) {
+        const BtIt ha = bt_hot<LT>(hot, kind, k + 1), hb = bt_hot<LT>(hot, kind, k + 2),
+                   hc = bt_hot<LT>(hot, kind, k + 3);
         const double fd = bt_check(ha, k, px, py, fa, fb, fc, dev);
         const double fe = bt_check(hb, k + 1, px, py, fb, fc, fd, dev);
         const double ff = bt_check(hc, k + 2, px, py, fc, fd, fe, dev);
@@ -580,9 +609,16 @@ __device__ __forceinline__ double closest_u_tab(const Scn& s, const BrTab& T, co
         fb = fe;
         fc = ff;
     }
-    dev = min(dev, len);
-    // resume brent_step from the snapshot before the first differing step (a search that followed
-    // the table restores its final state, which is inactive unless the march is longer than BT_K)
+    L.dev = min(dev, L.len);
+    L.fa = fa;
+    L.fb = fb;
+    L.fc = fc;
+}
+// resume brent_step from the snapshot before step dev (a search that followed the table restores
+// its final state, which is inactive unless the march is longer than BT_K); iu = result's interval
+template <bool LT>
+__device__ __forceinline__ double bt_finish(const Scn& s, const BrTab& T, const BtHot* hot, int kind, int dev,
+                                            double px, double py, int& iu) {
     const BtSnap& S = T.snap[kind][dev];
     Brent B;
     B.a = S.a;
@@ -600,15 +636,24 @@ __device__ __forceinline__ double closest_u_tab(const Scn& s, const BrTab& T, co
     B.ixf = S.ixf;
     if (__ballot(brent_active(B)) != 0ull) {
         const PathK K = path_k(s);
-        const BtIt pf = H(kind, S.j_fulc), pn = H(kind, S.j_nfc), px_ = H(kind, S.j_xf);
-        B.ffulc = norm2(pf.X - px, pf.Y - py);
-        B.fnfc = norm2(pn.X - px, pn.Y - py);
-        B.fx = norm2(px_.X - px, px_.Y - py);
+        B.ffulc = bt_dist<LT>(hot, kind, S.j_fulc, px, py);
+        B.fnfc = bt_dist<LT>(hot, kind, S.j_nfc, px, py);
+        B.fx = bt_dist<LT>(hot, kind, S.j_xf, px, py);
         while (brent_active(B)) brent_step(s, K, px, py, B);
     }
     iu = B.ixf;
     return B.xf;
 }
+template <bool LT>
+__device__ __forceinline__ double closest_u_tab(const Scn& s, const BrTab& T, const BtHot* hot, double px,
+                                                double py, int& iu) {
+    BtLane L = bt_start<LT>(T, hot, px, py);
+    bt_verify<LT>(hot, L, 1, BT_K, px, py);
+    return bt_finish<LT>(s, T, hot, L.kind, L.dev, px, py, iu);
+}
+// split point of the two-wave re-check: the first wave checks steps [1, bt_split), the second
+// [bt_split, len) (from its own window, bt_window)
+__device__ __forceinline__ int bt_split(const BrTab& T) { return max(3, (T.len[0] + 3) / 2); }
 
 // ------------------------------------------------------------------------------ bodies / physics
 // One cpSpaceStep(1/60) of the Drone.py body/joint configuration, split in

@@ -94,6 +94,12 @@ struct StepArgs {
 #define D2D_ABL 0        // diagnostic builds only: bit r skips role r's compute, bit 4 = perfect
                          // reset cache (no fills, every entry taken as ready): timing ablations
 #endif
+#ifndef D2D_SPLIT
+#define D2D_SPLIT 0      // 1: W3 re-checks the second half of W2's golden-march table
+#endif
+#ifndef D2D_FILL_COMPACT
+#define D2D_FILL_COMPACT 1  // K4 compacts the envs that need a fill into the leading lanes
+#endif
 #ifndef D2D_FILL_PERIOD
 #define D2D_FILL_PERIOD 16  // K4 after every this many steps (0: never; every reset synchronous)
 #endif
@@ -195,10 +201,11 @@ struct K1Shared {
     int scn[EPB];             // scenario index per env
     uint32_t cause[EPB];      // W0 -> W1, W2, W3: end cause (0: the env keeps running)
     uint32_t cvalid[EPB];     // W0 -> W1, W3: the env's reset-cache entry is ready
-    uint32_t pflags[EPB];     // W2 -> W0: LA-lock bit after the path role
+    uint32_t pflags[EPB];     // W3 -> W2: first differing step of the second half of the table re-check;
+                              // then W2 -> W0: LA-lock bit after the path role
     uint32_t ep[EPB];         // W0 -> W1, W3: episode counter (the state's copy changes at a reset)
     double sina[EPB];         // W0 -> W2: sin of the post-step frame angle (AA reward)
-    uint32_t f_done, f_ca, f_gs, f_pre;
+    uint32_t f_done, f_ca, f_gs, f_pre, f_ver;
     double pe[2][EPB];        // W3 -> W0: path_err, total_reward (prefetched for the epilogue)
     union {
         struct {
@@ -244,6 +251,7 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
         sh.f_ca = 0u;
         sh.f_gs = 0u;
         sh.f_pre = 0u;
+        sh.f_ver = 0u;
     }
     __syncthreads();
     STAMP(1);
@@ -435,8 +443,20 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
             F = load_frame(a, i);
             advance_position(F);
             uint32_t f = (uint32_t)fld(a.ist, D2D_I_FLAGS, n, i);
-            path_obs<LTAB>(a.cfg, S, brtab(a, sh.scn[lane]), F.px, F.py, F.a, f, po,
-                           LTAB ? hots + sh.scn[lane] : nullptr);
+            const BrTab* T = brtab(a, sh.scn[lane]);
+            if (D2D_SPLIT && T && !(D2D_ABLATE & 1)) {
+                // golden-march re-check of steps [1, split); W3 checks [split, len) meanwhile
+                const BtHot* hot = LTAB ? hots + sh.scn[lane] : &T->hot;
+                BtLane L = bt_start<LTAB>(*T, hot, F.px, F.py);
+                bt_verify<LTAB>(hot, L, 1, bt_split(*T), F.px, F.py);
+                flag_wait(sh.f_ver);
+                L.dev = min(L.dev, (int)sh.pflags[lane]);
+                int iu;
+                const double u = bt_finish<LTAB>(S, *T, hot, L.kind, L.dev, F.px, F.py, iu);
+                path_obs_u(a.cfg, S, F.px, F.py, F.a, u, f, po, iu);
+            } else {
+                path_obs<LTAB>(a.cfg, S, T, F.px, F.py, F.a, f, po, LTAB ? hots + sh.scn[lane] : nullptr);
+            }
             sh.pflags[lane] = f & D2D_FLAG_LA_LOCK;
         }
         STAMP(4);
@@ -484,8 +504,25 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
         }
     } else {
         // ---------------------------------------------------------------- auto-reset observation
-        D2D_SETPRIO(D2D_PRIO_W3);
+        if (D2D_SPLIT) D2D_SETPRIO(D2D_PRIO_W2);  // the re-check below is on W2's critical path
         double po[8];
+        if (D2D_SPLIT && valid && !(D2D_ABL & 4) && !(D2D_ABLATE & 1) && a.brt) {
+            // second half of W2's golden-march re-check (its first wave-priority work)
+            const BrTab& T = a.brt[sh.scn[lane]];
+            const BtHot* hot = LTAB ? hots + sh.scn[lane] : &T.hot;
+            Body F = load_frame(a, i);
+            advance_position(F);
+            BtLane L = bt_start<LTAB>(T, hot, F.px, F.py);
+            const int k0 = bt_split(T);
+            if (k0 < L.len) {
+                bt_window<LTAB>(hot, L, k0, F.px, F.py);
+                bt_verify<LTAB>(hot, L, k0, BT_K, F.px, F.py);
+            }
+            sh.pflags[lane] = (uint32_t)L.dev;
+        }
+        flag_raise(sh.f_ver);
+        if (D2D_SPLIT) __builtin_amdgcn_s_setprio(D2D_PRIO_W3);
+        else D2D_SETPRIO(D2D_PRIO_W3);
         if (valid) {
             // running path error / return for W0's epilogue
             sh.pe[0][lane] = fld(a.st, D2D_S_PATH_ERR, n, i);
@@ -644,18 +681,41 @@ __global__ __launch_bounds__(BLOCK) void d2d_reset_kernel(StepArgs a) {
 }
 
 // ------------------------------------------------------------------------------ cache fill (K4)
-// one lane per env: an env whose entry does not belong to its current episode computes the
-// observation its next auto-reset will return (test-mode spawn of the next episode's scenario)
+// an env whose entry does not belong to its current episode computes the observation its next
+// auto-reset will return (test-mode spawn of the next episode's scenario).  Only the envs reset
+// since the last fill need it (~1/5 of them at fill period 16): each workgroup compacts its
+// envs that do into the leading lanes (ballot + popcount), so the long search runs in as few
+// waves as possible instead of one wave per 64 envs with a few active lanes.
 template <bool LDS>
 __global__ __launch_bounds__(BLOCK) void d2d_fill_kernel(StepArgs a) {
     extern __shared__ __attribute__((aligned(16))) Scn s_scn[];
+    __shared__ int list[BLOCK];
+    __shared__ int cnt[BLOCK / 64];
     const Scn* scns = stage_scenarios<LDS, BLOCK>(a, s_scn);
-    __syncthreads();
-    const int i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= a.n) return;
     const int n = a.n;
+    const int i0 = blockIdx.x * BLOCK + threadIdx.x;
+    const bool need = (i0 < n) && (a.rc_tag[i0] != fld(a.ist, D2D_I_EPISODE, n, i0));
+    int i = i0;
+    if (!D2D_FILL_COMPACT) {
+        __syncthreads();
+        if (!need) return;
+    } else {
+    const uint64_t m = __ballot(need);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane == 0) cnt[wave] = __popcll(m);
+    __syncthreads();
+    int off = 0, total = 0;
+#pragma unroll
+    for (int w = 0; w < BLOCK / 64; ++w) {
+        off += (w < wave) ? cnt[w] : 0;
+        total += cnt[w];
+    }
+    if (need) list[off + __popcll(m & ((1ull << lane) - 1ull))] = i0;
+    __syncthreads();
+    if ((int)threadIdx.x >= total) return;
+    i = list[threadIdx.x];
+    }
     const int32_t ep = fld(a.ist, D2D_I_EPISODE, n, i);
-    if (a.rc_tag[i] == ep) return;
     const int si = next_scenario(a, i, (uint32_t)ep);
     const Scn& S = scns[si];
     double sp[7], so[19], o[8];
