@@ -30,7 +30,7 @@
 
 // Diagnostic-only ablation mask (tools/ablate.py builds separate timing-only libraries with it;
 // the product is always built with 0): 1 skip Brent, 2 skip sensing, 4 skip joint iterations,
-// 8 skip collision test.
+// 8 skip collision test, 16 skip the Brent continuation after the golden-march tables.
 #ifndef D2D_ABLATE
 #define D2D_ABLATE 0
 #endif
@@ -639,7 +639,7 @@ __device__ __forceinline__ double bt_finish(const Scn& s, const BrTab& T, const 
         B.ffulc = bt_dist<LT>(hot, kind, S.j_fulc, px, py);
         B.fnfc = bt_dist<LT>(hot, kind, S.j_nfc, px, py);
         B.fx = bt_dist<LT>(hot, kind, S.j_xf, px, py);
-        while (brent_active(B)) brent_step(s, K, px, py, B);
+        while (!(D2D_ABLATE & 16) && brent_active(B)) brent_step(s, K, px, py, B);
     }
     iu = B.ixf;
     return B.xf;

@@ -4,6 +4,7 @@
 // observation cache fill).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -15,6 +16,9 @@
 
 using namespace d2dk;
 
+#ifndef D2D_GROUP
+#define D2D_GROUP 1  // 0: no scenario-grouped lane map (diagnostic A/B builds only)
+#endif
 #ifndef D2D_BRTAB
 #define D2D_BRTAB 1  // 0: searches without the golden-march tables (diagnostic A/B builds only)
 #endif
@@ -35,6 +39,7 @@ int hip_fail(hipError_t e, const char* what) {
 struct d2d_handle {
     d2d_cfg cfg;
     int n = 0;
+    int ns = 0;   // state slots (columns of the internal [F][ns] arrays): n, or the grouped layout's
     int device = 0;
     int n_scn = 0;
     double* st = nullptr;
@@ -51,6 +56,11 @@ struct d2d_handle {
     int32_t* rc_rfl = nullptr;   // [n]
     int32_t* rc_tag = nullptr;   // [n]
     bool rc_dirty = true;        // scenarios changed since the cache was last dropped
+    // scenario-grouped slot layout (StepArgs::lane_env), built by d2d_set_scenarios
+    int32_t* lane_env = nullptr;  // [ns] slot -> env (-1: padding)
+    int32_t* wg_scn = nullptr;    // [ns / EPB] scenario of each slot group
+    int32_t* env_slot = nullptr;  // [n] env -> slot
+    int n_groups = 0;
     uint64_t n_steps = 0;        // d2d_step calls (fill cadence)
 };
 
@@ -59,6 +69,7 @@ namespace {
 StepArgs make_args(const d2d_t* h) {
     StepArgs a{};
     a.n = h->n;
+    a.ns = h->ns;
     a.n_scn = h->n_scn;
     a.st = h->st;
     a.ist = h->ist;
@@ -73,13 +84,15 @@ StepArgs make_args(const d2d_t* h) {
     a.rc_obs = h->rc_obs;
     a.rc_rfl = h->rc_rfl;
     a.rc_tag = h->rc_tag;
+    a.lane_env = h->lane_env;
+    a.wg_scn = h->wg_scn;
     return a;
 }
 
 // K4: fill every cache entry that does not belong to its env's current episode, ordered on `stream`
 hipError_t rc_fill(d2d_t* h, hipStream_t stream) {
     StepArgs a = make_args(h);
-    const dim3 grid((h->n + BLOCK - 1) / BLOCK);
+    const dim3 grid((h->ns + BLOCK - 1) / BLOCK);
     if (sizeof(d2d::Scn) * (size_t)h->n_scn <= K2_LDS_BUDGET)
         hipLaunchKernelGGL(d2d_fill_kernel<true>, grid, dim3(BLOCK), sizeof(d2d::Scn) * h->n_scn, stream, a);
     else
@@ -88,10 +101,138 @@ hipError_t rc_fill(d2d_t* h, hipStream_t stream) {
 }
 // drop every entry (new seed, counters or scenarios) and refill, ordered on `stream`
 hipError_t rc_rebuild(d2d_t* h, hipStream_t stream) {
-    hipError_t e = hipMemsetAsync(h->rc_tag, 0xFF, sizeof(int32_t) * (size_t)h->n, stream);
+    hipError_t e = hipMemsetAsync(h->rc_tag, 0xFF, sizeof(int32_t) * (size_t)h->ns, stream);
     if (e == hipSuccess && D2D_FILL_PERIOD > 0) e = rc_fill(h, stream);
     if (e == hipSuccess) h->rc_dirty = false;
     return e;
+}
+
+// Scenario-grouped slot layout for a static env -> scenario map with several scenarios: each K1
+// workgroup then steps 64 envs of ONE scenario (no per-lane scenario divergence in the Brent
+// search, one scenario + probe table staged in LDS) whose state is contiguous.  The envs, sorted
+// by (scenario, id), are cut into ceil(n / 64) groups -- no padding between scenarios, so the grid
+// is no larger than the identity layout's (at 65 536 envs: 1 024 workgroups = one resident round)
+// and at most n_scn - 1 groups straddle two or more scenarios (wg_scn = -1).  Groups are then
+// ordered by their first env id, so groups whose envs interleave (e.g. scenario = id mod 7) get
+// consecutive numbers (xcd_group places consecutive numbers on one XCD).
+void make_groups(int n, const int32_t* env_scn, int n_scn, std::vector<int32_t>& lanes, std::vector<int32_t>& ws) {
+    std::vector<int32_t> order((size_t)n);
+    for (int i = 0; i < n; ++i) order[(size_t)i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](int32_t x, int32_t y) { return env_scn[x] < env_scn[y]; });
+    const size_t ng = ((size_t)n + EPB - 1) / EPB;
+    std::vector<size_t> gi(ng);
+    for (size_t g = 0; g < ng; ++g) gi[g] = g;
+    std::sort(gi.begin(), gi.end(), [&](size_t x, size_t y) { return order[x * EPB] < order[y * EPB]; });
+    lanes.assign(ng * EPB, -1);
+    ws.assign(ng, 0);
+    for (size_t g = 0; g < ng; ++g) {
+        const size_t o = gi[g] * EPB;
+        int32_t sc = env_scn[order[o]];
+        for (size_t l = 0; l < EPB && o + l < (size_t)n; ++l) {
+            lanes[g * EPB + l] = order[o + l];
+            if (env_scn[order[o + l]] != sc) sc = -1;
+        }
+        ws[g] = sc;
+    }
+}
+
+// Internal arrays of one slot layout.
+struct Layout {
+    int ns = 0;
+    double* st = nullptr;
+    int32_t* ist = nullptr;
+    double* acc = nullptr;
+    float* rc_obs = nullptr;
+    int32_t* rc_rfl = nullptr;
+    int32_t* rc_tag = nullptr;
+    int32_t* lane_env = nullptr;
+    int32_t* wg_scn = nullptr;
+    int32_t* env_slot = nullptr;
+};
+void free_layout(Layout& L) {
+    for (void* p : {(void*)L.st, (void*)L.ist, (void*)L.acc, (void*)L.rc_obs, (void*)L.rc_rfl, (void*)L.rc_tag,
+                    (void*)L.lane_env, (void*)L.wg_scn, (void*)L.env_slot})
+        if (p) (void)hipFree(p);
+    L = Layout{};
+}
+// allocate a layout of n envs: identity (lanes empty) or grouped (lanes: slot -> env, ws: scenario
+// per group); state zeroed, reset cache empty
+hipError_t alloc_layout(Layout& L, int n, const std::vector<int32_t>& lanes, const std::vector<int32_t>& ws) {
+    L = Layout{};
+    L.ns = lanes.empty() ? n : (int)lanes.size();
+    const size_t ns = (size_t)L.ns;
+    hipError_t e;
+    if ((e = hipMalloc(&L.st, sizeof(double) * D2D_NSTATE * ns)) != hipSuccess ||
+        (e = hipMalloc(&L.ist, sizeof(int32_t) * D2D_NISTATE * ns)) != hipSuccess ||
+        (e = hipMalloc(&L.acc, sizeof(double) * D2D_NSTATS * ns)) != hipSuccess ||
+        (e = hipMalloc(&L.rc_obs, sizeof(float) * D2D_OBS_DIM * ns)) != hipSuccess ||
+        (e = hipMalloc(&L.rc_rfl, sizeof(int32_t) * ns)) != hipSuccess ||
+        (e = hipMalloc(&L.rc_tag, sizeof(int32_t) * ns)) != hipSuccess ||
+        (e = hipMemset(L.st, 0, sizeof(double) * D2D_NSTATE * ns)) != hipSuccess ||
+        (e = hipMemset(L.ist, 0, sizeof(int32_t) * D2D_NISTATE * ns)) != hipSuccess ||
+        (e = hipMemset(L.acc, 0, sizeof(double) * D2D_NSTATS * ns)) != hipSuccess ||
+        (e = hipMemset(L.rc_tag, 0xFF, sizeof(int32_t) * ns)) != hipSuccess) {
+        free_layout(L);
+        return e;
+    }
+    if (!lanes.empty()) {
+        std::vector<int32_t> es((size_t)n, 0);
+        for (size_t k = 0; k < lanes.size(); ++k)
+            if (lanes[k] >= 0) es[(size_t)lanes[k]] = (int32_t)k;
+        if ((e = hipMalloc(&L.lane_env, sizeof(int32_t) * ns)) != hipSuccess ||
+            (e = hipMalloc(&L.wg_scn, sizeof(int32_t) * ws.size())) != hipSuccess ||
+            (e = hipMalloc(&L.env_slot, sizeof(int32_t) * (size_t)n)) != hipSuccess ||
+            (e = hipMemcpy(L.lane_env, lanes.data(), sizeof(int32_t) * ns, hipMemcpyHostToDevice)) != hipSuccess ||
+            (e = hipMemcpy(L.wg_scn, ws.data(), sizeof(int32_t) * ws.size(), hipMemcpyHostToDevice)) != hipSuccess ||
+            (e = hipMemcpy(L.env_slot, es.data(), sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice)) != hipSuccess) {
+            free_layout(L);
+            return e;
+        }
+    }
+    return hipSuccess;
+}
+Layout take_layout(d2d_t* h) {
+    Layout L;
+    L.ns = h->ns;
+    L.st = h->st;
+    L.ist = h->ist;
+    L.acc = h->acc;
+    L.rc_obs = h->rc_obs;
+    L.rc_rfl = h->rc_rfl;
+    L.rc_tag = h->rc_tag;
+    L.lane_env = h->lane_env;
+    L.wg_scn = h->wg_scn;
+    L.env_slot = h->env_slot;
+    return L;
+}
+void put_layout(d2d_t* h, const Layout& L) {
+    h->ns = L.ns;
+    h->st = L.st;
+    h->ist = L.ist;
+    h->acc = L.acc;
+    h->rc_obs = L.rc_obs;
+    h->rc_rfl = L.rc_rfl;
+    h->rc_tag = L.rc_tag;
+    h->lane_env = L.lane_env;
+    h->wg_scn = L.wg_scn;
+    h->env_slot = L.env_slot;
+    h->n_groups = L.lane_env ? L.ns / EPB : 0;
+}
+// every env's state, flags and accumulators from layout `from` to layout `to` (stream-ordered)
+template <typename T>
+hipError_t permute(const T* src, int sstride, const int32_t* sslot, T* dst, int dstride, const int32_t* dslot, int nf,
+                   int n, hipStream_t stream) {
+    hipLaunchKernelGGL(d2d_permute_kernel<T>, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, stream, src, sstride, sslot,
+                       dst, dstride, dslot, nf, n);
+    return hipGetLastError();
+}
+hipError_t move_state(const Layout& from, const Layout& to, int n) {
+    hipError_t e;
+    if ((e = permute(from.st, from.ns, from.env_slot, to.st, to.ns, to.env_slot, D2D_NSTATE, n, 0)) != hipSuccess ||
+        (e = permute(from.ist, from.ns, from.env_slot, to.ist, to.ns, to.env_slot, D2D_NISTATE, n, 0)) != hipSuccess ||
+        (e = permute(from.acc, from.ns, from.env_slot, to.acc, to.ns, to.env_slot, D2D_NSTATS, n, 0)) != hipSuccess)
+        return e;
+    return hipDeviceSynchronize();
 }
 
 struct DeviceGuard {
@@ -126,21 +267,14 @@ int32_t d2d_create(const d2d_cfg* cfg, int32_t n_envs, int32_t device, d2d_t** o
     h->n = n_envs;
     h->device = device;
     const size_t n = (size_t)n_envs;
-    if ((e = hipMalloc(&h->st, sizeof(double) * D2D_NSTATE * n)) != hipSuccess ||
-        (e = hipMalloc(&h->ist, sizeof(int32_t) * D2D_NISTATE * n)) != hipSuccess ||
-        (e = hipMalloc(&h->acc, sizeof(double) * D2D_NSTATS * n)) != hipSuccess ||
-        (e = hipMalloc(&h->env_scn, sizeof(int32_t) * n)) != hipSuccess ||
-        (e = hipMalloc(&h->rc_obs, sizeof(float) * D2D_OBS_DIM * n)) != hipSuccess ||
-        (e = hipMalloc(&h->rc_rfl, sizeof(int32_t) * n)) != hipSuccess ||
-        (e = hipMalloc(&h->rc_tag, sizeof(int32_t) * n)) != hipSuccess) {
+    Layout L;
+    if ((e = hipMalloc(&h->env_scn, sizeof(int32_t) * n)) != hipSuccess ||
+        (e = alloc_layout(L, n_envs, {}, {})) != hipSuccess) {
         d2d_destroy(h);
         return hip_fail(e, "d2d_create: hipMalloc");
     }
-    (void)hipMemset(h->st, 0, sizeof(double) * D2D_NSTATE * n);
-    (void)hipMemset(h->ist, 0, sizeof(int32_t) * D2D_NISTATE * n);
-    (void)hipMemset(h->acc, 0, sizeof(double) * D2D_NSTATS * n);
+    put_layout(h, L);
     (void)hipMemset(h->env_scn, 0, sizeof(int32_t) * n);
-    (void)hipMemset(h->rc_tag, 0xFF, sizeof(int32_t) * n);
     if ((e = hipDeviceSynchronize()) != hipSuccess) {
         d2d_destroy(h);
         return hip_fail(e, "d2d_create: memset");
@@ -152,15 +286,11 @@ int32_t d2d_create(const d2d_cfg* cfg, int32_t n_envs, int32_t device, d2d_t** o
 void d2d_destroy(d2d_t* h) {
     if (!h) return;
     DeviceGuard g(h->device);
-    if (h->st) (void)hipFree(h->st);
-    if (h->ist) (void)hipFree(h->ist);
-    if (h->acc) (void)hipFree(h->acc);
+    Layout L = take_layout(h);
+    free_layout(L);
     if (h->scn) (void)hipFree(h->scn);
     if (h->brt) (void)hipFree(h->brt);
     if (h->env_scn) (void)hipFree(h->env_scn);
-    if (h->rc_obs) (void)hipFree(h->rc_obs);
-    if (h->rc_rfl) (void)hipFree(h->rc_rfl);
-    if (h->rc_tag) (void)hipFree(h->rc_tag);
     delete h;
 }
 
@@ -222,6 +352,20 @@ int32_t d2d_set_scenarios(d2d_t* h, const d2d_scn* scns, int32_t n_scn, const in
     } else if ((e = hipMemset(h->env_scn, 0, sizeof(int32_t) * (size_t)h->n)) != hipSuccess) {
         return hip_fail(e, "hipMemset env_scn");
     }
+    // slot layout: grouped for a static mixed map (pool mode redraws scenarios at every reset);
+    // the current state moves into the new layout
+    std::vector<int32_t> lanes, ws;
+    if (D2D_GROUP && env_scn_host && n_scn > 1 && !h->cfg.scn_pool) make_groups(h->n, env_scn_host, n_scn, lanes, ws);
+    if (!lanes.empty() || h->lane_env) {
+        Layout from = take_layout(h), to;
+        if ((e = alloc_layout(to, h->n, lanes, ws)) != hipSuccess) return hip_fail(e, "d2d_set_scenarios: layout");
+        if ((e = move_state(from, to, h->n)) != hipSuccess) {
+            free_layout(to);
+            return hip_fail(e, "d2d_set_scenarios: layout move");
+        }
+        put_layout(h, to);
+        free_layout(from);
+    }
     h->n_scn = n_scn;
     h->rc_dirty = true;  // cached reset observations belong to the old scenarios
     return D2D_OK;
@@ -235,7 +379,7 @@ int32_t d2d_reset(d2d_t* h, const uint8_t* mask_dev, uint64_t seed, float* obs_d
     StepArgs a = make_args(h);
     a.obs = obs_dev;
     a.mask = mask_dev;
-    const dim3 grid((h->n + BLOCK - 1) / BLOCK);
+    const dim3 grid((h->ns + BLOCK - 1) / BLOCK);
     if (sizeof(d2d::Scn) * (size_t)h->n_scn <= K2_LDS_BUDGET)
         hipLaunchKernelGGL(d2d_reset_kernel<true>, grid, dim3(BLOCK), sizeof(d2d::Scn) * h->n_scn, (hipStream_t)stream, a);
     else
@@ -268,7 +412,11 @@ int32_t d2d_step(d2d_t* h, const float* act_dev, float* obs_dev, float* rew_dev,
     a.tobs = term_obs_dev;
     const dim3 grid((h->n + EPB - 1) / EPB);
     const size_t lds_scn = sizeof(d2d::Scn) * (size_t)h->n_scn, lds_hot = sizeof(d2d::BtHot) * (size_t)h->n_scn;
-    if (a.brt && lds_scn + lds_hot + sizeof(K1Shared) <= K1_LDS_BUDGET)
+    static_assert(sizeof(d2d::Scn) + sizeof(d2d::BtHot) + sizeof(K1Shared) <= K1_LDS_BUDGET, "grouped K1 LDS");
+    if (h->lane_env)
+        hipLaunchKernelGGL(d2d_step_grouped_kernel, dim3(h->n_groups), dim3(K1_THREADS),
+                           sizeof(d2d::Scn) + sizeof(d2d::BtHot), (hipStream_t)stream, a);
+    else if (a.brt && lds_scn + lds_hot + sizeof(K1Shared) <= K1_LDS_BUDGET)
         hipLaunchKernelGGL((d2d_step_kernel<true, true>), grid, dim3(K1_THREADS), lds_scn + lds_hot, (hipStream_t)stream, a);
     else if (lds_scn + sizeof(K1Shared) <= K1_LDS_BUDGET)
         hipLaunchKernelGGL((d2d_step_kernel<true, false>), grid, dim3(K1_THREADS), lds_scn, (hipStream_t)stream, a);
@@ -287,13 +435,23 @@ int32_t d2d_get_state(d2d_t* h, double* state_dev, int32_t* istate_dev, void* st
     DeviceGuard g(h->device);
     hipError_t e;
     const size_t n = (size_t)h->n;
+    const hipStream_t s = (hipStream_t)stream;
+    if (h->lane_env) {  // grouped slot layout -> env order
+        if (state_dev && (e = permute(h->st, h->ns, h->env_slot, state_dev, h->n, (const int32_t*)nullptr, D2D_NSTATE,
+                                      h->n, s)) != hipSuccess)
+            return hip_fail(e, "d2d_get_state");
+        if (istate_dev && (e = permute(h->ist, h->ns, h->env_slot, istate_dev, h->n, (const int32_t*)nullptr,
+                                       D2D_NISTATE, h->n, s)) != hipSuccess)
+            return hip_fail(e, "d2d_get_state");
+        return D2D_OK;
+    }
     if (state_dev &&
-        (e = hipMemcpyAsync(state_dev, h->st, sizeof(double) * D2D_NSTATE * n, hipMemcpyDeviceToDevice,
-                            (hipStream_t)stream)) != hipSuccess)
+        (e = hipMemcpyAsync(state_dev, h->st, sizeof(double) * D2D_NSTATE * n, hipMemcpyDeviceToDevice, s)) !=
+            hipSuccess)
         return hip_fail(e, "d2d_get_state");
     if (istate_dev &&
-        (e = hipMemcpyAsync(istate_dev, h->ist, sizeof(int32_t) * D2D_NISTATE * n, hipMemcpyDeviceToDevice,
-                            (hipStream_t)stream)) != hipSuccess)
+        (e = hipMemcpyAsync(istate_dev, h->ist, sizeof(int32_t) * D2D_NISTATE * n, hipMemcpyDeviceToDevice, s)) !=
+            hipSuccess)
         return hip_fail(e, "d2d_get_state");
     return D2D_OK;
 }
@@ -303,14 +461,24 @@ int32_t d2d_set_state(d2d_t* h, const double* state_dev, const int32_t* istate_d
     DeviceGuard g(h->device);
     hipError_t e;
     const size_t n = (size_t)h->n;
-    if (state_dev &&
-        (e = hipMemcpyAsync(h->st, state_dev, sizeof(double) * D2D_NSTATE * n, hipMemcpyDeviceToDevice,
-                            (hipStream_t)stream)) != hipSuccess)
-        return hip_fail(e, "d2d_set_state");
-    if (istate_dev &&
-        (e = hipMemcpyAsync(h->ist, istate_dev, sizeof(int32_t) * D2D_NISTATE * n, hipMemcpyDeviceToDevice,
-                            (hipStream_t)stream)) != hipSuccess)
-        return hip_fail(e, "d2d_set_state");
+    const hipStream_t s = (hipStream_t)stream;
+    if (h->lane_env) {  // env order -> grouped slot layout
+        if (state_dev && (e = permute(state_dev, h->n, (const int32_t*)nullptr, h->st, h->ns, h->env_slot, D2D_NSTATE,
+                                      h->n, s)) != hipSuccess)
+            return hip_fail(e, "d2d_set_state");
+        if (istate_dev && (e = permute(istate_dev, h->n, (const int32_t*)nullptr, h->ist, h->ns, h->env_slot,
+                                       D2D_NISTATE, h->n, s)) != hipSuccess)
+            return hip_fail(e, "d2d_set_state");
+    } else {
+        if (state_dev &&
+            (e = hipMemcpyAsync(h->st, state_dev, sizeof(double) * D2D_NSTATE * n, hipMemcpyDeviceToDevice, s)) !=
+                hipSuccess)
+            return hip_fail(e, "d2d_set_state");
+        if (istate_dev &&
+            (e = hipMemcpyAsync(h->ist, istate_dev, sizeof(int32_t) * D2D_NISTATE * n, hipMemcpyDeviceToDevice, s)) !=
+                hipSuccess)
+            return hip_fail(e, "d2d_set_state");
+    }
     if ((e = rc_rebuild(h, (hipStream_t)stream)) != hipSuccess) return hip_fail(e, "d2d_set_state: cache rebuild");
     h->reset_done = true;
     return D2D_OK;
@@ -319,7 +487,7 @@ int32_t d2d_set_state(d2d_t* h, const double* state_dev, const int32_t* istate_d
 int32_t d2d_episode_stats(d2d_t* h, double* out_dev, int32_t clear, void* stream) {
     if (!h || !out_dev) return fail(D2D_E_ARG, "d2d_episode_stats: null handle/out");
     DeviceGuard g(h->device);
-    hipLaunchKernelGGL(d2d_stats_kernel, dim3(D2D_NSTATS), dim3(BLOCK), 0, (hipStream_t)stream, h->acc, h->n,
+    hipLaunchKernelGGL(d2d_stats_kernel, dim3(D2D_NSTATS), dim3(BLOCK), 0, (hipStream_t)stream, h->acc, h->ns,
                        out_dev, clear, h->acc);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "d2d_episode_stats launch");

@@ -56,7 +56,9 @@ constexpr size_t K2_LDS_BUDGET = 64 * 1024;
     } while (0)
 
 struct StepArgs {
-    int n;
+    int n;                   // envs
+    int ns;                  // state slots: the column count of every [F][ns] internal array (= n
+                             // unless the grouped lane map pads scenario groups, see lane_env)
     int n_scn;
     double* st;              // [NSTATE][n]
     int32_t* ist;            // [NISTATE][n]
@@ -80,6 +82,14 @@ struct StepArgs {
     float* rc_obs;           // [n][27] next reset observation
     int32_t* rc_rfl;         // [n] flags of the next reset observation (LA lock)
     int32_t* rc_tag;         // [n] episode counter the entry belongs to (-1: none)
+    // Scenario-grouped slot layout (null unless the env -> scenario map is static and mixed).
+    // Internal state lives in slots: slot s holds env lane_env[s] (-1: padding), and slots
+    // [64 g, 64 g + 64) all hold envs of scenario wg_scn[g], so K1 workgroup g (after the XCD-aware
+    // renumbering, xcd_group) reads its state coalesced and stages one scenario.  The caller's
+    // buffers (actions, obs, reward, flags, info, terminal obs), the scenario map and the spawn RNG
+    // stay indexed by env id.  Without the map slot == env.
+    const int32_t* lane_env;  // [ns] slot -> env
+    const int32_t* wg_scn;    // [ns / 64]
 };
 
 // Auto-reset observation cache.  The observation an env gets when it auto-resets depends only on
@@ -124,24 +134,38 @@ struct StepArgs {
 
 __device__ __forceinline__ const BrTab* brtab(const StepArgs& a, int si) { return a.brt ? a.brt + si : nullptr; }
 
+// Scenarios [first, first + count) into LDS; the returned table is indexed by the global scenario
+// index (a grouped K1 workgroup stages only its own scenario: the base is offset by -first, LDS
+// addresses are 32-bit and wrap back into the staged block for the indices it holds).
 template <bool LDS, int NT>
-__device__ __forceinline__ const Scn* stage_scenarios(const StepArgs& a, Scn* lds) {
+__device__ __forceinline__ const Scn* stage_scenarios(const StepArgs& a, Scn* lds, int first = 0, int count = -1) {
     if (!LDS) return a.scn;
-    const int words = a.n_scn * (int)(sizeof(Scn) / 8);
-    const double* src = reinterpret_cast<const double*>(a.scn);
+    if (count < 0) count = a.n_scn;
+    const int words = count * (int)(sizeof(Scn) / 8);
+    const double* src = reinterpret_cast<const double*>(a.scn + first);
     double* dst = reinterpret_cast<double*>(lds);
     for (int k = threadIdx.x; k < words; k += NT) dst[k] = src[k];
-    return lds;
+    return lds - first;
 }
 // the probe tables of the golden-march tables (BrTab::hot), staged after the scenarios
 template <int NT>
-__device__ __forceinline__ const BtHot* stage_hot(const StepArgs& a, BtHot* lds) {
+__device__ __forceinline__ const BtHot* stage_hot(const StepArgs& a, BtHot* lds, int first = 0, int count = -1) {
+    if (count < 0) count = a.n_scn;
     const int per = (int)(sizeof(BtHot) / 16);
-    for (int k = threadIdx.x; k < a.n_scn * per; k += NT) {
-        const double2* src = reinterpret_cast<const double2*>(&a.brt[k / per].hot) + (k % per);
+    for (int k = threadIdx.x; k < count * per; k += NT) {
+        const double2* src = reinterpret_cast<const double2*>(&a.brt[first + k / per].hot) + (k % per);
         reinterpret_cast<double2*>(lds)[k] = *src;
     }
-    return lds;
+    return lds - first;
+}
+// Workgroup renumbering for the grouped lane map: blocks b and b + 8 share an XCD (and its L2)
+// when the grid is dealt round-robin over the 8 XCDs, so consecutive group numbers -- groups whose
+// envs share cache lines -- go to blocks on one XCD.  Placement only affects speed.
+// XCD x = b % 8 holds per + (x < rem) blocks; its k-th block (k = b / 8) takes group number
+// (groups of XCDs before x) + k, a bijection on [0, nb).
+__device__ __forceinline__ int xcd_group(int b, int nb) {
+    const int per = nb / 8, rem = nb % 8, x = b % 8, k = b / 8;
+    return (x < rem) ? x * (per + 1) + k : rem * (per + 1) + (x - rem) * per + k;
 }
 
 __device__ __forceinline__ size_t fidx(int f, int n, int i) { return (size_t)f * (size_t)n + (size_t)i; }
@@ -155,7 +179,7 @@ __device__ __forceinline__ T& fld(T* base, int f, int n, int i) {
 
 // frame state as stored (pre-step)
 __device__ __forceinline__ Body load_frame(const StepArgs& a, int i) {
-    const int n = a.n;
+    const int n = a.ns;
     return Body{fld(a.st, 0, n, i), fld(a.st, 1, n, i), fld(a.st, 2, n, i),
                 fld(a.st, 3, n, i), fld(a.st, 4, n, i), fld(a.st, 5, n, i)};
 }
@@ -229,23 +253,25 @@ __device__ __forceinline__ void flag_wait(const uint32_t& f) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-// LDS: scenario tables in LDS; LTAB: the golden-march probe tables too (after the scenarios)
-template <bool LDS, bool LTAB>
-__global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
-    // dynamic LDS: n_scn scenario tables [+ n_scn probe tables] (sized at launch)
-    extern __shared__ __attribute__((aligned(16))) Scn s_scn[];
-    __shared__ __attribute__((aligned(16))) K1Shared sh;
+// LDS: scenario tables in LDS; LTAB: the golden-march probe tables too (after the scenarios);
+// GRP: grouped slot layout (a.lane_env) -- with LDS, the group is pure and stages only its own
+// scenario.  s_scn: the dynamic LDS (scenario tables [+ probe tables], sized at launch).
+template <bool LDS, bool LTAB, bool GRP>
+__device__ __forceinline__ void k1_body(const StepArgs& a, Scn* s_scn, K1Shared& sh, int wg) {
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    const int e0 = blockIdx.x * EPB;
-    const int i = e0 + lane;
-    const bool valid = i < a.n;
-    const int n = a.n;
+    const int e0 = wg * EPB;
+    const int i = e0 + lane;                     // slot: internal arrays, reset cache
+    const int ie = GRP ? a.lane_env[i] : i;      // env: caller's buffers, scenario map, spawn RNG
+    const bool valid = GRP ? ie >= 0 : i < a.n;
+    const int n = a.ns;
     const bool auto_reset = a.cfg.auto_reset != 0;
     STAMP(0);
-    const Scn* scns = stage_scenarios<LDS, K1_THREADS>(a, s_scn);
-    const BtHot* hots = LTAB ? stage_hot<K1_THREADS>(a, reinterpret_cast<BtHot*>(s_scn + a.n_scn)) : nullptr;
-    if (wave == 0) sh.scn[lane] = (valid && a.env_scn && a.n_scn > 1) ? a.env_scn[i] : 0;
+    const int s0 = (GRP && LDS) ? a.wg_scn[wg] : 0;
+    const int ncopy = (GRP && LDS) ? 1 : a.n_scn;
+    const Scn* scns = stage_scenarios<LDS, K1_THREADS>(a, s_scn, s0, ncopy);
+    const BtHot* hots = LTAB ? stage_hot<K1_THREADS>(a, reinterpret_cast<BtHot*>(s_scn + ncopy), s0, ncopy) : nullptr;
+    if (wave == 0) sh.scn[lane] = (valid && a.env_scn && a.n_scn > 1) ? a.env_scn[ie] : s0;
     if (threadIdx.x == 0) {
         sh.f_done = 0u;
         sh.f_ca = 0u;
@@ -256,7 +282,7 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
     __syncthreads();
     STAMP(1);
     const Scn& S = scns[sh.scn[lane]];
-    float* const trow = a.tobs ? a.tobs + (size_t)i * D2D_OBS_DIM : nullptr;
+    float* const trow = a.tobs ? a.tobs + (size_t)ie * D2D_OBS_DIM : nullptr;
     float* const orow = &sh.u.p.obs[lane * D2D_OBS_DIM];
 
     // W0 results kept for the epilogue
@@ -288,7 +314,7 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
             t = fld(a.ist, D2D_I_T, n, i);
             flags = (uint32_t)fld(a.ist, D2D_I_FLAGS, n, i);
             // thrust in float32 exactly as SB3's float32 action hits drone_2d_env.py:400-401
-            const float2 act = reinterpret_cast<const float2*>(a.act)[i];
+            const float2 act = reinterpret_cast<const float2*>(a.act)[ie];
             const float fs = (float)a.cfg.force_scale;
             const float lf = __fmul_rn(__fadd_rn(act.x / 2.0f, 0.5f), fs);
             const float rf = __fmul_rn(__fadd_rn(act.y / 2.0f, 0.5f), fs);
@@ -411,9 +437,9 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
                     for (int k = 0; k < 19; ++k) row[k] = c[k];
                 } else {
                     const uint32_t ep = sh.ep[lane];
-                    const Scn& SN = scns[next_scenario(a, i, ep)];
+                    const Scn& SN = scns[next_scenario(a, ie, ep)];
                     double sp[7], so[19];
-                    spawn_state(a, SN, i, ep, sp);
+                    spawn_state(a, SN, ie, ep, sp);
                     sensor_obs(a.cfg, SN, Body{sp[0], sp[1], sp[2], 0.0, 0.0, 0.0}, so);
 #pragma unroll
                     for (int k = 0; k < 19; ++k) row[k] = (float)so[k];
@@ -539,10 +565,10 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
         if (valid && done && auto_reset && !(D2D_ABL & 8)) {
             // the next episode: spawn state, reset observation (cached or computed), new state
             const uint32_t ep = sh.ep[lane];
-            const int nscn = next_scenario(a, i, ep);
+            const int nscn = next_scenario(a, ie, ep);
             const Scn& SN = scns[nscn];
             double sp[7];
-            spawn_state(a, SN, i, ep, sp);
+            spawn_state(a, SN, ie, ep, sp);
             uint32_t rfl = 0;
             if (cv) {
                 const float* c = a.rc_obs + (size_t)i * D2D_OBS_DIM + 19;
@@ -564,7 +590,7 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
             fld(a.ist, D2D_I_T, n, i) = 0;
             fld(a.ist, D2D_I_FLAGS, n, i) = (int32_t)rfl;
             fld(a.ist, D2D_I_EPISODE, n, i) = (int32_t)(ep + 1u);
-            if (a.cfg.scn_pool && a.env_scn) a.env_scn[i] = nscn;
+            if (a.cfg.scn_pool && a.env_scn) a.env_scn[ie] = nscn;
         }
         STAMP(4);
         flag_wait(sh.f_gs);
@@ -579,9 +605,16 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
     STAMP(3);
 
     // ---------------------------------------------------------------- epilogue
-    // obs tile: rows [e0, e0+rows) are one contiguous span of global memory
-    {
-        const int rows = min(EPB, n - e0);
+    // obs tile: rows [e0, e0+rows) are one contiguous span of global memory (grouped: one
+    // contiguous 108-byte row per env)
+    if (GRP && !(D2D_ABLATE & 32)) {
+        for (int k = threadIdx.x; k < EPB * D2D_OBS_DIM; k += K1_THREADS) {
+            const int r = k / D2D_OBS_DIM;
+            const int e = a.lane_env[e0 + r];
+            if (e >= 0) a.obs[(size_t)e * D2D_OBS_DIM + (k - r * D2D_OBS_DIM)] = sh.u.p.obs[k];
+        }
+    } else {
+        const int rows = max(0, min(EPB, a.n - e0));  // (D2D_ABLATE & 32: timing-only slot-order rows)
         const int words = rows * D2D_OBS_DIM;
         float* dst = a.obs + (size_t)e0 * D2D_OBS_DIM;
         for (int k = threadIdx.x; k < words; k += K1_THREADS) dst[k] = sh.u.p.obs[k];
@@ -599,11 +632,12 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
             trunc = true;
             term = false;
         }
-        a.rew[i] = (float)reward;
-        a.term[i] = (uint8_t)term;
-        a.trunc[i] = (uint8_t)trunc;
+        const int io = (D2D_ABLATE & 64) ? min(i, a.n - 1) : ie;  // (64: timing-only slot order)
+        a.rew[io] = (float)reward;
+        a.term[io] = (uint8_t)term;
+        a.trunc[io] = (uint8_t)trunc;
         if (a.info) {
-            float* r = a.info + (size_t)i * D2D_INFO_DIM;
+            float* r = a.info + (size_t)ie * D2D_INFO_DIM;
             r[D2D_INFO_CA] = (float)RV.cal;
             r[D2D_INFO_PA] = (float)sh.u.p.post[1][lane];
             r[D2D_INFO_PP] = (float)sh.u.p.post[2][lane];
@@ -640,25 +674,46 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
     STAMP(6);
 }
 
+template <bool LDS, bool LTAB>
+__global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
+    extern __shared__ __attribute__((aligned(16))) Scn s_scn[];
+    __shared__ __attribute__((aligned(16))) K1Shared sh;
+    k1_body<LDS, LTAB, false>(a, s_scn, sh, blockIdx.x);
+}
+// grouped slot layout: a pure group stages its scenario and probe table in LDS; a group that
+// straddles scenarios (at most n_scn - 1 of them: the layout has no padding between scenarios)
+// reads the tables through L1/L2
+__global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_grouped_kernel(StepArgs a) {
+    extern __shared__ __attribute__((aligned(16))) Scn s_scn[];
+    __shared__ __attribute__((aligned(16))) K1Shared sh;
+    const int wg = xcd_group(blockIdx.x, gridDim.x);
+    if (a.brt && a.wg_scn[wg] >= 0)
+        k1_body<true, true, true>(a, s_scn, sh, wg);
+    else
+        k1_body<false, false, true>(a, s_scn, sh, wg);
+}
+
 // ------------------------------------------------------------------------------------------ K2
 template <bool LDS>
 __global__ __launch_bounds__(BLOCK) void d2d_reset_kernel(StepArgs a) {
     extern __shared__ __attribute__((aligned(16))) Scn s_scn[];
     const Scn* scns = stage_scenarios<LDS, BLOCK>(a, s_scn);
     __syncthreads();
-    const int i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= a.n) return;
-    if (a.mask && !a.mask[i]) return;
-    const int n = a.n;
-    int si = (a.env_scn && a.n_scn > 1) ? a.env_scn[i] : 0;
+    const int i = blockIdx.x * BLOCK + threadIdx.x;  // slot
+    if (i >= a.ns) return;
+    const int ie = a.lane_env ? a.lane_env[i] : i;  // env
+    if (ie < 0) return;
+    if (a.mask && !a.mask[ie]) return;
+    const int n = a.ns;
+    int si = (a.env_scn && a.n_scn > 1) ? a.env_scn[ie] : 0;
     if (a.cfg.scn_pool && a.n_scn > 1) {
-        si = pool_pick(a.seed, (uint32_t)a.cfg.env_id_base + (uint32_t)i, (uint32_t)fld(a.ist, D2D_I_EPISODE, n, i),
+        si = pool_pick(a.seed, (uint32_t)a.cfg.env_id_base + (uint32_t)ie, (uint32_t)fld(a.ist, D2D_I_EPISODE, n, i),
                        a.n_scn);
-        a.env_scn[i] = si;
+        a.env_scn[ie] = si;
     }
     const Scn& s = scns[si];
     double sp[7];
-    spawn_state(a, s, i, (uint32_t)fld(a.ist, D2D_I_EPISODE, n, i), sp);
+    spawn_state(a, s, ie, (uint32_t)fld(a.ist, D2D_I_EPISODE, n, i), sp);
     const double th = sp[2];
     const double bodies[18] = {sp[0], sp[1], th, 0.0, 0.0, 0.0, sp[3], sp[4], th, 0.0, 0.0, 0.0,
                                sp[5], sp[6], th, 0.0, 0.0, 0.0};
@@ -676,8 +731,20 @@ __global__ __launch_bounds__(BLOCK) void d2d_reset_kernel(StepArgs a) {
     fld(a.ist, D2D_I_EPISODE, n, i) += 1;
     if (a.obs) {
 #pragma unroll
-        for (int k = 0; k < D2D_OBS_DIM; ++k) a.obs[(size_t)i * D2D_OBS_DIM + k] = (float)obs[k];
+        for (int k = 0; k < D2D_OBS_DIM; ++k) a.obs[(size_t)ie * D2D_OBS_DIM + k] = (float)obs[k];
     }
+}
+
+// ------------------------------------------------------------------------------ slot permutation
+// dst[f][dslot(e)] = src[f][sslot(e)] for every env e and field f < nf (a null map: slot == env):
+// get_state / set_state through the grouped slot layout, and re-layouts in d2d_set_scenarios
+template <typename T>
+__global__ __launch_bounds__(BLOCK) void d2d_permute_kernel(const T* src, int sstride, const int32_t* sslot, T* dst,
+                                                            int dstride, const int32_t* dslot, int nf, int n) {
+    const int e = blockIdx.x * BLOCK + threadIdx.x;
+    if (e >= n) return;
+    const int si = sslot ? sslot[e] : e, di = dslot ? dslot[e] : e;
+    for (int f = 0; f < nf; ++f) dst[(size_t)f * dstride + di] = src[(size_t)f * sstride + si];
 }
 
 // ------------------------------------------------------------------------------ cache fill (K4)
@@ -692,9 +759,10 @@ __global__ __launch_bounds__(BLOCK) void d2d_fill_kernel(StepArgs a) {
     __shared__ int list[BLOCK];
     __shared__ int cnt[BLOCK / 64];
     const Scn* scns = stage_scenarios<LDS, BLOCK>(a, s_scn);
-    const int n = a.n;
-    const int i0 = blockIdx.x * BLOCK + threadIdx.x;
-    const bool need = (i0 < n) && (a.rc_tag[i0] != fld(a.ist, D2D_I_EPISODE, n, i0));
+    const int n = a.ns;
+    const int i0 = blockIdx.x * BLOCK + threadIdx.x;  // slot
+    const bool need = (i0 < n) && (!a.lane_env || a.lane_env[i0] >= 0) &&
+                      (a.rc_tag[i0] != fld(a.ist, D2D_I_EPISODE, n, i0));
     int i = i0;
     if (!D2D_FILL_COMPACT) {
         __syncthreads();
@@ -716,10 +784,11 @@ __global__ __launch_bounds__(BLOCK) void d2d_fill_kernel(StepArgs a) {
     i = list[threadIdx.x];
     }
     const int32_t ep = fld(a.ist, D2D_I_EPISODE, n, i);
-    const int si = next_scenario(a, i, (uint32_t)ep);
+    const int ie = a.lane_env ? a.lane_env[i] : i;  // env of slot i
+    const int si = next_scenario(a, ie, (uint32_t)ep);
     const Scn& S = scns[si];
     double sp[7], so[19], o[8];
-    spawn_state(a, S, i, (uint32_t)ep, sp);
+    spawn_state(a, S, ie, (uint32_t)ep, sp);
     uint32_t f = 0;
     sensor_obs(a.cfg, S, Body{sp[0], sp[1], sp[2], 0.0, 0.0, 0.0}, so);
     path_obs(a.cfg, S, brtab(a, si), sp[0], sp[1], sp[2], f, o);

@@ -67,6 +67,23 @@ def test_vs_oracle_teacher_forced(d2, scn):
     venv.close()
 
 
+def test_grouped_lane_map_irregular(d2):
+    """Static mixed env -> scenario map with ragged groups: the step kernel's scenario-grouped lane
+    map (partial groups padded, a scenario with 3 envs, one with none, n not a multiple of 64)."""
+    rng = np.random.default_rng(7)
+    n = 1001
+    es = rng.choice(7, size=n, p=[0.3, 0.25, 0.2, 0.15, 0.1, 0.0, 0.0]).astype(np.int32)
+    es[[5, 500, 1000]] = 5  # three envs of scenario 5, none of scenario 6
+    venv, orc = make_pair(d2, n, SCENARIOS, seed=3, kwargs=_cfgkw(), env_scenario=es)
+    dones = 0
+    for t in range(120):
+        act = np.clip(rng.normal(0.0, 0.6, (n, 2)), -1, 1).astype(np.float32)
+        compare_step(venv, orc, act)
+        dones += int(orc.term.sum())
+    assert dones > 20
+    venv.close()
+
+
 def test_reset_cache_invalidation(d2):
     """The auto-reset observation cache (filled ahead of time by the fill kernel) must be dropped
     by a full reset with a new seed and by set_state (episode counters may change)."""

@@ -1,0 +1,24 @@
+#!/bin/bash
+# bench.py on every single-GPU BASELINE.json config (GPU box); one JSON line per config into
+# gpurun_out/configs_TAG.jsonl.  Each run has its own time limit; any failure ends the script.
+# Usage: bash tools/configs.sh TAG
+set -u
+TAG=${1:-r01}
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/configs_$TAG.jsonl
+: > "$OUT"
+run() {  # run <label> <bench args...>
+  local label=$1; shift
+  echo "=== $label ($(date +%T))"
+  timeout -k 10 300 python3 "$R/bench.py" --no-cpu-baseline "$@" > "$R/gpurun_out/cfg_$label.log" 2>&1
+  local rc=$?
+  [ $rc -eq 0 ] || { echo "STOP $label rc=$rc"; tail -n 5 "$R/gpurun_out/cfg_$label.log"; exit $rc; }
+  grep '^{' "$R/gpurun_out/cfg_$label.log" | sed "s/^{/{\"label\": \"$label\", /" >> "$OUT"
+  tail -n 1 "$OUT" | cut -c1-160
+}
+run cfg1_free_4096 --scenario corridor_free --envs 4096 --steps 1000 --warmup 50
+run cfg2_corridor_65536 --scenario corridor --steps 1000 --warmup 50
+run cfg3_large_65536 --scenario large --steps 1000 --warmup 50
+run cfg3_S_corridor_65536 --scenario S_corridor --steps 1000 --warmup 50
+run cfg4_mixed_65536 --scenario mixed --steps 1000 --warmup 50
+run cfg2_free_65536 --scenario corridor_free --steps 1000 --warmup 50

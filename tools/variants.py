@@ -39,9 +39,16 @@ def build(specs):
 
 
 def time_variant(d2, torch, lib, n, scenario, steps=200, warmup=30, auto_reset=True):
+    import numpy as np
+
     from drone2d_amd.config import ENV_TRAIN_CONFIG
 
-    venv = d2.Drone2dVecEnv(n, seed=1, with_info=False, native_lib=lib, auto_reset=auto_reset,
+    es = None
+    if scenario.startswith("mixed"):
+        # mixed: env i -> scenario i mod 7; mixedblock: (i // 64) mod 7 (homogeneous 64-env blocks)
+        es = (np.arange(n) // (64 if scenario == "mixedblock" else 1)) % 7
+        from bench import MIXED as scenario
+    venv = d2.Drone2dVecEnv(n, seed=1, with_info=False, native_lib=lib, auto_reset=auto_reset, env_scenario=es,
                             **dict(ENV_TRAIN_CONFIG, scenario=scenario))
     venv.reset()
     acts = [torch.rand(n, 2, device=venv.device) * 2 - 1 for _ in range(8)]
