@@ -494,6 +494,19 @@ int32_t d2d_episode_stats(d2d_t* h, double* out_dev, int32_t clear, void* stream
     return D2D_OK;
 }
 
+int32_t d2d_group_layout(int32_t n, const int32_t* env_scn, int32_t n_scn, int32_t* slot_env, int32_t* group_scn) {
+    if (n <= 0 || n_scn <= 0 || !env_scn || !slot_env || !group_scn)
+        return fail(D2D_E_ARG, "d2d_group_layout: n, n_scn must be > 0 and pointers non-null"), -1;
+    for (int i = 0; i < n; ++i)
+        if (env_scn[i] < 0 || env_scn[i] >= n_scn)
+            return fail(D2D_E_ARG, "d2d_group_layout: env scenario index out of range"), -1;
+    std::vector<int32_t> lanes, ws;
+    make_groups(n, env_scn, n_scn, lanes, ws);
+    std::copy(lanes.begin(), lanes.end(), slot_env);
+    std::copy(ws.begin(), ws.end(), group_scn);
+    return (int32_t)ws.size();
+}
+
 int32_t d2d_selftest(int32_t which, int64_t n, uint64_t seed, uint64_t* mismatches) {
     if (!mismatches || n < 0 || which < 0 || which > 2) return fail(D2D_E_ARG, "d2d_selftest: bad arguments");
     unsigned long long* bad = nullptr;

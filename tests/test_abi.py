@@ -92,6 +92,57 @@ def test_errors_without_device(hip_lib):
     assert hip_lib.d2d_n_envs(None) == -1
 
 
+@pytest.mark.parametrize("case", ["mod7", "ragged", "single", "tiny"])
+def test_group_layout_properties(hip_lib, case):
+    """The grouped slot layout of d2d_set_scenarios (host code): a bijection env <-> slot with no
+    padding between scenarios (ceil(n/64) groups), every pure group's envs of its scenario, at most
+    n_scn - 1 straddling groups, groups numbered by first env id, (scenario, id) order inside a group."""
+    import numpy as np
+
+    rng = np.random.default_rng(11)
+    if case == "mod7":
+        n, k = 65536, 7
+        es = np.arange(n) % k
+    elif case == "ragged":
+        n, k = 1001, 7
+        es = rng.choice(k, size=n, p=[0.3, 0.25, 0.2, 0.15, 0.1, 0.0, 0.0])
+        es[[5, 500, 1000]] = 5
+    elif case == "single":
+        n, k = 300, 3
+        es = np.full(n, 2)
+    else:
+        n, k = 5, 4
+        es = np.array([3, 0, 3, 1, 0])
+    es = np.ascontiguousarray(es, dtype=np.int32)
+    ng = (n + 63) // 64
+    slot_env = np.zeros(ng * 64, np.int32)
+    group_scn = np.zeros(ng, np.int32)
+    p = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+    assert hip_lib.d2d_group_layout(n, p(es), k, p(slot_env), p(group_scn)) == ng
+    valid = slot_env[slot_env >= 0]
+    assert sorted(valid.tolist()) == list(range(n))              # bijection
+    assert (slot_env >= 0).sum() == n and (g_pad := (slot_env < 0).sum()) == ng * 64 - n, g_pad
+    g = slot_env.reshape(ng, 64)
+    straddle = 0
+    for j in range(ng):
+        e = g[j][g[j] >= 0]
+        if group_scn[j] >= 0:
+            assert (es[e] == group_scn[j]).all()
+        else:
+            straddle += 1
+            assert len(set(es[e].tolist())) > 1
+    assert straddle <= k - 1
+    firsts = g[:, 0]
+    assert (np.diff(firsts) > 0).all()                           # numbered by first env id
+    for j in range(ng):                                          # (scenario, id) order in a group
+        e = g[j][g[j] >= 0]
+        key = [(int(es[x]), int(x)) for x in e]
+        assert key == sorted(key)
+    bad = np.array([0, 9], np.int32)
+    assert hip_lib.d2d_group_layout(2, p(bad), 3, p(slot_env), p(group_scn)) == -1
+    assert b"out of range" in hip_lib.d2d_last_error()
+
+
 def test_philox_known_answers(oracle_mod):
     """Random123 Philox4x32-10 KAT vectors (the spawn RNG spec shared by kernel and oracle)."""
     assert oracle_mod.philox([0, 0, 0, 0], [0, 0]) == [0x6627E8D5, 0xE169C58D, 0xBC57AC4C, 0x9B00DBD8]
