@@ -104,6 +104,13 @@ struct StepArgs {
 #define D2D_ABL 0        // diagnostic builds only: bit r skips role r's compute, bit 4 = perfect
                          // reset cache (no fills, every entry taken as ready): timing ablations
 #endif
+#ifndef D2D_PREFETCH
+#define D2D_PREFETCH 2   // K1 issues its state loads before the staging barrier (bit 0: W0 all, bit 2: W0 without
+                         // the joint impulses, bit 1: the frame for W1/W2)
+#endif
+#ifndef D2D_GLDS
+#define D2D_GLDS 1       // K1 stages its scenario (+ probe table) with LDS-DMA
+#endif
 #ifndef D2D_SPLIT
 #define D2D_SPLIT 0      // 1: W3 re-checks the second half of W2's golden-march table
 #endif
@@ -158,6 +165,21 @@ __device__ __forceinline__ const BtHot* stage_hot(const StepArgs& a, BtHot* lds,
     }
     return lds - first;
 }
+// Contiguous global -> LDS copy with LDS-DMA (global_load_lds_dwordx4: no VGPRs, asynchronous until
+// the next vmcnt wait; the __syncthreads() that follows drains it).  Each wave instruction moves
+// 1 KB (64 lanes x 16 B, LDS written at the wave-uniform base + lane x 16); bytes % 16 == 0.
+template <int NWAVES>
+__device__ __forceinline__ void glds_copy(void* lds_dst, const void* gsrc, int bytes) {
+    using LP = __attribute__((address_space(3))) void;
+    using GP = __attribute__((address_space(1))) void;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    for (int c = wave; c * 1024 < bytes; c += NWAVES) {
+        const int off = c * 1024 + lane * 16;
+        if (off < bytes)
+            __builtin_amdgcn_global_load_lds((GP*)((const char*)gsrc + off), (LP*)((char*)lds_dst + c * 1024), 16, 0, 0);
+    }
+}
+
 // Workgroup renumbering for the grouped lane map: blocks b and b + 8 share an XCD (and its L2)
 // when the grid is dealt round-robin over the 8 XCDs, so consecutive group numbers -- groups whose
 // envs share cache lines -- go to blocks on one XCD.  Placement only affects speed.
@@ -269,9 +291,48 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, Scn* s_scn, K1Shared&
     STAMP(0);
     const int s0 = (GRP && LDS) ? a.wg_scn[wg] : 0;
     const int ncopy = (GRP && LDS) ? 1 : a.n_scn;
-    const Scn* scns = stage_scenarios<LDS, K1_THREADS>(a, s_scn, s0, ncopy);
-    const BtHot* hots = LTAB ? stage_hot<K1_THREADS>(a, reinterpret_cast<BtHot*>(s_scn + ncopy), s0, ncopy) : nullptr;
+    const Scn* scns;
+    const BtHot* hots = nullptr;
+    if (D2D_GLDS && LDS && (ncopy == 1 || !LTAB)) {
+        // one scenario (+ its probe table) or scenarios only: contiguous sources, LDS-DMA
+        glds_copy<K1_THREADS / 64>(s_scn, a.scn + s0, (int)sizeof(Scn) * ncopy);
+        if (LTAB) glds_copy<K1_THREADS / 64>(s_scn + 1, &a.brt[s0].hot, (int)sizeof(BtHot));
+        scns = s_scn - s0;
+        if (LTAB) hots = reinterpret_cast<const BtHot*>(s_scn + 1) - s0;
+    } else {
+        scns = stage_scenarios<LDS, K1_THREADS>(a, s_scn, s0, ncopy);
+        if (LTAB) hots = stage_hot<K1_THREADS>(a, reinterpret_cast<BtHot*>(s_scn + ncopy), s0, ncopy);
+    }
     if (wave == 0) sh.scn[lane] = (valid && a.env_scn && a.n_scn > 1) ? a.env_scn[ie] : s0;
+    // state loads issued before the staging barrier, so their HBM latency overlaps the staging:
+    // W0 the whole state + action, the other roles the frame
+    Body PB[3]{};
+    double PJ[12];
+    int Pt = 0;
+    uint32_t Pfl = 0;
+    float2 Pact = make_float2(0.0f, 0.0f);
+    if (D2D_PREFETCH && valid) {
+        if (wave == 0 && (D2D_PREFETCH & 5)) {
+#pragma unroll
+            for (int b = 0; b < 3; ++b) {
+                PB[b].px = fld(a.st, 6 * b + 0, n, i);
+                PB[b].py = fld(a.st, 6 * b + 1, n, i);
+                PB[b].a = fld(a.st, 6 * b + 2, n, i);
+                PB[b].vx = fld(a.st, 6 * b + 3, n, i);
+                PB[b].vy = fld(a.st, 6 * b + 4, n, i);
+                PB[b].w = fld(a.st, 6 * b + 5, n, i);
+            }
+            if (D2D_PREFETCH & 1) {
+#pragma unroll
+                for (int k = 0; k < 12; ++k) PJ[k] = fld(a.st, D2D_S_J + k, n, i);
+            }
+            Pt = fld(a.ist, D2D_I_T, n, i);
+            Pfl = (uint32_t)fld(a.ist, D2D_I_FLAGS, n, i);
+            Pact = reinterpret_cast<const float2*>(a.act)[ie];
+        } else if (wave != 0 && (D2D_PREFETCH & 2)) {
+            PB[0] = load_frame(a, i);
+        }
+    }
     if (threadIdx.x == 0) {
         sh.f_done = 0u;
         sh.f_ca = 0u;
@@ -300,21 +361,30 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, Scn* s_scn, K1Shared&
         Body B[3];
         double j[12], cs[3], sn[3], fx = 0.0, fy = 0.0, tq = 0.0;
         if (valid && !(D2D_ABL & 1)) {
+            if (D2D_PREFETCH & 5) {
 #pragma unroll
-            for (int b = 0; b < 3; ++b) {
-                B[b].px = fld(a.st, 6 * b + 0, n, i);
-                B[b].py = fld(a.st, 6 * b + 1, n, i);
-                B[b].a = fld(a.st, 6 * b + 2, n, i);
-                B[b].vx = fld(a.st, 6 * b + 3, n, i);
-                B[b].vy = fld(a.st, 6 * b + 4, n, i);
-                B[b].w = fld(a.st, 6 * b + 5, n, i);
+                for (int b = 0; b < 3; ++b) B[b] = PB[b];
+#pragma unroll
+                for (int k = 0; k < 12; ++k) j[k] = (D2D_PREFETCH & 1) ? PJ[k] : fld(a.st, D2D_S_J + k, n, i);
+                t = Pt;
+                flags = Pfl;
+            } else {
+#pragma unroll
+                for (int b = 0; b < 3; ++b) {
+                    B[b].px = fld(a.st, 6 * b + 0, n, i);
+                    B[b].py = fld(a.st, 6 * b + 1, n, i);
+                    B[b].a = fld(a.st, 6 * b + 2, n, i);
+                    B[b].vx = fld(a.st, 6 * b + 3, n, i);
+                    B[b].vy = fld(a.st, 6 * b + 4, n, i);
+                    B[b].w = fld(a.st, 6 * b + 5, n, i);
+                }
+#pragma unroll
+                for (int k = 0; k < 12; ++k) j[k] = fld(a.st, D2D_S_J + k, n, i);
+                t = fld(a.ist, D2D_I_T, n, i);
+                flags = (uint32_t)fld(a.ist, D2D_I_FLAGS, n, i);
             }
-#pragma unroll
-            for (int k = 0; k < 12; ++k) j[k] = fld(a.st, D2D_S_J + k, n, i);
-            t = fld(a.ist, D2D_I_T, n, i);
-            flags = (uint32_t)fld(a.ist, D2D_I_FLAGS, n, i);
             // thrust in float32 exactly as SB3's float32 action hits drone_2d_env.py:400-401
-            const float2 act = reinterpret_cast<const float2*>(a.act)[ie];
+            const float2 act = (D2D_PREFETCH & 5) ? Pact : reinterpret_cast<const float2*>(a.act)[ie];
             const float fs = (float)a.cfg.force_scale;
             const float lf = __fmul_rn(__fadd_rn(act.x / 2.0f, 0.5f), fs);
             const float rf = __fmul_rn(__fadd_rn(act.y / 2.0f, 0.5f), fs);
@@ -404,7 +474,7 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, Scn* s_scn, K1Shared&
         float row[19];
         bool need = false;
         if (valid && !(D2D_ABL & 2)) {
-            Body F = load_frame(a, i);
+            Body F = (D2D_PREFETCH & 2) ? PB[0] : load_frame(a, i);
             advance_position(F);
             double so[19];
             sensor_pos(a.cfg, S, F.px, F.py, F.a, so);
@@ -466,7 +536,7 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, Scn* s_scn, K1Shared&
         double po[8];
         Body F{};
         if (valid && !(D2D_ABL & 4)) {
-            F = load_frame(a, i);
+            F = (D2D_PREFETCH & 2) ? PB[0] : load_frame(a, i);
             advance_position(F);
             uint32_t f = (uint32_t)fld(a.ist, D2D_I_FLAGS, n, i);
             const BrTab* T = brtab(a, sh.scn[lane]);
