@@ -584,8 +584,9 @@ __device__ __forceinline__ BtLane bt_start(const BrTab& T, const BtHot* hot, dou
     L.fc = L.kind ? f1 : f0;
     return L;
 }
-// the window before step k >= 3 when steps 1 .. k-1 followed the table: fulc, nfc, xf are the probes
-// of steps k-3, k-2, k-1 (probe indices k-2, k-1, k)
+// the window before step k >= 4 when steps 1 .. k-1 followed the table: fulc, nfc, xf are the probes
+// of steps k-3, k-2, k-1 (probe indices k-2, k-1, k).  (Before step 3 of a kind-0 march fulc is
+// still the initial point, index 0: the snapshot's j_* indices hold the general case.)
 template <bool LT>
 __device__ __forceinline__ void bt_window(const BtHot* hot, BtLane& L, int k, double px, double py) {
     L.fa = bt_dist<LT>(hot, L.kind, k - 2, px, py);
@@ -653,7 +654,7 @@ __device__ __forceinline__ double closest_u_tab(const Scn& s, const BrTab& T, co
 }
 // split point of the two-wave re-check: the first wave checks steps [1, bt_split), the second
 // [bt_split, len) (from its own window, bt_window)
-__device__ __forceinline__ int bt_split(const BrTab& T) { return max(3, (T.len[0] + 3) / 2); }
+__device__ __forceinline__ int bt_split(const BrTab& T) { return max(4, (T.len[0] + 3) / 2); }
 
 // ------------------------------------------------------------------------------ bodies / physics
 // One cpSpaceStep(1/60) of the Drone.py body/joint configuration, split in

@@ -92,7 +92,8 @@ StepArgs make_args(const d2d_t* h) {
 // K4: fill every cache entry that does not belong to its env's current episode, ordered on `stream`
 hipError_t rc_fill(d2d_t* h, hipStream_t stream) {
     StepArgs a = make_args(h);
-    const dim3 grid((h->ns + BLOCK - 1) / BLOCK);
+    const int spb = (D2D_FILL_SPLIT && D2D_FILL_COMPACT) ? FILL_SPB : BLOCK;
+    const dim3 grid((h->ns + spb - 1) / spb);
     if (sizeof(d2d::Scn) * (size_t)h->n_scn <= K2_LDS_BUDGET)
         hipLaunchKernelGGL(d2d_fill_kernel<true>, grid, dim3(BLOCK), sizeof(d2d::Scn) * h->n_scn, stream, a);
     else

@@ -22,7 +22,8 @@
 // even with 7 scenario tables).
 //
 // K2 d2d_reset_kernel: masked reset, one lane per env.  K3 d2d_stats_kernel: fixed-order reduction.
-// K4 d2d_fill_kernel: fills the auto-reset observation cache (one lane per env).
+// K4 d2d_fill_kernel: fills the auto-reset observation cache (the envs that need it compacted,
+// four waves per 64 of them: fill_split).
 #pragma once
 #include "d2d_device.h"
 
@@ -116,6 +117,10 @@ struct StepArgs {
 #endif
 #ifndef D2D_FILL_COMPACT
 #define D2D_FILL_COMPACT 1  // K4 compacts the envs that need a fill into the leading lanes
+#endif
+constexpr int FILL_SPB = 128;  // K4 split path: slots per block (~26 fills per 16 steps at 65 536 envs)
+#ifndef D2D_FILL_SPLIT
+#define D2D_FILL_SPLIT 1  // K4: the block's four waves share each round of 64 envs (fill_split)
 #endif
 #ifndef D2D_FILL_PERIOD
 #define D2D_FILL_PERIOD 16  // K4 after every this many steps (0: never; every reset synchronous)
@@ -818,6 +823,77 @@ __global__ __launch_bounds__(BLOCK) void d2d_permute_kernel(const T* src, int ss
 }
 
 // ------------------------------------------------------------------------------ cache fill (K4)
+// K4 with the four waves of a block working on the same 64 compacted envs at a time (K4 runs
+// alone on a mostly idle GPU, so its duration is one env's latency chain): wave 0 the spawn-state
+// sensor part, waves 1-3 one third each of the golden-march re-check, then wave 1 the Brent
+// continuation and the path part.  Same operations as the one-lane-per-env path.
+__device__ __forceinline__ void fill_split(const StepArgs& a, const Scn* scns, const int* list, int total) {
+    __shared__ int devp[3][64];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int n = a.ns;
+    for (int r0 = 0; r0 < total; r0 += 64) {
+        const bool act = r0 + lane < total;
+        const int i = list[act ? r0 + lane : r0];  // inactive lanes repeat the round's first env
+        const int32_t ep = fld(a.ist, D2D_I_EPISODE, n, i);
+        const int ie = a.lane_env ? a.lane_env[i] : i;
+        const int si = next_scenario(a, ie, (uint32_t)ep);
+        const Scn& S = scns[si];
+        const BrTab* T = brtab(a, si);
+        double sp[7];
+        spawn_state(a, S, ie, (uint32_t)ep, sp);
+        float* c = a.rc_obs + (size_t)i * D2D_OBS_DIM;
+        if (wave == 0) {
+            double so[19];
+            sensor_obs(a.cfg, S, Body{sp[0], sp[1], sp[2], 0.0, 0.0, 0.0}, so);
+            if (act) {
+#pragma unroll
+                for (int k = 0; k < 19; ++k) c[k] = (float)so[k];
+            }
+        } else if (T) {
+            const int w = wave - 1;
+            BtLane L = bt_start<false>(*T, &T->hot, sp[0], sp[1]);
+            // steps [1, b1), [b1, b2), [b2, BT_K)
+            const int third = (T->len[0] + 2) / 3;
+            const int b1 = 1 + third, b2 = 1 + 2 * third;
+            if (w == 0) {
+                bt_verify<false>(&T->hot, L, 1, b1, sp[0], sp[1]);
+            } else {
+                const int k0 = (w == 1) ? b1 : b2, k1 = (w == 1) ? b2 : BT_K;
+                if (k0 < min(k1, L.len)) {
+                    // the window before step k0 (table-following so far): the snapshot's probes
+                    const BtSnap& W = T->snap[L.kind][k0];
+                    L.fa = bt_dist<false>(&T->hot, L.kind, W.j_fulc, sp[0], sp[1]);
+                    L.fb = bt_dist<false>(&T->hot, L.kind, W.j_nfc, sp[0], sp[1]);
+                    L.fc = bt_dist<false>(&T->hot, L.kind, W.j_xf, sp[0], sp[1]);
+                    bt_verify<false>(&T->hot, L, k0, k1, sp[0], sp[1]);
+                }
+            }
+            devp[w][lane] = L.dev;
+        }
+        __syncthreads();
+        if (wave == 1) {
+            double o[8];
+            uint32_t f = 0;
+            if (T) {
+                const int kind = bt_start<false>(*T, &T->hot, sp[0], sp[1]).kind;
+                const int dev = min(devp[0][lane], min(devp[1][lane], devp[2][lane]));
+                int iu;
+                const double u = bt_finish<false>(S, *T, &T->hot, kind, dev, sp[0], sp[1], iu);
+                path_obs_u(a.cfg, S, sp[0], sp[1], sp[2], u, f, o, iu);
+            } else {
+                path_obs(a.cfg, S, nullptr, sp[0], sp[1], sp[2], f, o);
+            }
+            if (act) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) c[19 + k] = (float)o[k];
+                a.rc_rfl[i] = (int32_t)f;
+            }
+        }
+        __syncthreads();  // the sensor part is stored before the tag; devp is reused next round
+        if (wave == 1 && act) a.rc_tag[i] = ep;
+    }
+}
+
 // an env whose entry does not belong to its current episode computes the observation its next
 // auto-reset will return (test-mode spawn of the next episode's scenario).  Only the envs reset
 // since the last fill need it (~1/5 of them at fill period 16): each workgroup compacts its
@@ -830,10 +906,12 @@ __global__ __launch_bounds__(BLOCK) void d2d_fill_kernel(StepArgs a) {
     __shared__ int cnt[BLOCK / 64];
     const Scn* scns = stage_scenarios<LDS, BLOCK>(a, s_scn);
     const int n = a.ns;
-    const int i0 = blockIdx.x * BLOCK + threadIdx.x;  // slot
-    const bool need = (i0 < n) && (!a.lane_env || a.lane_env[i0] >= 0) &&
+    // slots per block: BLOCK, or FILL_SPB with the split path (about one 64-env round per block)
+    const int spb = (D2D_FILL_SPLIT && D2D_FILL_COMPACT) ? FILL_SPB : BLOCK;
+    const int i0 = blockIdx.x * spb + threadIdx.x;  // slot
+    const bool need = ((int)threadIdx.x < spb) && (i0 < n) && (!a.lane_env || a.lane_env[i0] >= 0) &&
                       (a.rc_tag[i0] != fld(a.ist, D2D_I_EPISODE, n, i0));
-    int i = i0;
+    int i = i0, total = 0;
     if (!D2D_FILL_COMPACT) {
         __syncthreads();
         if (!need) return;
@@ -842,7 +920,7 @@ __global__ __launch_bounds__(BLOCK) void d2d_fill_kernel(StepArgs a) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     if (lane == 0) cnt[wave] = __popcll(m);
     __syncthreads();
-    int off = 0, total = 0;
+    int off = 0;
 #pragma unroll
     for (int w = 0; w < BLOCK / 64; ++w) {
         off += (w < wave) ? cnt[w] : 0;
@@ -850,8 +928,16 @@ __global__ __launch_bounds__(BLOCK) void d2d_fill_kernel(StepArgs a) {
     }
     if (need) list[off + __popcll(m & ((1ull << lane) - 1ull))] = i0;
     __syncthreads();
-    if ((int)threadIdx.x >= total) return;
-    i = list[threadIdx.x];
+    if (D2D_FILL_SPLIT) {
+        if (total == 0) return;  // block-uniform
+    } else {
+        if ((int)threadIdx.x >= total) return;
+        i = list[threadIdx.x];
+    }
+    }
+    if (D2D_FILL_SPLIT && D2D_FILL_COMPACT) {
+        fill_split(a, scns, list, total);
+        return;
     }
     const int32_t ep = fld(a.ist, D2D_I_EPISODE, n, i);
     const int ie = a.lane_env ? a.lane_env[i] : i;  // env of slot i
