@@ -113,7 +113,7 @@ struct StepArgs {
 #define D2D_GLDS 1       // K1 stages its scenario (+ probe table) with LDS-DMA
 #endif
 #ifndef D2D_SPLIT
-#define D2D_SPLIT 0      // 1: W3 re-checks the second half of W2's golden-march table
+#define D2D_SPLIT 1      // W3 re-checks the second half of W2's golden-march table (0: W2 alone)
 #endif
 #ifndef D2D_FILL_COMPACT
 #define D2D_FILL_COMPACT 1  // K4 compacts the envs that need a fill into the leading lanes
