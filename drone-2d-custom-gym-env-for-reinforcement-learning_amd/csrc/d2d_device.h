@@ -224,6 +224,9 @@ __device__ __forceinline__ void spawn_draw(const Scn& s, uint64_t seed, uint32_t
 // u > us[k] (equal values give +0), padded +inf knots give +inf (u finite) or NaN (u = +inf, sign
 // clear), and u = -inf gives +inf -- the Python loop's counts in every case; NaN u maps to
 // n_wps - 1 as the loop does.  No compare masks, so the 15 knot tests issue back to back.
+#ifndef D2D_SENSE_MINAXIS
+#define D2D_SENSE_MINAXIS 1  // circle distances / frame contact with min / max instead of selects
+#endif
 #ifndef D2D_KNOT_CMP
 #define D2D_KNOT_CMP 1   // 1: compares (measured faster in the full kernel), 0: sign bits (faster alone)
 #endif
@@ -745,7 +748,12 @@ __device__ __forceinline__ bool frame_hits(const Scn& s, const Body& F, double c
         const double dx = s.cx[k] - F.px, dy = s.cy[k] - F.py;
         const double lx = dx * cs + dy * sn;
         const double ly = -dx * sn + dy * cs;
+#if D2D_SENSE_MINAXIS
+        // clamp by max / min: equal to clipd for every input (a NaN lx or ly gives a NaN e: no hit)
+        const double ex = lx - fmin(fmax(lx, -FRAME_HX), FRAME_HX), ey = ly - fmin(fmax(ly, -FRAME_HY), FRAME_HY);
+#else
         const double ex = lx - clipd(lx, -FRAME_HX, FRAME_HX), ey = ly - clipd(ly, -FRAME_HY, FRAME_HY);
+#endif
         const double r = s.cr[k];
         hit |= (ex * ex + ey * ey <= r * r);
     }
@@ -994,6 +1002,13 @@ __device__ __forceinline__ void sensor_pos(const d2d_cfg& cfg, const Scn& s, dou
         const double cx = s.cx[i], cy = s.cy[i];
         const double ax = (50.0 + x) - cx, bxx = (-50.0 + x) - cx;
         const double ay = (-5.0 + y) - cy, byy = (5.0 + y) - cy;
+#if D2D_SENSE_MINAXIS
+        // min over the vertices (±50, ±5) of RN(dx² + dy²) == RN(min dx² + min dy²): squaring and
+        // rounding are monotone, so the x and y parts minimise independently (bit-identical to
+        // the four sums; NaN coordinates give NaN either way)
+        const double mx = fmin(fabs(ax), fabs(bxx)), my = fmin(fabs(ay), fabs(byy));
+        const double q = mx * mx + my * my;
+#else
         const double ax2 = ax * ax, bx2 = bxx * bxx, ay2 = ay * ay, by2 = byy * byy;
         // vertex order (50,-5), (50,5), (-50,5), (-50,-5)
         const double q0 = ax2 + ay2, q1 = ax2 + by2, q2 = bx2 + by2, q3 = bx2 + ay2;
@@ -1001,6 +1016,7 @@ __device__ __forceinline__ void sensor_pos(const d2d_cfg& cfg, const Scn& s, dou
         q = (q1 < q) ? q1 : q;
         q = (q2 < q) ? q2 : q;
         q = (q3 < q) ? q3 : q;
+#endif
         const double d = sqrt_dist(q) - s.cr[i];
         // stable ascending insertion into the top-3 (equal keys keep index order)
         const bool l0 = (bi0 < 0) || d < bd0, l1 = (bi1 < 0) || d < bd1, l2 = (bi2 < 0) || d < bd2;
