@@ -101,11 +101,19 @@ def cpu_baseline(args, kwargs):
     for _ in range(steps):
         b.step(act, nthreads=threads)
     dt = time.perf_counter() - t0
+    # the same batch on one core (1 core and all cores), a shorter sample
+    t1 = time.perf_counter()
+    steps1 = 0
+    while steps1 < 1 or (time.perf_counter() - t1 < args.cpu_seconds / 4 and steps1 < 20000):
+        b.step(act, nthreads=1)
+        steps1 += 1
+    dt1 = time.perf_counter() - t1
     b.close()
     return {"value": n * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
+            "single_core_value": n * steps1 / dt1,
             "sample": f"C oracle (oracle/d2d_oracle.c, scalar fp64 port of the reference step), "
                       f"{n} envs x {steps} steps of {args.scenario} with auto-reset, {threads} threads, "
-                      f"{dt:.1f} s"}
+                      f"{dt:.1f} s; single core: {steps1} steps, {dt1:.1f} s"}
 
 
 def main():
