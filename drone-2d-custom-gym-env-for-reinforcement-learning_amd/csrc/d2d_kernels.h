@@ -10,16 +10,20 @@
 //       waves at once), 6-pivot joint sweep,
 //       store the state; velocity part of the observation (obs 0-2, 17-18) and of the reward
 //   W1  sensor part (obs 3..16, CA inputs); for envs that end: the spawn-state sensor part
-//   W2  path role: Brent closest point, obs 19..26, the position / path terms of the reward while
-//       the physics wave finishes, then the sum
-//   W3  for envs that end: the spawn-state path part
+//   W2  path role: Brent closest point through the golden-march tables (steps [1, bt_split) of the
+//       table re-check), obs 19..26, the position / path terms of the reward while the physics wave
+//       finishes, then the sum
+//   W3  steps [bt_split, len) of W2's table re-check (D2D_SPLIT); then, for envs that end, the
+//       spawn state and the spawn-state path part
 //   (W1 and W3 take the spawn-state parts from the auto-reset observation cache when it is ready)
 //   epilogue (after the one barrier): the 64x27 f32 obs tile is stored as one contiguous span;
 //   W0 writes reward / flags / info / bookkeeping / auto-reset state.
 //
-// The critical path is W2's Brent search (highest wave priority); everything else runs under it.
-// At 65 536 envs this is 1 024 workgroups = 4 per CU = 4 waves per SIMD (VGPR <= 128, LDS <= 40 KB
-// even with 7 scenario tables).
+// W2's Brent search runs at the highest wave priority.  At 65 536 envs this is 1 024 workgroups = 4
+// per CU = 4 waves per SIMD, one of each role (VGPR <= 128, LDS <= 40 KB); every SIMD then issues
+// VALU work ~85 % of the time (DESIGN.md "What bounds it").  The scenario (+ probe table) is staged
+// into LDS by LDS-DMA while the waves' first state loads are in flight.  d2d_step_grouped_kernel is
+// the same body over the scenario-grouped slot layout (StepArgs::lane_env).
 //
 // K2 d2d_reset_kernel: masked reset, one lane per env.  K3 d2d_stats_kernel: fixed-order reduction.
 // K4 d2d_fill_kernel: fills the auto-reset observation cache (the envs that need it compacted,
@@ -246,6 +250,7 @@ __device__ __forceinline__ int next_scenario(const StepArgs& a, int j, uint32_t 
 //   f_ca    W1 -> W0,W2     CA inputs from obs 8..10 (CAStatic)
 //   f_gs    W0 -> W1,W2,W3  joint sweep finished: the jb region becomes the obs tile
 //   f_pre   W0 -> W2        velocity part of the reward (RewardVel)
+//   f_ver   W3 -> W2        first differing step in the second half of the table re-check
 struct K1Shared {
     double acc[D2D_NSTATS][EPB];  // W3 -> W0: episode accumulators of envs that end (prefetched)
     double cas[6][EPB];       // W1 -> W0, W2: CAStatic (d, os, oc, lpa, lca, rr)
