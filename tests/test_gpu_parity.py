@@ -84,6 +84,30 @@ def test_grouped_lane_map_irregular(d2):
     venv.close()
 
 
+def test_layout_change_keeps_state(d2):
+    """d2d_set_scenarios with a new env -> scenario map moves the running state into the new slot
+    layout (grouped -> regrouped -> identity): get_state in env order and the episode statistics are
+    unchanged, and stepping continues in parity with the oracle."""
+    rng = np.random.default_rng(9)
+    n = 777
+    es = rng.integers(0, 7, n).astype(np.int32)
+    venv, orc = make_pair(d2, n, SCENARIOS, seed=4, kwargs=_cfgkw(), env_scenario=es)
+    for _ in range(40):
+        compare_step(venv, orc, np.clip(rng.normal(0.0, 0.6, (n, 2)), -1, 1).astype(np.float32))
+    st0, ist0 = (x.cpu().numpy() for x in venv.get_state())
+    stats0 = venv.episode_stats(clear=False).cpu().numpy()
+    for new_map in (rng.permutation(es), np.zeros(n, np.int32), es):
+        venv._upload_scenarios(new_map)
+        st1, ist1 = (x.cpu().numpy() for x in venv.get_state())
+        np.testing.assert_array_equal(st1, st0)
+        np.testing.assert_array_equal(ist1, ist0)
+        np.testing.assert_allclose(venv.episode_stats(clear=False).cpu().numpy(), stats0, rtol=1e-12)
+    # back on the original map: keeps stepping in parity (the reset cache was dropped and refilled)
+    for _ in range(30):
+        compare_step(venv, orc, np.clip(rng.normal(0.0, 0.6, (n, 2)), -1, 1).astype(np.float32))
+    venv.close()
+
+
 def test_reset_cache_invalidation(d2):
     """The auto-reset observation cache (filled ahead of time by the fill kernel) must be dropped
     by a full reset with a new seed and by set_state (episode counters may change)."""
