@@ -223,6 +223,12 @@ def main():
                          "success": float(st[2]), "collisions": float(st[4]),
                          "allreduce_ms": t_ar * 1e3},
         }
+        vf = os.path.join(REPO, "profiles", f"valu_{args.scenario}_{n}.json")
+        if os.path.exists(vf):
+            # the kernel's actual bound (fp64 VALU issue), from the committed rocprofv3 SQ pass
+            v = json.load(open(vf))
+            line["valu"] = {k: v[k] for k in ("valu_insts_per_simd", "valu_active_cycles_per_simd",
+                                              "wave_lifetime_cycles", "valu_busy_frac", "source")}
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(args, kwargs)
         print(json.dumps(line), flush=True)

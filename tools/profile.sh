@@ -29,3 +29,4 @@ step pmc_write 600 rocprofv3 $KR -T --output-format csv -d "$OUT/pmc_write" -o w
 step pmc_sq 600 rocprofv3 $KR -T --output-format csv -d "$OUT/pmc_sq" -o sq --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_ANY -- $B --eager --steps 40 --warmup 30
 step pmc_clk 600 rocprofv3 $KR -T --output-format csv -d "$OUT/pmc_clk" -o clk --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES -- $B --eager --steps 40 --warmup 30
 python3 "$R/tools/traffic.py" "$OUT" --out "$OUT/traffic.json"
+python3 "$R/tools/valu.py" "$OUT"/pmc_sq/sq_counter_collection.csv --out "$OUT/valu.json"
