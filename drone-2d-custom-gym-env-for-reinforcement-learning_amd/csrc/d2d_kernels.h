@@ -21,7 +21,7 @@
 //
 // W2's Brent search runs at the highest wave priority.  At 65 536 envs this is 1 024 workgroups = 4
 // per CU = 4 waves per SIMD, one of each role (VGPR <= 128, LDS <= 40 KB); every SIMD then issues
-// VALU work ~85 % of the time (DESIGN.md "What bounds it").  The scenario (+ probe table) is staged
+// VALU work ~87 % of the time (DESIGN.md "What bounds it").  The scenario (+ probe table) is staged
 // into LDS by LDS-DMA while the waves' first state loads are in flight.  d2d_step_grouped_kernel is
 // the same body over the scenario-grouped slot layout (StepArgs::lane_env).
 //
