@@ -49,8 +49,10 @@ MIXED = ["perpendicular", "parallel", "S_parallel", "corridor", "S_corridor", "l
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=1000)
-    p.add_argument("--warmup", type=int, default=50)
+    p.add_argument("--steps", type=int, default=2000)
+    p.add_argument("--warmup", type=int, default=300,
+                   help="untimed steps; ~4 mean episode lengths, so the timed loop sees the steady-state mix "
+                        "of envs (the first episodes after reset all start at the spawn boxes)")
     p.add_argument("--envs", type=int, default=ENVS_PER_GPU)
     p.add_argument("--scenario", default=SCENARIO,
                    help="test scenario name, NAME_free (no obstacles: configs[1]) or 'mixed' (configs[4])")
