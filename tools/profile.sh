@@ -22,11 +22,12 @@ step() {  # step <name> <timeout> <cmd...>: stop on any failure
   [ $rc -eq 0 ] || { echo "STOP"; exit $rc; }
 }
 
-step kt 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/kt" -o kt -- $B --steps 1000 --warmup 50
-step kt_eager 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/kt_eager" -o kt -- $B --eager --steps 300 --warmup 30
-step pmc_fetch 600 rocprofv3 $KR -T --output-format csv -d "$OUT/pmc_fetch" -o fetch --pmc FETCH_SIZE -- $B --eager --steps 40 --warmup 30
-step pmc_write 600 rocprofv3 $KR -T --output-format csv -d "$OUT/pmc_write" -o write --pmc WRITE_SIZE -- $B --eager --steps 40 --warmup 30
-step pmc_sq 600 rocprofv3 $KR -T --output-format csv -d "$OUT/pmc_sq" -o sq --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_ANY -- $B --eager --steps 40 --warmup 30
-step pmc_clk 600 rocprofv3 $KR -T --output-format csv -d "$OUT/pmc_clk" -o clk --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES -- $B --eager --steps 40 --warmup 30
+# the bench's own defaults (2 000 graph-replayed steps after 300 warmup steps)
+step kt 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/kt" -o kt -- $B
+step kt_eager 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/kt_eager" -o kt -- $B --eager --steps 300 --warmup 300
+step pmc_fetch 600 rocprofv3 $KR -T --output-format csv -d "$OUT/pmc_fetch" -o fetch --pmc FETCH_SIZE -- $B --eager --steps 40 --warmup 300
+step pmc_write 600 rocprofv3 $KR -T --output-format csv -d "$OUT/pmc_write" -o write --pmc WRITE_SIZE -- $B --eager --steps 40 --warmup 300
+step pmc_sq 600 rocprofv3 $KR -T --output-format csv -d "$OUT/pmc_sq" -o sq --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_ANY -- $B --eager --steps 40 --warmup 300
+step pmc_clk 600 rocprofv3 $KR -T --output-format csv -d "$OUT/pmc_clk" -o clk --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES -- $B --eager --steps 40 --warmup 300
 python3 "$R/tools/traffic.py" "$OUT" --out "$OUT/traffic.json"
 python3 "$R/tools/valu.py" "$OUT"/pmc_sq/sq_counter_collection.csv --out "$OUT/valu.json"
