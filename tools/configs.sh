@@ -16,9 +16,9 @@ run() {  # run <label> <bench args...>
   grep '^{' "$R/gpurun_out/cfg_$label.log" | sed "s/^{/{\"label\": \"$label\", /" >> "$OUT"
   tail -n 1 "$OUT" | cut -c1-160
 }
-run cfg1_free_4096 --scenario corridor_free --envs 4096 --steps 1000 --warmup 50
-run cfg2_corridor_65536 --scenario corridor --steps 1000 --warmup 50
-run cfg3_large_65536 --scenario large --steps 1000 --warmup 50
-run cfg3_S_corridor_65536 --scenario S_corridor --steps 1000 --warmup 50
-run cfg4_mixed_65536 --scenario mixed --steps 1000 --warmup 50
-run cfg2_free_65536 --scenario corridor_free --steps 1000 --warmup 50
+run cfg1_free_4096 --scenario corridor_free --envs 4096
+run cfg2_corridor_65536 --scenario corridor
+run cfg3_large_65536 --scenario large
+run cfg3_S_corridor_65536 --scenario S_corridor
+run cfg4_mixed_65536 --scenario mixed
+run cfg2_free_65536 --scenario corridor_free
