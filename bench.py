@@ -40,6 +40,7 @@ METRIC = "env-steps/sec at 65 536 parallel envs; 1/2/4/8 MI355X scaling"
 ENVS_PER_GPU = 65536
 SCENARIO = "corridor"
 BYTES_PER_ENV_STEP = 650   # DESIGN.md "Algorithmic bytes": 272 read + 378 written, info off
+INFO_BYTES = 48            # --info: the f32 [N, 12] info row per env-step
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec)
 ACTION_BANK = 16
 # BASELINE.json configs[4]: env i gets scenario i mod 7 in this order
@@ -58,6 +59,8 @@ def parse():
                    help="test scenario name, NAME_free (no obstacles: configs[1]) or 'mixed' (configs[4])")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (s)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--info", action="store_true",
+                   help="also write the per-env info rows (f32 [N, 12], what the SB3 adapter reads): +48 B/env-step")
     p.add_argument("--eager", action="store_true",
                    help="launch every step from Python instead of replaying the captured hipGraph")
     return p.parse_args()
@@ -130,7 +133,7 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
     n = args.envs
     # this rank's block of a global batch of world x n envs (global env ids, no step collective)
-    venv = shard.make_shard_venv(n * world, rank, world, device=dev, seed=12345, with_info=False, **kwargs)
+    venv = shard.make_shard_venv(n * world, rank, world, device=dev, seed=12345, with_info=args.info, **kwargs)
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
     bank = [(torch.rand(n, 2, device=dev, generator=g) * 2 - 1).contiguous() for _ in range(ACTION_BANK)]
     venv.reset()
@@ -194,10 +197,12 @@ def main():
     if rank == 0:
         total_steps = n * world * n_timed
         value = total_steps / wall
-        achieved = BYTES_PER_ENV_STEP * n / (kern_ms * 1e-3) / 1e9
+        bytes_env = BYTES_PER_ENV_STEP + (INFO_BYTES if args.info else 0)
+        achieved = bytes_env * n / (kern_ms * 1e-3) / 1e9
         st = stats.cpu().numpy()
         traffic = None
-        tf = os.path.join(REPO, "profiles", f"traffic_{args.scenario}_{n}.json")
+        tag = f"{args.scenario}_{n}" + ("_info" if args.info else "")
+        tf = os.path.join(REPO, "profiles", f"traffic_{tag}.json")
         if os.path.exists(tf):
             traffic = json.load(open(tf)).get("bytes_per_launch")
         line = {
@@ -216,16 +221,17 @@ def main():
             "config": {"workload": f"{args.scenario}, {n} envs per GPU, U(-1,1) f32 actions, in-kernel auto-reset",
                        "envs_per_gpu": n, "total_envs": n * world, "scenario": args.scenario,
                        "parallelism": f"env-shard x{world}", "hipgraph": bool(graph is not None),
-                       "outputs": "obs f32[N,27], reward f32, terminated/truncated u8 (info rows off)"},
+                       "outputs": "obs f32[N,27], reward f32, terminated/truncated u8, terminal obs"
+                                  + (", info f32[N,12]" if args.info else " (info rows off)")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "d2d_step_kernel + d2d_fill_kernel/16 (per step)", "kernel_ms": kern_ms,
-                         "bytes_per_env_step": BYTES_PER_ENV_STEP},
+                         "bytes_per_env_step": bytes_env},
             "episodes": {"finished": float(st[1]), "mean_return": float(st[0] / max(st[1], 1)),
                          "success": float(st[2]), "collisions": float(st[4]),
                          "allreduce_ms": t_ar * 1e3},
         }
-        vf = os.path.join(REPO, "profiles", f"valu_{args.scenario}_{n}.json")
+        vf = os.path.join(REPO, "profiles", f"valu_{tag}.json")
         if os.path.exists(vf):
             # the kernel's actual bound (fp64 VALU issue), from the committed rocprofv3 SQ pass
             v = json.load(open(vf))
