@@ -8,7 +8,12 @@
   (``best_models_config_and_res/run17see3/res/<scenario>/results.txt``, 100 runs each) and its
   env config (``env_train_config.txt`` is a Python dict literal: parsed with ast.literal_eval).
 
-Outputs: tests/golden/agent_17_90.npz, tests/golden/agent_17_90_results.json.
+* the per-episode arrays the reference saved beside each results.txt (collisions / rewards / apes /
+  time_spent ``.npy``, read with ``numpy.load(allow_pickle=False)``) and the results.txt text itself,
+  so the harness's results writer can be checked byte for byte against the reference's output.
+
+Outputs: tests/golden/agent_17_90.npz, tests/golden/agent_17_90_results.json,
+tests/golden/agent_17_90_episodes.npz.
 """
 import ast
 import io
@@ -33,7 +38,7 @@ def main():
             "action_net.weight", "action_net.bias", "log_std"]
     np.savez(os.path.join(HERE, "agent_17_90.npz"),
              **{k.replace(".", "_"): sd[k].numpy().astype(np.float32) for k in keep})
-    res = {}
+    res, txt, eps = {}, {}, {}
     resdir = os.path.join(REF, RUN, "res")
     for scn in sorted(os.listdir(resdir)):
         f = os.path.join(resdir, scn, "results.txt")
@@ -48,8 +53,13 @@ def main():
             except ValueError:
                 d[k.strip()] = v
         res[scn] = d
+        txt[scn] = open(f).read()
+        for k in ("collisions", "rewards", "apes", "time_spent"):
+            eps[f"{scn}__{k}"] = np.load(os.path.join(resdir, scn, f"{k}.npy"), allow_pickle=False)
     cfg = ast.literal_eval(open(os.path.join(REF, RUN, "env_train_config.txt")).read())
-    json.dump({"agent": AGENT, "source": RUN + "/res/*/results.txt", "env_config": cfg, "results": res},
+    np.savez(os.path.join(HERE, "agent_17_90_episodes.npz"), **eps)
+    json.dump({"agent": AGENT, "source": RUN + "/res/*/results.txt", "env_config": cfg, "results": res,
+               "results_txt": txt},
               open(os.path.join(HERE, "agent_17_90_results.json"), "w"), indent=1, default=str)
     print("wrote", len(res), "scenario results")
 
