@@ -36,3 +36,30 @@ def test_agent_success_rate_matches_reference(d2, scn):
     c, cq = s["Collision rate"], ref["Collision rate"]
     sec = math.sqrt(max(cq * (1 - cq), 0.0099) / 100 + max(c * (1 - c), 0.0099) / 1000)
     assert abs(c - cq) < 4 * sec, (scn, c, cq)
+
+
+@pytest.mark.parametrize("scn", ["corridor", "large", "S_corridor", "impossible"])
+def test_agent_episode_distributions_match_reference(d2, scn):
+    """Per-episode flight time, APE and total reward against the reference's own saved arrays
+    (run17see3/res/<scn>/{time_spent,apes,rewards}.npy, tests/golden/agent_17_90_episodes.npz):
+    two-sample KS test, p > 1e-3.  The reference's saved rewards were produced with its
+    env_train_config reward weights (PP_rew_max 3.5, abs_inv_CA_min_rew 1/6; tools/closed_loop.py
+    --config train vs test, DESIGN.md "Closed loop"), so this run uses those kwargs; the dynamics and
+    observations do not depend on them."""
+    import numpy as np
+    from scipy.stats import ks_2samp
+
+    from drone2d_amd import harness
+    from drone2d_amd.config import ENV_TEST_CONFIG
+
+    ref = json.load(open(os.path.join(HERE, "golden", "agent_17_90_results.json")))
+    eps = np.load(os.path.join(HERE, "golden", "agent_17_90_episodes.npz"))
+    kw = dict(ENV_TEST_CONFIG, **{k: v for k, v in ref["env_config"].items() if not k.startswith("render")})
+    pol = harness.MlpActor.from_npz(os.path.join(HERE, "golden", "agent_17_90.npz"))
+    venv = d2.Drone2dVecEnv(4096, seed=11, with_info=True, **dict(kw, scenario=scn))
+    m = harness.run_first_episodes(venv, pol, seed=11)
+    venv.close()
+    assert m["unfinished"] == 0
+    for k in ("time_spent", "apes", "rewards"):
+        p = ks_2samp(np.asarray(m[k], np.float64), eps[f"{scn}__{k}"].astype(np.float64)).pvalue
+        assert p > 1e-3, (scn, k, p)

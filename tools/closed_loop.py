@@ -6,7 +6,15 @@ scenario with N envs each (stochastic policy, as the reference's ``model.predict
 reference's result files under gpurun_out/Tests/agent_17/<scenario>/ and compares success /
 collision rates with the reference's own 100-run results (tests/golden/agent_17_90_results.json).
 
-    python tools/closed_loop.py [--envs 2000] [--seed 0]
+    python tools/closed_loop.py [--envs 2000] [--seed 0] [--config test|train]
+
+Besides the rates, the per-episode distributions (flight time, APE, total reward) are compared with
+the reference's own saved arrays (tests/golden/agent_17_90_episodes.npz): z of the mean difference
+and the two-sample KS p-value.  ``--config`` picks the env kwargs: the reference's current
+env_test_config (default) or its env_train_config (run17see3/env_train_config.txt): the two differ
+in reward weights only (initial_throw / n_fall_steps are inert in the reference), so the flight time
+and APE distributions must not move between them while the total rewards tell which configuration
+the reference's saved results were produced with.
 """
 from __future__ import annotations
 
@@ -28,6 +36,7 @@ def main():
     ap.add_argument("--envs", type=int, default=2000)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--scenarios", default=",".join(SCENARIOS))
+    ap.add_argument("--config", default="test", choices=["test", "train"])
     a = ap.parse_args()
     import torch  # noqa: F401
 
@@ -36,14 +45,22 @@ def main():
     from drone2d_amd.config import ENV_TEST_CONFIG
 
     ref = json.load(open(os.path.join(REPO, "tests", "golden", "agent_17_90_results.json")))
+    import numpy as np
+    from scipy.stats import ks_2samp
+
+    eps = np.load(os.path.join(REPO, "tests", "golden", "agent_17_90_episodes.npz"))
+    if a.config == "test":
+        base = dict(ENV_TEST_CONFIG)
+    else:
+        base = dict(ENV_TEST_CONFIG, **{k: v for k, v in ref["env_config"].items() if not k.startswith("render")})
     pol = harness.MlpActor.from_npz(os.path.join(REPO, "tests", "golden", "agent_17_90.npz"))
     out = {}
     for scn in a.scenarios.split(","):
         t0 = time.perf_counter()
-        venv = d2.Drone2dVecEnv(a.envs, seed=a.seed, with_info=True, **dict(ENV_TEST_CONFIG, scenario=scn))
+        venv = d2.Drone2dVecEnv(a.envs, seed=a.seed, with_info=True, **dict(base, scenario=scn))
         m = harness.run_first_episodes(venv, pol, seed=a.seed)
         venv.close()
-        s = harness.write_results(m, os.path.join(REPO, "gpurun_out", "Tests", "agent_17", scn), scn, "17",
+        s = harness.write_results(m, os.path.join(REPO, "gpurun_out", "Tests", "agent_17_" + a.config, scn), scn, "17",
                                   ref["agent"])
         r = ref["results"][scn]
         p, q = s["Success rate"], r["Success rate"]
@@ -53,9 +70,16 @@ def main():
                                                                "Average flight time")},
                     "runs": [n_ours, n_ref], "success_z": (p - q) / se, "unfinished": m["unfinished"],
                     "seconds": time.perf_counter() - t0}
+        for k in ("time_spent", "apes", "rewards"):
+            x, y = np.asarray(m[k], np.float64), eps[f"{scn}__{k}"].astype(np.float64)
+            se_m = math.sqrt(x.var() / max(len(x), 1) + y.var() / len(y))
+            out[scn][k] = {"ours": float(x.mean()), "ref": float(y.mean()),
+                           "z": float((x.mean() - y.mean()) / max(se_m, 1e-12)),
+                           "ks_p": float(ks_2samp(x, y).pvalue)}
         print(scn, json.dumps(out[scn]), flush=True)
     os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
-    json.dump(out, open(os.path.join(REPO, "gpurun_out", "closed_loop.json"), "w"), indent=1)
+    json.dump({"config": a.config, "envs": a.envs, "seed": a.seed, "scenarios": out},
+              open(os.path.join(REPO, "gpurun_out", f"closed_loop_{a.config}.json"), "w"), indent=1)
 
 
 if __name__ == "__main__":
