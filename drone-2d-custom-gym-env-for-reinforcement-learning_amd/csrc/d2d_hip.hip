@@ -113,7 +113,9 @@ hipError_t rc_rebuild(d2d_t* h, hipStream_t stream) {
 // search, one scenario + probe table staged in LDS) whose state is contiguous.  The envs, sorted
 // by (scenario, id), are cut into ceil(n / 64) groups -- no padding between scenarios, so the grid
 // is no larger than the identity layout's (at 65 536 envs: 1 024 workgroups = one resident round)
-// and at most n_scn - 1 groups straddle two or more scenarios (wg_scn = -1).  Groups are then
+// and at most n_scn - 1 groups straddle scenarios: wg_scn = -(s + 2) for a group of scenarios s and
+// s + 1 (K1 stages both scenarios in LDS; their probe tables are read through L1/L2), -1 for a group
+// of three or more (everything through L1/L2).  Groups are then
 // ordered by their first env id, so groups whose envs interleave (e.g. scenario = id mod 7) get
 // consecutive numbers (xcd_group places consecutive numbers on one XCD).
 void make_groups(int n, const int32_t* env_scn, int n_scn, std::vector<int32_t>& lanes, std::vector<int32_t>& ws) {
@@ -128,12 +130,14 @@ void make_groups(int n, const int32_t* env_scn, int n_scn, std::vector<int32_t>&
     ws.assign(ng, 0);
     for (size_t g = 0; g < ng; ++g) {
         const size_t o = gi[g] * EPB;
-        int32_t sc = env_scn[order[o]];
+        const int32_t lo = env_scn[order[o]];
+        int32_t hi = lo;
         for (size_t l = 0; l < EPB && o + l < (size_t)n; ++l) {
             lanes[g * EPB + l] = order[o + l];
-            if (env_scn[order[o + l]] != sc) sc = -1;
+            hi = std::max(hi, env_scn[order[o + l]]);
         }
-        ws[g] = sc;
+        // pure: the scenario; straddling exactly two consecutive scenarios: -(lo + 2); more: -1
+        ws[g] = hi == lo ? lo : (hi == lo + 1 ? -(lo + 2) : -1);
     }
 }
 

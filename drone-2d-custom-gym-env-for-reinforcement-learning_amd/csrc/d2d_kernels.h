@@ -94,7 +94,7 @@ struct StepArgs {
     // buffers (actions, obs, reward, flags, info, terminal obs), the scenario map and the spawn RNG
     // stay indexed by env id.  Without the map slot == env.
     const int32_t* lane_env;  // [ns] slot -> env
-    const int32_t* wg_scn;    // [ns / 64]
+    const int32_t* wg_scn;    // [ns / 64]  (-(s + 2): scenarios s and s + 1; -1: three or more)
 };
 
 // Auto-reset observation cache.  The observation an env gets when it auto-resets depends only on
@@ -115,6 +115,9 @@ struct StepArgs {
 #endif
 #ifndef D2D_GLDS
 #define D2D_GLDS 1       // K1 stages its scenario (+ probe table) with LDS-DMA
+#endif
+#ifndef D2D_STRADDLE_LDS
+#define D2D_STRADDLE_LDS 1  // a grouped-layout workgroup straddling two scenarios stages both in LDS
 #endif
 #ifndef D2D_SPLIT
 #define D2D_SPLIT 1      // W3 re-checks the second half of W2's golden-march table (0: W2 alone)
@@ -299,8 +302,9 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, Scn* s_scn, K1Shared&
     const int n = a.ns;
     const bool auto_reset = a.cfg.auto_reset != 0;
     STAMP(0);
-    const int s0 = (GRP && LDS) ? a.wg_scn[wg] : 0;
-    const int ncopy = (GRP && LDS) ? 1 : a.n_scn;
+    const int ws = (GRP && LDS) ? a.wg_scn[wg] : 0;
+    const int s0 = ws >= 0 ? ws : -ws - 2;          // a straddling group: its two scenarios s0, s0 + 1
+    const int ncopy = (GRP && LDS) ? (ws >= 0 ? 1 : 2) : a.n_scn;
     const Scn* scns;
     const BtHot* hots = nullptr;
     if (D2D_GLDS && LDS && (ncopy == 1 || !LTAB)) {
@@ -761,14 +765,19 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
     k1_body<LDS, LTAB, false>(a, s_scn, sh, blockIdx.x);
 }
 // grouped slot layout: a pure group stages its scenario and probe table in LDS; a group that
-// straddles scenarios (at most n_scn - 1 of them: the layout has no padding between scenarios)
-// reads the tables through L1/L2
+// straddles two scenarios (at most n_scn - 1 of them: the layout has no padding between scenarios)
+// stages both scenarios (2 x Scn fits in the Scn + BtHot allocation) and reads the probe tables
+// through L1/L2; a group of three or more scenarios reads everything through L1/L2
 __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_grouped_kernel(StepArgs a) {
     extern __shared__ __attribute__((aligned(16))) Scn s_scn[];
     __shared__ __attribute__((aligned(16))) K1Shared sh;
+    static_assert(2 * sizeof(Scn) <= sizeof(Scn) + sizeof(BtHot), "two staged scenarios");
     const int wg = xcd_group(blockIdx.x, gridDim.x);
-    if (a.brt && a.wg_scn[wg] >= 0)
+    const int ws = a.wg_scn[wg];
+    if (a.brt && ws >= 0)
         k1_body<true, true, true>(a, s_scn, sh, wg);
+    else if (D2D_STRADDLE_LDS && ws <= -2)
+        k1_body<true, false, true>(a, s_scn, sh, wg);
     else
         k1_body<false, false, true>(a, s_scn, sh, wg);
 }

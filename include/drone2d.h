@@ -192,8 +192,8 @@ int32_t d2d_selftest(int32_t which, int64_t n, uint64_t seed, uint64_t* mismatch
 /* The internal slot layout d2d_set_scenarios builds for a static env->scenario map with several
  * scenarios (host-only, no device needed; for tests and diagnostics, no reference counterpart):
  * envs sorted by (scenario, id) are cut into ceil(n/64) groups of 64 slots; slot_env[64 g + l] is
- * the env in slot l of group g (-1: padding at the end), group_scn[g] the group's scenario (-1 if it
- * straddles scenarios).  slot_env: int32[ceil(n/64) * 64], group_scn: int32[ceil(n/64)].
+ * the env in slot l of group g (-1: padding at the end), group_scn[g] the group's scenario, or
+ * -(s + 2) if it straddles exactly scenarios s and s + 1, or -1 if it holds three or more.  slot_env: int32[ceil(n/64) * 64], group_scn: int32[ceil(n/64)].
  * Returns the number of groups, or -1 on bad arguments (d2d_last_error says which). */
 int32_t d2d_group_layout(int32_t n, const int32_t* env_scn, int32_t n_scn, int32_t* slot_env, int32_t* group_scn);
 

@@ -128,9 +128,13 @@ def test_group_layout_properties(hip_lib, case):
         e = g[j][g[j] >= 0]
         if group_scn[j] >= 0:
             assert (es[e] == group_scn[j]).all()
-        else:
+        elif group_scn[j] <= -2:                                 # exactly scenarios s, s + 1
             straddle += 1
-            assert len(set(es[e].tolist())) > 1
+            s = -int(group_scn[j]) - 2
+            assert set(es[e].tolist()) == {s, s + 1}
+        else:                                                    # three or more
+            straddle += 1
+            assert group_scn[j] == -1 and len(set(es[e].tolist())) > 2
     assert straddle <= k - 1
     firsts = g[:, 0]
     assert (np.diff(firsts) > 0).all()                           # numbered by first env id
