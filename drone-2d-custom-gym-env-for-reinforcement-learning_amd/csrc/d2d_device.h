@@ -332,6 +332,9 @@ __device__ __forceinline__ bool brent_active(const Brent& B) {
     const double tol2 = 2.0 * tol1;
     return (fabs(B.xf - xm) > (tol2 - 0.5 * (B.b - B.a))) & (B.num < 500);
 }
+#ifndef D2D_PAR_BALLOT
+#define D2D_PAR_BALLOT 1  // brent_step: the parabolic candidate only when some lane of the wave takes it
+#endif
 __device__ __forceinline__ void brent_step(const Scn& s, const PathK& K, double px, double py, Brent& B) {
     const double a = B.a, b = B.b, xf = B.xf, fx = B.fx, nfc = B.nfc, fulc = B.fulc;
     const double xm = 0.5 * (a + b);
@@ -345,10 +348,14 @@ __device__ __forceinline__ void brent_step(const Scn& s, const PathK& K, double 
     p = (q > 0.0) ? -p : p;
     q = fabs(q);
     const bool par = (fabs(B.e) > tol1) & (fabs(p) < fabs(0.5 * q * B.e)) & (p > q * (a - xf)) & (p < q * (b - xf));
-    // only used when `par` holds: then q > 0 and |p / q| < |e| / 2, a normal quotient
-    double rat_p = div_normal(p + 0.0, q);
-    const double xp = xf + rat_p;
-    rat_p = (((xp - a) < tol2) | ((b - xp) < tol2)) ? tol1 * sgn_nz(xm - xf) : rat_p;
+    // only used when `par` holds: then q > 0 and |p / q| < |e| / 2, a normal quotient.  Skipped
+    // when no lane of the wave takes the parabolic step (the golden tails of long searches)
+    double rat_p = 0.0;
+    if (!D2D_PAR_BALLOT || __ballot(par) != 0ull) {
+        rat_p = div_normal(p + 0.0, q);
+        const double xp = xf + rat_p;
+        rat_p = (((xp - a) < tol2) | ((b - xp) < tol2)) ? tol1 * sgn_nz(xm - xf) : rat_p;
+    }
     // golden-section candidate
     const double e_g = (xf >= xm) ? a - xf : b - xf;
     const double rat_g = BR_GOLDEN * e_g;

@@ -38,7 +38,7 @@ def build(specs):
         print("built", lib_for(tag), d)
 
 
-def time_variant(d2, torch, lib, n, scenario, steps=200, warmup=30, auto_reset=True):
+def time_variant(d2, torch, lib, n, scenario, steps=1000, warmup=300, auto_reset=True):
     import numpy as np
 
     from drone2d_amd.config import ENV_TRAIN_CONFIG
@@ -66,7 +66,7 @@ def time_variant(d2, torch, lib, n, scenario, steps=200, warmup=30, auto_reset=T
     return ms
 
 
-def run(tags, n, scenario, rounds, auto_reset=True):
+def run(tags, n, scenario, rounds, auto_reset=True, steps=1000, warmup=300):
     import torch
 
     import drone2d_amd as d2
@@ -74,7 +74,8 @@ def run(tags, n, scenario, rounds, auto_reset=True):
     res = {t: [] for t in tags}
     for r in range(rounds):
         for t in tags:
-            res[t].append(time_variant(d2, torch, lib_for(t), n, scenario, auto_reset=auto_reset))
+            res[t].append(time_variant(d2, torch, lib_for(t), n, scenario, steps=steps, warmup=warmup,
+                                       auto_reset=auto_reset))
     out = {t: {"ms_per_step_min": min(v), "ms_per_step_all": v} for t, v in res.items()}
     out = {"envs": n, "scenario": scenario, "auto_reset": auto_reset, "variants": out}
     print(json.dumps(out, indent=1))
@@ -91,8 +92,11 @@ if __name__ == "__main__":
     ap.add_argument("--scenario", default="corridor")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--no-auto-reset", action="store_true")
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=300, help="untimed steps: the bench's steady state")
     a = ap.parse_args()
     if a.mode == "build":
         build(a.specs)
     else:
-        run([s.partition("::")[0].partition(":")[0] for s in a.specs], a.envs, a.scenario, a.rounds, not a.no_auto_reset)
+        run([s.partition("::")[0].partition(":")[0] for s in a.specs], a.envs, a.scenario, a.rounds, not a.no_auto_reset,
+            a.steps, a.warmup)
