@@ -143,32 +143,44 @@ def main():
         venv.step(bank[k % ACTION_BANK])
     venv.episode_stats(clear=True)
 
-    graph = None
+    # exactly args.steps timed steps: reps replays of a 16-step graph + one graph of the remainder
+    reps, rem = divmod(args.steps, ACTION_BANK)
+    graph = tail = None
     if not args.eager:
         # capture ACTION_BANK steps (even count: the output double-buffer returns to its start)
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            for k in range(ACTION_BANK):
-                venv.step(bank[k])
+        if reps:
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                for k in range(ACTION_BANK):
+                    venv.step(bank[k])
+        if rem:
+            tail = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(tail):
+                for k in range(rem):
+                    venv.step(bank[k])
         torch.cuda.synchronize()
+    hipgraph = not args.eager
 
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    segs = (reps + (1 if rem else 0)) if hipgraph else args.steps
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(segs)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(segs)]
     barrier_sync(world)
     t0 = time.perf_counter()
-    if graph is not None:
-        reps = (args.steps + ACTION_BANK - 1) // ACTION_BANK
+    if hipgraph:
         for r in range(reps):
             starts[r].record(stream)
             graph.replay()
             ends[r].record(stream)
-        n_timed = reps * ACTION_BANK
+        if rem:
+            starts[reps].record(stream)
+            tail.replay()
+            ends[reps].record(stream)
     else:
         for k in range(args.steps):
             starts[k].record(stream)
             venv.step(bank[k % ACTION_BANK])
             ends[k].record(stream)
-        n_timed = args.steps
+    n_timed = args.steps
     barrier_sync(world)
     wall = time.perf_counter() - t0
 
@@ -181,10 +193,8 @@ def main():
         shard.allreduce_stats(stats)  # the one RCCL collective: 8 doubles per logging interval
         torch.cuda.synchronize()
         t_ar = time.perf_counter() - t1
-    if graph is not None:
-        kern_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts[:reps], ends[:reps])])) / ACTION_BANK
-    else:
-        kern_ms = float(np.mean([s.elapsed_time(e) for s, e in zip(starts, ends)]))
+    # device time of the timed steps (HIP events on the launch stream) per step
+    kern_ms = float(np.sum([s.elapsed_time(e) for s, e in zip(starts, ends)])) / n_timed
 
     wall_t = torch.tensor([wall], dtype=torch.float64, device=dev)
     kern_t = torch.tensor([kern_ms], dtype=torch.float64, device=dev)
@@ -220,7 +230,7 @@ def main():
             "data": "synthetic",
             "config": {"workload": f"{args.scenario}, {n} envs per GPU, U(-1,1) f32 actions, in-kernel auto-reset",
                        "envs_per_gpu": n, "total_envs": n * world, "scenario": args.scenario,
-                       "parallelism": f"env-shard x{world}", "hipgraph": bool(graph is not None),
+                       "parallelism": f"env-shard x{world}", "hipgraph": hipgraph,
                        "outputs": "obs f32[N,27], reward f32, terminated/truncated u8, terminal obs"
                                   + (", info f32[N,12]" if args.info else " (info rows off)")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -21,4 +21,5 @@ run() {  # run <name> <timeout-s> <cmd...>; allow exit 0/1 (test failures), stop
 
 run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
 run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-run bench 600 python bench.py --steps 300 --warmup 30
+run bench 600 python bench.py
+run bench_k20 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline
