@@ -28,6 +28,9 @@ SIGNATURES = {
     "d2d_step": (C.c_int32, [_VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP]),
     "d2d_get_state": (C.c_int32, [_VP, _VP, _VP, _VP]),
     "d2d_set_state": (C.c_int32, [_VP, _VP, _VP, _VP]),
+    "d2d_refresh_pool": (C.c_int32, [_VP, C.POINTER(abi.D2DScn), C.c_int32]),
+    "d2d_get_env_scenarios": (C.c_int32, [_VP, _VP, _VP]),
+    "d2d_set_env_scenarios": (C.c_int32, [_VP, _VP, _VP]),
     "d2d_episode_stats": (C.c_int32, [_VP, _VP, C.c_int32, _VP]),
     "d2d_selftest": (C.c_int32, [C.c_int32, C.c_int64, C.c_uint64, C.POINTER(C.c_uint64)]),
     "d2d_group_layout": (C.c_int32, [C.c_int32, _VP, C.c_int32, _VP, _VP]),

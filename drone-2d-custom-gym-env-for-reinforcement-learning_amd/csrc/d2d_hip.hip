@@ -48,6 +48,10 @@ struct d2d_handle {
     d2d::Scn* scn = nullptr;    // device table: ABI scenarios + derived fields
     d2d::BrTab* brt = nullptr;  // golden-march tables of the scenarios (d2d_brtab_kernel)
     int32_t* env_scn = nullptr;
+    // pool mode: the scenario table has two halves of pool_n entries; resets draw from the half at
+    // pool_base (host copy; the kernels read *pool_dev), d2d_refresh_pool fills and switches halves
+    int pool_base = 0, pool_n = 0;
+    int32_t* pool_dev = nullptr;
     uint64_t seed = 0;
     bool reset_done = false;
     uint64_t* stamps = nullptr;  // diagnostic builds (D2D_STAMPS) only
@@ -77,6 +81,8 @@ StepArgs make_args(const d2d_t* h) {
     a.scn = h->scn;
     a.brt = D2D_BRTAB ? h->brt : nullptr;
     a.env_scn = h->env_scn;
+    a.pool_base = h->pool_dev;
+    a.pool_n = h->pool_n;
     a.cfg = h->cfg;
     a.damping_dt = std::pow(h->cfg.damping, 1.0 / 60.0);
     a.seed = h->seed;
@@ -274,6 +280,8 @@ int32_t d2d_create(const d2d_cfg* cfg, int32_t n_envs, int32_t device, d2d_t** o
     const size_t n = (size_t)n_envs;
     Layout L;
     if ((e = hipMalloc(&h->env_scn, sizeof(int32_t) * n)) != hipSuccess ||
+        (e = hipMalloc(&h->pool_dev, sizeof(int32_t))) != hipSuccess ||
+        (e = hipMemset(h->pool_dev, 0, sizeof(int32_t))) != hipSuccess ||
         (e = alloc_layout(L, n_envs, {}, {})) != hipSuccess) {
         d2d_destroy(h);
         return hip_fail(e, "d2d_create: hipMalloc");
@@ -296,6 +304,7 @@ void d2d_destroy(d2d_t* h) {
     if (h->scn) (void)hipFree(h->scn);
     if (h->brt) (void)hipFree(h->brt);
     if (h->env_scn) (void)hipFree(h->env_scn);
+    if (h->pool_dev) (void)hipFree(h->pool_dev);
     delete h;
 }
 
@@ -324,55 +333,69 @@ int32_t d2d_set_scenarios(d2d_t* h, const d2d_scn* scns, int32_t n_scn, const in
             if (env_scn_host[i] < 0 || env_scn_host[i] >= n_scn)
                 return fail(D2D_E_ARG, "d2d_set_scenarios: env scenario index out of range");
     }
-    DeviceGuard g(h->device);
-    hipError_t e;
-    if (h->scn) {
-        (void)hipFree(h->scn);
-        h->scn = nullptr;
-    }
-    if (h->brt) {
-        (void)hipFree(h->brt);
-        h->brt = nullptr;
-    }
+    // validate and build everything before touching the handle: a bad scenario leaves it as it was
     std::vector<d2d::Scn> tab((size_t)n_scn);
     for (int k = 0; k < n_scn; ++k) {
         if (!d2d::scn_build(scns[k], tab[k]))
             return fail(D2D_E_ARG, "d2d_set_scenarios: us[n_wps-2] - us[n_wps-3] must exceed 0.001");
     }
+    DeviceGuard g(h->device);
+    hipError_t e;
+    d2d::Scn* scn = nullptr;
+    d2d::BrTab* brt = nullptr;
+    auto drop = [&](hipError_t err, const char* what) {
+        if (scn) (void)hipFree(scn);
+        if (brt) (void)hipFree(brt);
+        return hip_fail(err, what);
+    };
+    // pool mode: room for a second pool half (d2d_refresh_pool), zero until the first refresh
+    const size_t T = (size_t)n_scn * (h->cfg.scn_pool ? 2 : 1);
     const size_t bytes = sizeof(d2d::Scn) * (size_t)n_scn;
-    if ((e = hipMalloc(&h->scn, bytes)) != hipSuccess) return hip_fail(e, "hipMalloc scn");
-    if ((e = hipMemcpy(h->scn, tab.data(), bytes, hipMemcpyHostToDevice)) != hipSuccess)
-        return hip_fail(e, "hipMemcpy scn");
+    if ((e = hipMalloc(&scn, sizeof(d2d::Scn) * T)) != hipSuccess) return drop(e, "hipMalloc scn");
+    if ((e = hipMemset(scn, 0, sizeof(d2d::Scn) * T)) != hipSuccess) return drop(e, "hipMemset scn");
+    if ((e = hipMemcpy(scn, tab.data(), bytes, hipMemcpyHostToDevice)) != hipSuccess) return drop(e, "hipMemcpy scn");
     // golden-march tables: forced searches on the device (same arithmetic as the step kernels)
-    const size_t tbytes = sizeof(d2d::BrTab) * (size_t)n_scn;
-    if ((e = hipMalloc(&h->brt, tbytes)) != hipSuccess) return hip_fail(e, "hipMalloc brt");
-    if ((e = hipMemset(h->brt, 0, tbytes)) != hipSuccess) return hip_fail(e, "hipMemset brt");
-    hipLaunchKernelGGL(d2d_brtab_kernel, dim3((2 * n_scn + 63) / 64), dim3(64), 0, 0, h->scn, n_scn, h->brt);
-    if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "d2d_brtab_kernel launch");
-    if ((e = hipDeviceSynchronize()) != hipSuccess) return hip_fail(e, "d2d_brtab_kernel");
-    if (env_scn_host) {
-        if ((e = hipMemcpy(h->env_scn, env_scn_host, sizeof(int32_t) * (size_t)h->n, hipMemcpyHostToDevice)) !=
-            hipSuccess)
-            return hip_fail(e, "hipMemcpy env_scn");
-    } else if ((e = hipMemset(h->env_scn, 0, sizeof(int32_t) * (size_t)h->n)) != hipSuccess) {
-        return hip_fail(e, "hipMemset env_scn");
-    }
+    if ((e = hipMalloc(&brt, sizeof(d2d::BrTab) * T)) != hipSuccess) return drop(e, "hipMalloc brt");
+    if ((e = hipMemset(brt, 0, sizeof(d2d::BrTab) * T)) != hipSuccess) return drop(e, "hipMemset brt");
+    hipLaunchKernelGGL(d2d_brtab_kernel, dim3((2 * n_scn + 63) / 64), dim3(64), 0, 0, scn, n_scn, brt);
+    if ((e = hipGetLastError()) != hipSuccess) return drop(e, "d2d_brtab_kernel launch");
+    if ((e = hipMemset(h->pool_dev, 0, sizeof(int32_t))) != hipSuccess) return drop(e, "hipMemset pool");
+    if ((e = hipDeviceSynchronize()) != hipSuccess) return drop(e, "d2d_brtab_kernel");
     // slot layout: grouped for a static mixed map (pool mode redraws scenarios at every reset);
     // the current state moves into the new layout
     std::vector<int32_t> lanes, ws;
     if (D2D_GROUP && env_scn_host && n_scn > 1 && !h->cfg.scn_pool) make_groups(h->n, env_scn_host, n_scn, lanes, ws);
-    if (!lanes.empty() || h->lane_env) {
-        Layout from = take_layout(h), to;
-        if ((e = alloc_layout(to, h->n, lanes, ws)) != hipSuccess) return hip_fail(e, "d2d_set_scenarios: layout");
-        if ((e = move_state(from, to, h->n)) != hipSuccess) {
+    Layout to;
+    const bool relayout = !lanes.empty() || h->lane_env;
+    if (relayout) {
+        if ((e = alloc_layout(to, h->n, lanes, ws)) != hipSuccess) return drop(e, "d2d_set_scenarios: layout");
+        if ((e = move_state(take_layout(h), to, h->n)) != hipSuccess) {
             free_layout(to);
-            return hip_fail(e, "d2d_set_scenarios: layout move");
+            return drop(e, "d2d_set_scenarios: layout move");
         }
+    }
+    // commit: from here on the handle holds the new scenarios
+    if (relayout) {
+        Layout from = take_layout(h);
         put_layout(h, to);
         free_layout(from);
     }
-    h->n_scn = n_scn;
+    if (h->scn) (void)hipFree(h->scn);
+    if (h->brt) (void)hipFree(h->brt);
+    h->scn = scn;
+    h->brt = brt;
+    h->n_scn = (int)T;
+    h->pool_base = 0;
+    h->pool_n = n_scn;
     h->rc_dirty = true;  // cached reset observations belong to the old scenarios
+    e = env_scn_host ? hipMemcpy(h->env_scn, env_scn_host, sizeof(int32_t) * (size_t)h->n, hipMemcpyHostToDevice)
+                     : hipMemset(h->env_scn, 0, sizeof(int32_t) * (size_t)h->n);
+    if (e != hipSuccess) {
+        // the env -> scenario map is unknown: no step or reset until the next d2d_set_scenarios
+        h->n_scn = 0;
+        h->reset_done = false;
+        return hip_fail(e, "d2d_set_scenarios: env_scn upload");
+    }
     return D2D_OK;
 }
 
@@ -401,7 +424,7 @@ int32_t d2d_step(d2d_t* h, const float* act_dev, float* obs_dev, float* rew_dev,
                  uint8_t* trunc_dev, float* info_dev, float* term_obs_dev, void* stream) {
     if (!h || !act_dev || !obs_dev || !rew_dev || !term_dev || !trunc_dev)
         return fail(D2D_E_ARG, "d2d_step: null handle or required buffer");
-    if (!h->reset_done) return fail(D2D_E_STATE, "d2d_step: call d2d_reset first");
+    if (h->n_scn <= 0 || !h->reset_done) return fail(D2D_E_STATE, "d2d_step: call d2d_set_scenarios and d2d_reset first");
     if (((uintptr_t)act_dev & 7u) != 0) return fail(D2D_E_ARG, "d2d_step: act_dev must be 8-byte aligned");
     DeviceGuard g(h->device);
     hipError_t e;
@@ -463,6 +486,7 @@ int32_t d2d_get_state(d2d_t* h, double* state_dev, int32_t* istate_dev, void* st
 
 int32_t d2d_set_state(d2d_t* h, const double* state_dev, const int32_t* istate_dev, void* stream) {
     if (!h) return fail(D2D_E_ARG, "d2d_set_state: null handle");
+    if (h->n_scn <= 0) return fail(D2D_E_STATE, "d2d_set_state: call d2d_set_scenarios first");
     DeviceGuard g(h->device);
     hipError_t e;
     const size_t n = (size_t)h->n;
@@ -486,6 +510,77 @@ int32_t d2d_set_state(d2d_t* h, const double* state_dev, const int32_t* istate_d
     }
     if ((e = rc_rebuild(h, (hipStream_t)stream)) != hipSuccess) return hip_fail(e, "d2d_set_state: cache rebuild");
     h->reset_done = true;
+    return D2D_OK;
+}
+
+int32_t d2d_refresh_pool(d2d_t* h, const d2d_scn* scns, int32_t n_scn) {
+    if (!h || !scns) return fail(D2D_E_ARG, "d2d_refresh_pool: null handle/scenarios");
+    if (!h->cfg.scn_pool) return fail(D2D_E_ARG, "d2d_refresh_pool: pool mode only (cfg.scn_pool = 1)");
+    if (h->n_scn <= 0) return fail(D2D_E_STATE, "d2d_refresh_pool: call d2d_set_scenarios first");
+    if (n_scn != h->pool_n) return fail(D2D_E_ARG, "d2d_refresh_pool: n_scn must equal the pool size");
+    std::vector<d2d::Scn> tab((size_t)n_scn);
+    for (int k = 0; k < n_scn; ++k) {
+        const d2d_scn& s = scns[k];
+        if (s.n_wps < 3 || s.n_wps > D2D_MAX_WPS || s.n_circles < 0 || s.n_circles > D2D_MAX_CIRCLES ||
+            !d2d::scn_build(s, tab[k]))
+            return fail(D2D_E_ARG, "d2d_refresh_pool: invalid scenario");
+    }
+    DeviceGuard g(h->device);
+    hipError_t e;
+    const size_t P = (size_t)n_scn;
+    const int half = h->pool_base == 0 ? n_scn : 0;
+    // the half about to be overwritten must not hold a running episode (one that started before the
+    // previous refresh): episodes last at most cfg.n_steps steps, so refreshes further apart are safe
+    std::vector<int32_t> es((size_t)h->n);
+    if ((e = hipDeviceSynchronize()) != hipSuccess ||  // in-flight steps may still draw from the old half
+        (e = hipMemcpy(es.data(), h->env_scn, sizeof(int32_t) * es.size(), hipMemcpyDeviceToHost)) != hipSuccess)
+        return hip_fail(e, "d2d_refresh_pool: read env_scn");
+    int busy = 0;
+    for (int32_t v : es) busy += (v >= half && v < half + n_scn);
+    if (busy)
+        return fail(D2D_E_STATE, "d2d_refresh_pool: " + std::to_string(busy) +
+                                     " envs still run episodes from the pool before the previous refresh");
+    if ((e = hipMemcpy(h->scn + half, tab.data(), P * sizeof(d2d::Scn), hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemset(h->brt + half, 0, P * sizeof(d2d::BrTab))) != hipSuccess)
+        return hip_fail(e, "d2d_refresh_pool: upload");
+    hipLaunchKernelGGL(d2d_brtab_kernel, dim3((2 * n_scn + 63) / 64), dim3(64), 0, 0, h->scn + half, n_scn, h->brt + half);
+    if ((e = hipGetLastError()) != hipSuccess || (e = hipDeviceSynchronize()) != hipSuccess)
+        return hip_fail(e, "d2d_refresh_pool: d2d_brtab_kernel");
+    if ((e = hipMemcpy(h->pool_dev, &half, sizeof(int32_t), hipMemcpyHostToDevice)) != hipSuccess)
+        return hip_fail(e, "d2d_refresh_pool: switch");
+    h->pool_base = half;
+    // cached next-episode observations were drawn from the old half: drop and refill now (a
+    // captured graph replays d2d_step's kernels without the host-side rebuild check)
+    if ((e = rc_rebuild(h, nullptr)) != hipSuccess || (e = hipDeviceSynchronize()) != hipSuccess)
+        return hip_fail(e, "d2d_refresh_pool: cache rebuild");
+    return D2D_OK;
+}
+
+int32_t d2d_get_env_scenarios(d2d_t* h, int32_t* env_scn_dev, void* stream) {
+    if (!h || !env_scn_dev) return fail(D2D_E_ARG, "d2d_get_env_scenarios: null handle/out");
+    DeviceGuard g(h->device);
+    hipError_t e = hipMemcpyAsync(env_scn_dev, h->env_scn, sizeof(int32_t) * (size_t)h->n, hipMemcpyDeviceToDevice,
+                                  (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(e, "d2d_get_env_scenarios");
+    return D2D_OK;
+}
+
+int32_t d2d_set_env_scenarios(d2d_t* h, const int32_t* env_scn_dev, void* stream) {
+    if (!h || !env_scn_dev) return fail(D2D_E_ARG, "d2d_set_env_scenarios: null handle/map");
+    if (!h->cfg.scn_pool)
+        return fail(D2D_E_ARG, "d2d_set_env_scenarios: pool mode only (change a static map with d2d_set_scenarios)");
+    if (h->n_scn <= 0) return fail(D2D_E_STATE, "d2d_set_env_scenarios: call d2d_set_scenarios first");
+    DeviceGuard g(h->device);
+    const hipStream_t s = (hipStream_t)stream;
+    std::vector<int32_t> m((size_t)h->n);
+    hipError_t e = hipMemcpyAsync(m.data(), env_scn_dev, sizeof(int32_t) * m.size(), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return hip_fail(e, "d2d_set_env_scenarios: read map");
+    for (int32_t v : m)
+        if (v < 0 || v >= h->n_scn) return fail(D2D_E_ARG, "d2d_set_env_scenarios: scenario index out of range");
+    if ((e = hipMemcpyAsync(h->env_scn, m.data(), sizeof(int32_t) * m.size(), hipMemcpyHostToDevice, s)) != hipSuccess ||
+        (e = hipStreamSynchronize(s)) != hipSuccess)
+        return hip_fail(e, "d2d_set_env_scenarios");
     return D2D_OK;
 }
 

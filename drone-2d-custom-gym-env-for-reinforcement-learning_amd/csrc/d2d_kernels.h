@@ -71,6 +71,9 @@ struct StepArgs {
     const Scn* scn;          // [n_scn]
     const BrTab* brt;        // [n_scn] golden-march tables (d2d_brtab_kernel), or null
     int32_t* env_scn;        // [n] or null (all scenario 0); rewritten at resets in pool mode
+    const int32_t* pool_base;  // pool mode: resets draw from scenarios [*pool_base, *pool_base + pool_n);
+    int pool_n;                // d2d_refresh_pool switches *pool_base between the two table halves
+                               // (device memory, so captured graphs follow a refresh)
     d2d_cfg cfg;
     double damping_dt;       // pow(cfg.damping, dt), host glibc
     uint64_t seed;
@@ -240,9 +243,12 @@ __device__ __forceinline__ bool flag_seen(const uint32_t& f) {
     return __builtin_amdgcn_readfirstlane(*(const volatile LdsU32*)&f) != 0u;
 }
 // scenario of the episode that follows episode counter `ep` of env j (curriculum pool: a fresh draw)
+__device__ __forceinline__ int pool_scenario(const StepArgs& a, int j, uint32_t ep) {
+    return *a.pool_base + (a.pool_n > 1 ? pool_pick(a.seed, (uint32_t)a.cfg.env_id_base + (uint32_t)j, ep, a.pool_n) : 0);
+}
 __device__ __forceinline__ int next_scenario(const StepArgs& a, int j, uint32_t ep) {
+    if (a.cfg.scn_pool) return pool_scenario(a, j, ep);
     if (a.n_scn <= 1) return 0;
-    if (a.cfg.scn_pool) return pool_pick(a.seed, (uint32_t)a.cfg.env_id_base + (uint32_t)j, ep, a.n_scn);
     return a.env_scn[j];
 }
 
@@ -795,9 +801,8 @@ __global__ __launch_bounds__(BLOCK) void d2d_reset_kernel(StepArgs a) {
     if (a.mask && !a.mask[ie]) return;
     const int n = a.ns;
     int si = (a.env_scn && a.n_scn > 1) ? a.env_scn[ie] : 0;
-    if (a.cfg.scn_pool && a.n_scn > 1) {
-        si = pool_pick(a.seed, (uint32_t)a.cfg.env_id_base + (uint32_t)ie, (uint32_t)fld(a.ist, D2D_I_EPISODE, n, i),
-                       a.n_scn);
+    if (a.cfg.scn_pool) {
+        si = pool_scenario(a, ie, (uint32_t)fld(a.ist, D2D_I_EPISODE, n, i));
         a.env_scn[ie] = si;
     }
     const Scn& s = scns[si];

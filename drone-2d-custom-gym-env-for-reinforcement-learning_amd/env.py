@@ -179,6 +179,28 @@ class Drone2dVecEnv:
         self._upload_scenarios()
         return self.reset()
 
+    def refresh_curriculum(self, seed: int | None = None, stage: str | None = None, sim_num: int | None = None):
+        """Replace the curriculum pool by a fresh draw of the same size WITHOUT stopping the running
+        episodes (``d2d_refresh_pool``): resets from now on draw from the new pool, episodes that
+        started earlier finish on their own scenarios.  ``seed`` defaults to the previous pool seed
+        + 1; ``stage`` / ``sim_num`` optionally move the curriculum on (the reference applies a new
+        stage at each env's next reset, drone_2d_env.py:76-86).  Refresh at most once per
+        ``n_steps`` steps (the library refuses while an env still runs an episode from the pool
+        before the previous refresh)."""
+        if not self.cfg.scn_pool:
+            raise ValueError("refresh_curriculum needs an env created in curriculum mode (mode='curriculum')")
+        kw = dict(self.kwargs, mode="curriculum")
+        if stage is not None:
+            kw["scenario"] = stage
+        elif sim_num is not None:
+            kw["scenario"] = "curriculum"
+            kw["sim_num"] = int(sim_num)
+        kw["curriculum_seed"] = int(seed) if seed is not None else int(kw.get("curriculum_seed", 0)) + 1
+        scns = build_scenarios(kw)
+        arr = (abi.D2DScn * len(scns))(*[s.to_c() for s in scns])
+        check(self._lib.d2d_refresh_pool(self._h, arr, len(scns)), "d2d_refresh_pool")
+        self.kwargs, self.scenarios = kw, scns
+
     def _stream(self):
         return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
@@ -250,6 +272,36 @@ class Drone2dVecEnv:
         check(self._lib.d2d_set_state(self._h, self._ptr(st), self._ptr(ist), self._stream()), "d2d_set_state")
         self._keep = (st, ist)
 
+    def get_env_scenarios(self) -> torch.Tensor:
+        """int32 [N]: each env's current scenario index (in curriculum pool mode every reset redraws it)."""
+        es = torch.empty(self.num_envs, dtype=torch.int32, device=self.device)
+        check(self._lib.d2d_get_env_scenarios(self._h, self._ptr(es), self._stream()), "d2d_get_env_scenarios")
+        return es
+
+    def set_env_scenarios(self, env_scn: torch.Tensor):
+        """Restore the per-env scenario indices of a checkpoint (curriculum pool mode only)."""
+        es = torch.as_tensor(env_scn).to(self.device, torch.int32).contiguous()
+        if es.shape != (self.num_envs,):
+            raise ValueError("env_scn must have shape [num_envs]")
+        check(self._lib.d2d_set_env_scenarios(self._h, self._ptr(es), self._stream()), "d2d_set_env_scenarios")
+
+    def state_dict(self) -> dict:
+        """Checkpoint of the running batch: physics/bookkeeping state, per-env scenario indices and
+        the spawn seed (the reference has no resume path)."""
+        st, ist = self.get_state()
+        return {"state": st, "istate": ist, "env_scn": self.get_env_scenarios(), "seed": self.seed_value}
+
+    def load_state_dict(self, sd: dict):
+        """Restore a ``state_dict()`` into a batch built with the same kwargs (and, in pool mode,
+        the same curriculum pool): episodes continue exactly where they were."""
+        self.seed_value = int(sd["seed"])
+        self.reset()  # installs the seed for later auto-resets; the state is overwritten below
+        if self.cfg.scn_pool:
+            self.set_env_scenarios(sd["env_scn"])
+        elif not torch.equal(torch.as_tensor(sd["env_scn"]).cpu(), self.get_env_scenarios().cpu()):
+            raise ValueError("checkpoint env -> scenario map differs from this batch's (static map)")
+        self.set_state(sd["state"], sd["istate"])
+
     def episode_stats(self, clear: bool = True) -> torch.Tensor:
         """float64 [8]: (sum return, episodes, successes, fails, collisions, sum APE, sum len, 0)."""
         check(self._lib.d2d_episode_stats(self._h, self._ptr(self._stats), 1 if clear else 0, self._stream()),
@@ -257,8 +309,13 @@ class Drone2dVecEnv:
         return self._stats
 
 
-def info_dicts(info_row: np.ndarray, n_obstacles: int) -> dict:
-    """Rebuild the reference's ``info`` dict (drone_2d_env.py:575-613) from one info row."""
+def info_dicts(info_row: np.ndarray, n_obstacles: int | None = None) -> dict:
+    """Rebuild the reference's ``info`` dict (drone_2d_env.py:575-613) from one info row.
+
+    ``dist_closest_obs`` is taken as the kernel wrote it: +inf for an obstacle-free scenario
+    (drone_2d_env.py:587), so it is right for every env even in curriculum pool mode, where the
+    scenario changes at every reset.  ``n_obstacles`` is accepted for compatibility and unused.
+    """
     cause = int(info_row[abi.INFO_CAUSE])
     d = {
         "reward": float(info_row[abi.INFO_REWARD]),
@@ -269,7 +326,7 @@ def info_dicts(info_row: np.ndarray, n_obstacles: int) -> dict:
         "reach_end_reward": float(info_row[abi.INFO_REACH]),
         "agressive_alpha_reward": float(info_row[abi.INFO_AA]),
         "env_steps": int(info_row[abi.INFO_STEPS]),
-        "dist_closest_obs": float(info_row[abi.INFO_DCLOSE]) if n_obstacles else float("inf"),
+        "dist_closest_obs": float(info_row[abi.INFO_DCLOSE]),
         "APE": 0, "total_reward": 0, "n_collisions": 0, "n_successful_runs": 0, "n_failed_runs": 0,
         "flight_path": 0,
     }
@@ -307,7 +364,6 @@ class Drone2dEnv:
                                    **{k: v for k, v in kwargs.items() if k != "seed"})
         self.action_space = self._venv.action_space
         self.observation_space = self._venv.observation_space
-        self._n_obs = len(self._venv.scenarios[0].circles)
         self.flight_path = []
         self._done = False
         self.reset()  # the reference spawns in __init__ (drone_2d_env.py:144)
@@ -329,7 +385,7 @@ class Drone2dEnv:
         o = obs[0].double().cpu().numpy()
         r = float(rew[0].item())
         done = bool(term[0].item() or trunc[0].item()) or self._done  # self.done is sticky (:594)
-        d = info_dicts(info[0].cpu().numpy(), self._n_obs)
+        d = info_dicts(info[0].cpu().numpy())
         if self.kwargs.get("render_path"):
             st, _ = self._venv.get_state()
             x, y = float(st[0, 0]), float(st[1, 0])

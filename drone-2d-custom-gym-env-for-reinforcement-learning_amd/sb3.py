@@ -77,8 +77,6 @@ class SB3VecEnv(_Base):
             backend = Drone2dVecEnv(num_envs, device=device, seed=seed, auto_reset=True, with_info=True, **kwargs)
         self.venv = backend
         self.infos_mode = infos
-        self._n_obstacles = [len(s.circles) for s in self.venv.scenarios]
-        self._env_scn = np.asarray(self.venv.env_scenario) if self.venv.env_scenario is not None else None
         self._actions = None
         if _VecEnvBase is not None:  # pragma: no cover
             super().__init__(num_envs, self.venv.observation_space, self.venv.action_space)
@@ -109,7 +107,7 @@ class SB3VecEnv(_Base):
         tobs_np = tobs[torch.as_tensor(idx, device=tobs.device)].cpu().numpy() if len(idx) else None
         if self.infos_mode == "full":
             rows = info.cpu().numpy()
-            infos = [info_dicts(rows[i], self._nobs(i)) for i in range(self.num_envs)]
+            infos = [info_dicts(rows[i]) for i in range(self.num_envs)]
             for d in infos:
                 d["TimeLimit.truncated"] = False  # set below for finished envs (truncated and not terminated)
         else:
@@ -117,7 +115,7 @@ class SB3VecEnv(_Base):
             if self.infos_mode == "done" and len(idx):
                 rows = info[torch.as_tensor(idx, device=info.device)].cpu().numpy()
                 for k, i in enumerate(idx):
-                    infos[i] = info_dicts(rows[k], self._nobs(i))
+                    infos[i] = info_dicts(rows[k])
         for k, i in enumerate(idx):
             infos[i]["TimeLimit.truncated"] = bool(trunc_np[i])
             infos[i]["terminal_observation"] = tobs_np[k]
@@ -147,9 +145,6 @@ class SB3VecEnv(_Base):
         return [False for _ in self._indices(indices)]
 
     # ---------------------------------------------------------------- helpers
-    def _nobs(self, i):
-        return self._n_obstacles[0] if self._env_scn is None else self._n_obstacles[int(self._env_scn[i])]
-
     def _indices(self, indices):
         if indices is None:
             return range(self.num_envs)

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define D2D_ABI_VERSION 2
+#define D2D_ABI_VERSION 3
 
 #define D2D_MAX_WPS 16                    /* largest test path: 'large' has 14 waypoints   */
 #define D2D_MAX_SEGS (D2D_MAX_WPS - 2)    /* QPMI2D fits n_wps-2 quadratics (predef_path.py:34) */
@@ -176,6 +176,25 @@ int32_t d2d_step(d2d_t* h, const float* act_dev, float* obs_dev, float* rew_dev,
  * state_dev: float64 [D2D_NSTATE][n_envs], istate_dev: int32 [D2D_NISTATE][n_envs]. */
 int32_t d2d_get_state(d2d_t* h, double* state_dev, int32_t* istate_dev, void* stream);
 int32_t d2d_set_state(d2d_t* h, const double* state_dev, const int32_t* istate_dev, void* stream);
+
+/* Curriculum pool mode only: replace the pool by n_scn fresh scenarios (n_scn = the size given to
+ * d2d_set_scenarios) without stopping the running episodes.  The handle keeps two pool halves:
+ * the new scenarios go into the half not used by the current pool, resets from now on draw from it,
+ * and episodes that started earlier finish on their own scenarios.  Returns D2D_E_STATE if an env
+ * still runs an episode drawn before the previous refresh (refresh at most once per cfg.n_steps
+ * steps).  Synchronises the device.  (The reference draws a fresh path and obstacle set at every
+ * curriculum reset, drone_2d_env.py:199-215, 324-372; refreshing the pool regularly approaches
+ * that distribution.) */
+int32_t d2d_refresh_pool(d2d_t* h, const d2d_scn* scns, int32_t n_scn);
+
+/* Checkpointing in curriculum pool mode (cfg.scn_pool = 1), where every reset rewrites the env's
+ * scenario index: copy the per-env scenario map (int32 [n_envs], env order) out of / into the handle,
+ * alongside d2d_get_state / d2d_set_state, so a restored episode continues on its own path and
+ * obstacles (the reference keeps them in the env object until reset, drone_2d_env.py:199-215).
+ * d2d_set_env_scenarios is for pool mode only (a static map is changed by d2d_set_scenarios, which
+ * re-lays the state out) and synchronises `stream` to range-check the indices on the host. */
+int32_t d2d_get_env_scenarios(d2d_t* h, int32_t* env_scn_dev, void* stream);
+int32_t d2d_set_env_scenarios(d2d_t* h, const int32_t* env_scn_dev, void* stream);
 
 /* Reduce the per-env finished-episode accumulators into out_dev (float64 [D2D_NSTATS]) with a
  * fixed-order (bitwise reproducible) block reduction; clear != 0 zeroes the accumulators after. */

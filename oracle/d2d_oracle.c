@@ -556,7 +556,8 @@ struct d2dcpu {
     d2d_cfg cfg;
     int n;
     d2d_scn* scn;
-    int n_scn;
+    int n_scn;     /* table size: pool mode 2 x pool_n (two halves, d2dcpu_refresh_pool) */
+    int pool_base, pool_n;
     int32_t* env_scn;
     double* st;    /* [NSTATE][n] */
     int32_t* ist;  /* [NISTATE][n] */
@@ -579,11 +580,29 @@ void d2dcpu_destroy(d2dcpu_t* h) {
     free(h->st); free(h->ist); free(h->acc); free(h->env_scn); free(h->scn); free(h);
 }
 int32_t d2dcpu_set_scenarios(d2dcpu_t* h, const d2d_scn* s, int32_t n_scn, const int32_t* env_scn) {
+    const int T = n_scn * (h->cfg.scn_pool ? 2 : 1);
     free(h->scn);
-    h->scn = (d2d_scn*)malloc(sizeof(d2d_scn) * (size_t)n_scn);
+    h->scn = (d2d_scn*)calloc((size_t)T, sizeof(d2d_scn));
     memcpy(h->scn, s, sizeof(d2d_scn) * (size_t)n_scn);
-    h->n_scn = n_scn;
+    h->n_scn = T;
+    h->pool_base = 0;
+    h->pool_n = n_scn;
     for (int i = 0; i < h->n; ++i) h->env_scn[i] = env_scn ? env_scn[i] : 0;
+    return 0;
+}
+
+/* pool mode: new scenarios into the half not in use, later resets draw from it (d2d_refresh_pool) */
+int32_t d2dcpu_refresh_pool(d2dcpu_t* h, const d2d_scn* s, int32_t n_scn) {
+    if (!h->cfg.scn_pool || n_scn != h->pool_n) return D2D_E_ARG;
+    const int half = h->pool_base == 0 ? n_scn : 0;
+    for (int i = 0; i < h->n; ++i)
+        if (h->env_scn[i] >= half && h->env_scn[i] < half + n_scn) return D2D_E_STATE;
+    memcpy(h->scn + half, s, sizeof(d2d_scn) * (size_t)n_scn);
+    h->pool_base = half;
+    return 0;
+}
+int32_t d2dcpu_get_env_scenarios(const d2dcpu_t* h, int32_t* out) {
+    memcpy(out, h->env_scn, sizeof(int32_t) * (size_t)h->n);
     return 0;
 }
 
@@ -604,9 +623,9 @@ static void write_obs(float* dst, const double* obs) {
 /* test-mode reset of env i (drone_2d_env.py:218-311 + Drone.py:20-52 + reset :908-912) */
 static void o_reset_env(d2dcpu_t* h, int i, float* obs_out) {
     uint32_t ep = (uint32_t)h->ist[(size_t)D2D_I_EPISODE * h->n + i];
-    if (h->cfg.scn_pool && h->n_scn > 1)
-        h->env_scn[i] = (int32_t)d2dcpu_pool_pick(h->seed, (uint32_t)h->cfg.env_id_base + (uint32_t)i, ep,
-                                                  (uint32_t)h->n_scn);
+    if (h->cfg.scn_pool)  /* the current pool half (d2dcpu_refresh_pool) */
+        h->env_scn[i] = h->pool_base + (h->pool_n > 1 ? (int32_t)d2dcpu_pool_pick(h->seed,
+                            (uint32_t)h->cfg.env_id_base + (uint32_t)i, ep, (uint32_t)h->pool_n) : 0);
     const d2d_scn* s = &h->scn[h->env_scn[i]];
     double u[3];
     d2dcpu_spawn_uniforms(h->seed, (uint32_t)h->cfg.env_id_base + (uint32_t)i, ep, u);

@@ -12,6 +12,8 @@ typedef struct d2dcpu d2dcpu_t;
 d2dcpu_t* d2dcpu_create(const d2d_cfg* cfg, int32_t n_envs);
 void d2dcpu_destroy(d2dcpu_t* h);
 int32_t d2dcpu_set_scenarios(d2dcpu_t* h, const d2d_scn* scns, int32_t n_scn, const int32_t* env_scn);
+int32_t d2dcpu_refresh_pool(d2dcpu_t* h, const d2d_scn* scns, int32_t n_scn);
+int32_t d2dcpu_get_env_scenarios(const d2dcpu_t* h, int32_t* env_scn);
 int32_t d2dcpu_reset(d2dcpu_t* h, const uint8_t* mask, uint64_t seed, float* obs);
 int32_t d2dcpu_step(d2dcpu_t* h, const float* act, float* obs, float* rew, uint8_t* term,
                     uint8_t* trunc, float* info, float* term_obs);

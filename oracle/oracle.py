@@ -46,6 +46,8 @@ def load() -> C.CDLL:
             "d2dcpu_destroy": (None, [VP]),
             "d2dcpu_set_scenarios": (I32, [VP, P(abi.D2DScn), I32, VP]),
             "d2dcpu_reset": (I32, [VP, VP, C.c_uint64, VP]),
+            "d2dcpu_refresh_pool": (I32, [VP, P(abi.D2DScn), I32]),
+            "d2dcpu_get_env_scenarios": (I32, [VP, VP]),
             "d2dcpu_step": (I32, [VP, VP, VP, VP, VP, VP, VP, VP]),
             "d2dcpu_step_mt": (I32, [VP, VP, VP, VP, VP, VP, VP, VP, I32]),
             "d2dcpu_get_state": (I32, [VP, VP, VP]),
@@ -127,6 +129,16 @@ class OracleBatch:
         st = np.ascontiguousarray(st, dtype=np.float64)
         ist = np.ascontiguousarray(ist, dtype=np.int32)
         self.lib.d2dcpu_set_state(self.h, _p(st), _p(ist))
+
+    def refresh_pool(self, scenarios_c) -> int:
+        arr = (self.abi.D2DScn * len(scenarios_c))(*scenarios_c)
+        self._scn_refresh = arr
+        return self.lib.d2dcpu_refresh_pool(self.h, arr, len(scenarios_c))
+
+    def get_env_scenarios(self):
+        out = np.zeros(self.n, np.int32)
+        self.lib.d2dcpu_get_env_scenarios(self.h, _p(out))
+        return out
 
     def episode_stats(self, clear=True):
         out = np.zeros(self.abi.NSTATS, np.float64)

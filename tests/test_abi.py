@@ -68,7 +68,7 @@ def test_hip_library_exports_every_header_symbol(hip_lib):
     for f in header_functions():
         assert hasattr(hip_lib, f), f
         assert f in _native.SIGNATURES, f  # and the ctypes binding declares it
-    assert hip_lib.d2d_abi_version() == abi.ABI_VERSION == 2
+    assert hip_lib.d2d_abi_version() == abi.ABI_VERSION == 3
 
 
 def test_hip_library_is_gfx950(d2):

@@ -40,7 +40,7 @@ def _run(backend, acts):
     return torch.stack(obs_all), torch.stack(rew_all), backend.episode_stats()
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, hip=False):
     import sys
 
     here = os.path.dirname(os.path.abspath(__file__))
@@ -57,9 +57,14 @@ def _worker(rank, world, port, out_dir):
     assert (r, w) == (rank, world)
     off, cnt = shard.shard_range(N_TOTAL, world, rank)
     es = shard.shard_env_scenario(shard.global_env_scenario(N_TOTAL, len(SCN)), off, cnt)
-    be = OracleVecBackend(cnt, seed=21, env_scenario=es, env_id_offset=off, **_kw())
+    if hip:  # this rank's HIP shard (every rank on cuda:0 of a one-GPU box; gloo for the gathers)
+        be = shard.make_shard_venv(N_TOTAL, rank, world, device=torch.device("cuda", 0), seed=21, **_kw())
+        assert be.cfg.env_id_base == off and np.array_equal(be.env_scenario, es)
+    else:
+        be = OracleVecBackend(cnt, seed=21, env_scenario=es, env_id_offset=off, **_kw())
     obs, rew, stats = _run(be, _actions()[:, off:off + cnt])
-    stats = shard.allreduce_stats(stats.clone())
+    obs, rew = obs.cpu(), rew.cpu()
+    stats = shard.allreduce_stats(stats.clone().cpu())
     # gather the per-env outputs (uneven shards: pad to the largest block)
     big = shard.shard_range(N_TOTAL, world, 0)[1]
     pad_o = torch.zeros(STEPS, big, 27)
@@ -101,22 +106,41 @@ def test_shard_range_partitions():
         shard_range(3, 4, 0)
 
 
-def test_two_rank_gloo_sharding_matches_single_batch(tmp_path, d2):
-    from oracle_backend import OracleVecBackend
-
+def _sharded(tmp_path, hip):
     world = 2
     ctx = mp.get_context("spawn")
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, str(tmp_path))) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, str(tmp_path), hip)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
         p.join(timeout=300)
         assert p.exitcode == 0
-    got = torch.load(os.path.join(tmp_path, "sharded.pt"), weights_only=True)
+    return torch.load(os.path.join(tmp_path, "sharded.pt"), weights_only=True)
+
+
+def test_two_rank_gloo_sharding_matches_single_batch(tmp_path, d2):
+    from oracle_backend import OracleVecBackend
+
+    got = _sharded(tmp_path, hip=False)
     single = OracleVecBackend(N_TOTAL, seed=21, **_kw())
     obs, rew, stats = _run(single, _actions())
     single.close()
+    _check(got, obs, rew, stats)
+
+
+@pytest.mark.gpu
+def test_two_process_hip_shards_match_single_batch(tmp_path, d2):
+    """Two processes, each stepping its HIP shard (env_id_offset, sliced scenario map) through
+    libdrone2d_hip.so, gathered over gloo: identical to one unsharded HIP batch, bit for bit."""
+    got = _sharded(tmp_path, hip=True)
+    single = d2.Drone2dVecEnv(N_TOTAL, device=torch.device("cuda", 0), seed=21, **_kw())
+    obs, rew, stats = _run(single, _actions())
+    single.close()
+    _check(got, obs.cpu(), rew.cpu(), stats.cpu())
+
+
+def _check(got, obs, rew, stats):
     assert torch.equal(got["obs"], obs)
     assert torch.equal(got["rew"], rew)
     # per-env accumulators are identical; the reduction order differs (block sums), so compare the
