@@ -10,7 +10,7 @@ class OracleVecBackend:
 
         import drone2d_amd  # noqa: F401
         from drone2d_amd.config import make_cfg
-        from drone2d_amd.env import _make_box, build_scenarios
+        from drone2d_amd.env import _make_box, build_scenarios, is_curriculum
 
         oracle.build()
         self.kwargs = dict(kwargs)
@@ -21,6 +21,7 @@ class OracleVecBackend:
         self.env_scenario = np.ascontiguousarray(np.asarray(env_scenario, dtype=np.int32))
         self.cfg = make_cfg(dict(self.kwargs), auto_reset=True, timeup_truncates=timeup_truncates,
                             env_id_base=env_id_offset)
+        self.cfg.scn_pool = 1 if is_curriculum(self.kwargs) else 0  # as Drone2dVecEnv
         self.orc = oracle.OracleBatch(self.cfg, [s.to_c() for s in self.scenarios], self.num_envs,
                                       env_scenario=self.env_scenario)
         self.seed_value = int(seed)

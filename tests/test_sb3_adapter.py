@@ -123,3 +123,29 @@ def test_adapter_hip_matches_oracle(d2):
     assert dones_total > 0
     hip.close()
     ref.close()
+
+
+def test_dist_closest_obs_in_curriculum_pool(d2):
+    """Curriculum pool mode redraws each env's scenario at every reset (some stage_3 entries have
+    no obstacles): info['dist_closest_obs'] must be the kernel's value for the episode's own
+    scenario (+inf without obstacles), not one looked up from the initial env -> scenario map."""
+    from drone2d_amd import abi
+
+    n = 128
+    kw = _kw(scenario="stage_3", mode="curriculum", curriculum_pool=32, curriculum_seed=3)
+    be = OracleVecBackend(n, seed=5, **kw)
+    n_free = sum(len(s.circles) == 0 for s in be.scenarios)
+    assert 0 < n_free < len(be.scenarios)
+    env = _adapter(be, "done")
+    env.reset()
+    rng = np.random.default_rng(0)
+    seen = {True: 0, False: 0}
+    for _ in range(400):
+        env.step_async(rng.uniform(-1, 1, (n, 2)).astype(np.float32))
+        _, _, dones, infos = env.step_wait()
+        rows = be.orc.info
+        for i in np.nonzero(dones)[0]:
+            d = infos[i]["dist_closest_obs"]
+            assert d == float(rows[i, abi.INFO_DCLOSE]) or (np.isinf(d) and np.isinf(rows[i, abi.INFO_DCLOSE]))
+            seen[bool(np.isinf(d))] += 1
+    assert seen[True] > 0 and seen[False] > 0
