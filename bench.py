@@ -69,9 +69,12 @@ def parse():
 def setup_dist(args):
     from drone2d_amd import shard
 
-    rank, world, local = shard.init_process_group_from_env("nccl")
-    if world == 1:
-        torch.cuda.set_device(0)
+    # RCCL ("nccl") between GPUs; D2D_BENCH_BACKEND=gloo rehearses the multi-rank path with every
+    # rank on the one GPU of a single-GPU box (RCCL refuses two ranks on one device)
+    backend = os.environ.get("D2D_BENCH_BACKEND", "nccl")
+    rank, world, local = shard.init_process_group_from_env(backend)
+    if world == 1 or backend != "nccl":
+        torch.cuda.set_device(local % torch.cuda.device_count())
     return rank, world, local
 
 

@@ -335,8 +335,17 @@ __device__ __forceinline__ bool brent_active(const Brent& B) {
 #ifndef D2D_PAR_BALLOT
 #define D2D_PAR_BALLOT 1  // brent_step: the parabolic candidate only when some lane of the wave takes it
 #endif
+#ifndef D2D_COPYSIGN
+#define D2D_COPYSIGN 1  // the step's sign by copysign (bitfield insert) instead of compare + select
+#endif
+#ifndef D2D_KTRACK
+#define D2D_KTRACK 0  // 1: the state carries the knots us[ia + 1], us[ixf + 1]; 0: us[ia + 1] re-read from the table
+#endif
 __device__ __forceinline__ void brent_step(const Scn& s, const PathK& K, double px, double py, Brent& B) {
     const double a = B.a, b = B.b, xf = B.xf, fx = B.fx, nfc = B.nfc, fulc = B.fulc;
+    // the upper knot of a's interval, for the one-compare interval test below (issued first: its
+    // LDS latency hides behind the candidate computation)
+    const double ka = D2D_KTRACK ? B.ka : s.rec[REC_U1][B.ia];
     const double xm = 0.5 * (a + b);
     const double tol1 = BR_SQRT_EPS * fabs(xf) + BR_XATOL3;
     const double tol2 = 2.0 * tol1;
@@ -366,12 +375,14 @@ __device__ __forceinline__ void brent_step(const Scn& s, const PathK& K, double 
     // parabolic step is taken only when |p/q| < |e|/2), so np.max's NaN rule never applies and the
     // product is exactly -mx for rat < 0 and +mx otherwise
     const double mx = fmax(fabs(rat), tol1);
-    const double x = xf + ((rat < 0.0) ? -mx : mx);
+    // (rat is never -0: e_g = a - xf or b - xf is +0 at worst, the parabolic step is p + 0.0 over
+    // |q| or tol1 times a nonzero sign, so copysign gives the same -mx / +mx)
+    const double x = xf + (D2D_COPYSIGN ? copysign(mx, rat) : ((rat < 0.0) ? -mx : mx));
     // knot interval of x: one compare once the bracket spans <= 2 intervals (wave-uniform choice)
     const bool fast = (x >= a) & (x <= b) & (B.ib <= B.ia + 1);
     int ix;
     if (__ballot(!fast) == 0ull) {
-        ix = min(B.ia + ((x <= B.ka) ? 0 : 1), K.nw - 1);
+        ix = min(B.ia + ((x <= ka) ? 0 : 1), K.nw - 1);
     } else {
         // the knot scan re-reads the knots each time (an opaque pointer stops the compiler from
         // keeping all 15 in registers across the loop: the fast path does not need them)
@@ -391,14 +402,16 @@ __device__ __forceinline__ void brent_step(const Scn& s, const PathK& K, double 
     const bool to_a = le == ge;
     const double t = le ? xf : x;
     const int ti = le ? B.ixf : ix;
-    const double tk = le ? B.kxf : kx;
     B.a = to_a ? t : a;
     B.b = to_a ? b : t;
     B.ia = to_a ? ti : B.ia;
-    B.ka = to_a ? tk : B.ka;
     B.ib = to_a ? B.ib : ti;
     B.ixf = le ? ix : B.ixf;
-    B.kxf = le ? kx : B.kxf;
+    if (D2D_KTRACK) {
+        const double tk = le ? B.kxf : kx;
+        B.ka = to_a ? tk : B.ka;
+        B.kxf = le ? kx : B.kxf;
+    }
     const double nfulc = (le | c1) ? nfc : (c2 ? x : fulc);
     const double nffulc = (le | c1) ? B.fnfc : (c2 ? fu : B.ffulc);
     const double nnfc = le ? xf : (c1 ? x : nfc);
@@ -831,6 +844,9 @@ __device__ __forceinline__ Arms make_arms(const double cs[3], const double sn[3]
 
 // stage 2.  pos = {frame px, py, left px, py, right px, py} (post position update); vel[9] =
 // (vx, vy, w) of frame, left, right; j[12] the accumulated pivot impulses.
+#ifndef D2D_SWEEP_UNROLL
+#define D2D_SWEEP_UNROLL 1  // unroll factor of the 10-sweep loop (2: no loop-carried register moves)
+#endif
 constexpr int JB_PER_JOINT = 5;  // K^-1 (a, b = c, d) + bias (x, y)
 template <bool JBUF>
 __device__ __forceinline__ void phys_velocities(const Arms& A, const double pos[6], double damping_dt, double fx,
@@ -891,7 +907,7 @@ __device__ __forceinline__ void phys_velocities(const Arms& A, const double pos[
         vel[2] += II_F * (r2x * jy - r2y * jx);
     }
     // 10 sequential-impulse sweeps (Space.iterations default)
-#pragma unroll 1
+#pragma unroll D2D_SWEEP_UNROLL
     for (int it = 0; it < ((D2D_ABLATE & 4) ? 0 : 10); ++it) {
 #pragma unroll
         for (int k = 0; k < 6; ++k) {
