@@ -51,8 +51,9 @@ constexpr double VEL_MAX = 1330.0;            // drone_2d_env.py:635
 //   per-lane base (field-major, so lanes in different intervals hit different LDS banks) instead
 //   of the scattered coefficient gathers: the "B" quadratic min(n, nseg-1), the "A" quadratic of
 //   the blend (n-1, or the last one for n = 0: Python's x_params[-1]), us[n], us[n+1] and
-//   RN(1 / (us[n+1] - us[n])).
-enum { REC_XB = 0, REC_XA = 6, REC_U0 = 12, REC_U1 = 13, REC_IDU = 14, REC_N = 15 };
+//   RN(1 / (us[n+1] - us[n])), and the blend threshold T: in interval n QPMI2D.__call__ blends the
+//   two quadratics exactly when u < T[n] (below).
+enum { REC_XB = 0, REC_XA = 6, REC_U0 = 12, REC_U1 = 13, REC_IDU = 14, REC_T = 15, REC_N = 16 };
 struct Scn {
     int32_t n_wps, n_circles;
     double us[D2D_MAX_WPS];
@@ -81,6 +82,15 @@ inline bool scn_build(const d2d_scn& a, Scn& s) {
         s.rec[REC_U0][n] = s.us[n];
         s.rec[REC_U1][n] = s.us[n1];
         s.rec[REC_IDU][n] = 1.0 / (s.us[n1] - s.us[n]);
+        // predef_path.py:88-142 per interval n = u_index(u): "first" (u in [us[0], us[1]], B only),
+        // "last" (u in [us[-2] - 0.001, us[-1]] or n == nw-1, B only), else the blend.  For n < nw-1
+        // u <= us[n+1] <= L, so last <=> u >= last_lo; for n = 0, first <=> u >= us[0].  Hence blend
+        // <=> u < T[n] with T[0] = min(us[0], last_lo), T[0 < n < nw-1] = last_lo, T[nw-1] = -inf
+        // (also for NaN u, which u_index maps to nw-1).  scn_build's check above keeps last_lo
+        // inside interval nw-3.
+        const double last_lo = s.us[nw - 2] - 0.001;
+        s.rec[REC_T][n] = (n == 0) ? (s.us[0] < last_lo ? s.us[0] : last_lo)
+                                   : (n < nw - 1 ? last_lo : -__builtin_inf());
     }
     for (int k = 0; k < D2D_MAX_CIRCLES; ++k) {
         s.cx[k] = a.cx[k];
@@ -253,15 +263,10 @@ __device__ __forceinline__ PathK path_k(const Scn& s) {
 // and the reference's case analysis picks the result with selects (same arithmetic per case).
 // first <=> n == 0 && u >= us[0];  last <=> u in [us[nw-2] - 0.001, L] or n == nw-1, and in every
 // first / last case the record's "B" quadratic is the one the reference uses (scn_build).
-__device__ __forceinline__ void path_eval_n(const Scn& s, const PathK& K, double u, int n, double& x, double& y,
-                                            double& u1_out) {
-    const int nw = K.nw;
-    double r[REC_N];
-#pragma unroll
-    for (int f = 0; f < REC_N; ++f) r[f] = s.rec[f][n];
-    const bool first = (n == 0) & (u >= K.us0);
-    const bool last = !first & (((u >= K.last_lo) & (u <= K.L)) | (n == nw - 1));
-    const bool blend = !first & !last;
+__device__ __forceinline__ void path_eval_rec(const double r[REC_N], const PathK& K, double u, int n, double& x,
+                                              double& y, double& u1_out) {
+    // the reference's first / last / blend case analysis as one compare (scn_build, REC_T)
+    const bool blend = u < r[REC_T];
     const double uu = u * u;
     const double xB = r[REC_XB + 0] * uu + r[REC_XB + 1] * u + r[REC_XB + 2];
     const double yB = r[REC_XB + 3] * uu + r[REC_XB + 4] * u + r[REC_XB + 5];
@@ -275,6 +280,13 @@ __device__ __forceinline__ void path_eval_n(const Scn& s, const PathK& K, double
     x = blend ? xb : xB;
     y = blend ? yb : yB;
     u1_out = u1;
+}
+__device__ __forceinline__ void path_eval_n(const Scn& s, const PathK& K, double u, int n, double& x, double& y,
+                                            double& u1_out) {
+    double r[REC_N];
+#pragma unroll
+    for (int f = 0; f < REC_N; ++f) r[f] = s.rec[f][n];
+    path_eval_rec(r, K, u, n, x, y, u1_out);
 }
 __device__ __forceinline__ void path_eval(const Scn& s, const PathK& K, double u, double& x, double& y) {
     double u1;
@@ -335,6 +347,9 @@ __device__ __forceinline__ bool brent_active(const Brent& B) {
 #ifndef D2D_PAR_BALLOT
 #define D2D_PAR_BALLOT 1  // brent_step: the parabolic candidate only when some lane of the wave takes it
 #endif
+#ifndef D2D_RECPF
+#define D2D_RECPF 0  // brent_step reads the record of a's interval before the candidate is known
+#endif
 #ifndef D2D_COPYSIGN
 #define D2D_COPYSIGN 1  // the step's sign by copysign (bitfield insert) instead of compare + select
 #endif
@@ -343,9 +358,15 @@ __device__ __forceinline__ bool brent_active(const Brent& B) {
 #endif
 __device__ __forceinline__ void brent_step(const Scn& s, const PathK& K, double px, double py, Brent& B) {
     const double a = B.a, b = B.b, xf = B.xf, fx = B.fx, nfc = B.nfc, fulc = B.fulc;
-    // the upper knot of a's interval, for the one-compare interval test below (issued first: its
-    // LDS latency hides behind the candidate computation)
-    const double ka = D2D_KTRACK ? B.ka : s.rec[REC_U1][B.ia];
+    // the record of a's interval, read first: once the bracket lies in one knot interval (most of
+    // a continuation) the probe falls in it, and the LDS latency hides behind the candidate
+    // computation instead of following it.  Its upper knot serves the one-compare interval test.
+    double rp[REC_N];
+    if (D2D_RECPF) {
+#pragma unroll
+        for (int f = 0; f < REC_N; ++f) rp[f] = s.rec[f][B.ia];
+    }
+    const double ka = D2D_KTRACK ? B.ka : (D2D_RECPF ? rp[REC_U1] : s.rec[REC_U1][B.ia]);
     const double xm = 0.5 * (a + b);
     const double tol1 = BR_SQRT_EPS * fabs(xf) + BR_XATOL3;
     const double tol2 = 2.0 * tol1;
@@ -363,7 +384,10 @@ __device__ __forceinline__ void brent_step(const Scn& s, const PathK& K, double 
     if (!D2D_PAR_BALLOT || __ballot(par) != 0ull) {
         rat_p = div_normal(p + 0.0, q);
         const double xp = xf + rat_p;
-        rat_p = (((xp - a) < tol2) | ((b - xp) < tol2)) ? tol1 * sgn_nz(xm - xf) : rat_p;
+        // tol1 * (np.sign(d) + (d == 0)) for d = xm - xf: a, b and xf are finite (the initial
+        // bracket and finite steps), so d is not NaN and the product is -tol1 for d < 0, else +tol1
+        const double d = xm - xf;
+        rat_p = (((xp - a) < tol2) | ((b - xp) < tol2)) ? ((d < 0.0) ? -tol1 : tol1) : rat_p;
     }
     // golden-section candidate
     const double e_g = (xf >= xm) ? a - xf : b - xf;
@@ -390,8 +414,18 @@ __device__ __forceinline__ void brent_step(const Scn& s, const PathK& K, double 
         asm volatile("" : "+v"(sp));
         ix = u_index(*sp, x);
     }
-    double kx;
-    const double fu = path_dist_n(s, K, x, ix, px, py, kx);
+    double kx, fu;
+    if (D2D_RECPF) {
+        double xq, yq;
+        if (__ballot(ix != B.ia) != 0ull) {
+#pragma unroll
+            for (int f = 0; f < REC_N; ++f) rp[f] = (ix != B.ia) ? s.rec[f][ix] : rp[f];
+        }
+        path_eval_rec(rp, K, x, ix, xq, yq, kx);
+        fu = norm2(xq - px, yq - py);
+    } else {
+        fu = path_dist_n(s, K, x, ix, px, py, kx);
+    }
     B.num += 1;
     const bool le = fu <= fx;
     const bool c1 = !le & ((fu <= B.fnfc) | (nfc == xf));
