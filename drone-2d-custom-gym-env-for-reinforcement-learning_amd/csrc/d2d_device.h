@@ -796,10 +796,22 @@ __device__ __forceinline__ void advance_position(Body& b) {
     b.py = b.py + (b.vy + 0.0) * DT;
     b.a = b.a + (b.w + 0.0) * DT;
 }
+#ifndef D2D_COLL_CULL
+#define D2D_COLL_CULL 1  // skip a circle for the whole wave when it is out of reach of every lane's frame
+#endif
 __device__ __forceinline__ bool frame_hits(const Scn& s, const Body& F, double cs, double sn) {
     bool hit = false;
     for (int k = 0; k < ((D2D_ABLATE & 8) ? 0 : s.n_circles); ++k) {
         const double dx = s.cx[k] - F.px, dy = s.cy[k] - F.py;
+        if (D2D_COLL_CULL) {
+            // every point of the box is within sqrt(50^2 + 5^2) = 50.25 of its center, so a center
+            // offset of at least r + 51.25 on either axis puts the circle beyond r of the box: the
+            // exact test below would say "no contact" for this lane.  Steady state: ~8 % of the
+            // (wave, circle) pairs of corridor, ~5 % of S_corridor's, have a lane in reach.
+            const double reach = s.cr[k] + 51.25;
+            const bool near = (fabs(dx) < reach) & (fabs(dy) < reach);
+            if (__ballot(near) == 0ull) continue;
+        }
         const double lx = dx * cs + dy * sn;
         const double ly = -dx * sn + dy * cs;
 #if D2D_SENSE_MINAXIS
@@ -878,6 +890,9 @@ __device__ __forceinline__ Arms make_arms(const double cs[3], const double sn[3]
 
 // stage 2.  pos = {frame px, py, left px, py, right px, py} (post position update); vel[9] =
 // (vx, vy, w) of frame, left, right; j[12] the accumulated pivot impulses.
+#ifndef D2D_ZERO_ARM
+#define D2D_ZERO_ARM 1  // joint sweep: skip the signed-zero terms of the motor-centre pivots
+#endif
 #ifndef D2D_SWEEP_UNROLL
 #define D2D_SWEEP_UNROLL 1  // unroll factor of the 10-sweep loop (2: no loop-carried register moves)
 #endif
@@ -963,7 +978,14 @@ __device__ __forceinline__ void phys_velocities(const Arms& A, const double pos[
                 ka = kk[kq][0]; kb = kk[kq][1]; kd = kk[kq][2]; bx = kk[kq][3]; by = kk[kq][4];
             }
             const double kc = kb;
-            const double v1x = vel[3 * m + 0] + (-r1y) * vel[3 * m + 2], v1y = vel[3 * m + 1] + r1x * vel[3 * m + 2];
+            // the middle pivots (k = 1, 4) sit at the motor's centre: r1 = (+0, +0), so the motor's
+            // perp(r1) * w terms and its angular impulse are signed zeros.  Adding a signed zero
+            // leaves a velocity unchanged unless it is -0, and velocities are never -0 here (the
+            // gravity / force update adds +0 or a nonzero term, sums of nonzero terms round to +0,
+            // never -0); they are dropped for finite states (ZERO_ARM)
+            const bool za = D2D_ZERO_ARM && (k % 3 == 1);
+            const double v1x = za ? vel[3 * m + 0] : vel[3 * m + 0] + (-r1y) * vel[3 * m + 2];
+            const double v1y = za ? vel[3 * m + 1] : vel[3 * m + 1] + r1x * vel[3 * m + 2];
             const double v2x = vel[0] + (-r2y) * vel[2], v2y = vel[1] + r2x * vel[2];
             const double ux = bx - (v2x - v1x), uy = by - (v2y - v1y);
             double jx = ux * ka + uy * kb;
@@ -976,7 +998,7 @@ __device__ __forceinline__ void phys_velocities(const Arms& A, const double pos[
             jy = ny - oy;
             vel[3 * m + 0] = vel[3 * m + 0] + (-jx) * MI_M;
             vel[3 * m + 1] = vel[3 * m + 1] + (-jy) * MI_M;
-            vel[3 * m + 2] += II_M * (r1x * (-jy) - r1y * (-jx));
+            if (!za) vel[3 * m + 2] += II_M * (r1x * (-jy) - r1y * (-jx));
             vel[0] = vel[0] + jx * MI_F;
             vel[1] = vel[1] + jy * MI_F;
             vel[2] += II_F * (r2x * jy - r2y * jx);
