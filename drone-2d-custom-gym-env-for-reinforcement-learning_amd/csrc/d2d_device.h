@@ -61,7 +61,8 @@ struct Scn {
     double cx[D2D_MAX_CIRCLES], cy[D2D_MAX_CIRCLES], cr[D2D_MAX_CIRCLES];
     double wp_last_x, wp_last_y;
     double spawn_xmin, spawn_xmax, spawn_ymin, spawn_ymax, spawn_amin, spawn_amax;
-    double pad;  // sizeof(Scn) % 16 == 0: the probe tables staged after the scenarios stay 16-B aligned
+    double r_uniform;  // the common radius when every circle has the same one (all test scenarios), else NaN
+                       // (also keeps sizeof(Scn) % 16 == 0: the probe tables staged after it stay aligned)
 };
 static_assert(sizeof(Scn) % 16 == 0, "Scn size");
 // Returns false if the table is outside what the record form reproduces exactly: the last-segment
@@ -105,6 +106,12 @@ inline bool scn_build(const d2d_scn& a, Scn& s) {
     s.spawn_ymax = a.spawn_ymax;
     s.spawn_amin = a.spawn_amin;
     s.spawn_amax = a.spawn_amax;
+    s.r_uniform = __builtin_nan("");
+    if (a.n_circles > 0) {
+        bool same = true;
+        for (int k = 1; k < a.n_circles; ++k) same = same && (a.cr[k] == a.cr[0]);
+        if (same) s.r_uniform = a.cr[0];
+    }
     return true;
 }
 // a / b correctly rounded from y = RN(1/b) (Markstein): q = RN(a*y) is within 1 ulp of a/b, the
@@ -236,6 +243,9 @@ __device__ __forceinline__ void spawn_draw(const Scn& s, uint64_t seed, uint32_t
 // n_wps - 1 as the loop does.  No compare masks, so the 15 knot tests issue back to back.
 #ifndef D2D_SENSE_MINAXIS
 #define D2D_SENSE_MINAXIS 1  // circle distances / frame contact with min / max instead of selects
+#endif
+#ifndef D2D_SENSE_SQ
+#define D2D_SENSE_SQ 1   // uniform-radius obstacle sets: top-3 by squared distance, 4 square roots per env
 #endif
 #ifndef D2D_KNOT_CMP
 #define D2D_KNOT_CMP 1   // 1: compares (measured faster in the full kernel), 0: sign bits (faster alone)
@@ -1077,7 +1087,50 @@ __device__ __forceinline__ void sensor_pos(const d2d_cfg& cfg, const Scn& s, dou
     double bd0 = __builtin_inf(), bd1 = __builtin_inf(), bd2 = __builtin_inf();
     int bi0 = -1, bi1 = -1, bi2 = -1;
     const int nc = (D2D_ABLATE & 2) ? 0 : s.n_circles;
-    for (int i = 0; i < nc; ++i) {
+    bool full = true;
+    if (D2D_SENSE_SQ && s.r_uniform == s.r_uniform) {
+        // every circle has radius r: d = sqrt(q) - r is non-decreasing in the squared distance q,
+        // so the stable top-3 by d is the stable top-3 by q unless two of the candidates round to
+        // the same d (then the reference's index order among them can differ from q's order).
+        // Keep the top 4 by q, take the 4 square roots, and fall back to the reference loop below
+        // on any equal d among them -- otherwise every circle outside has d >= d4 > d3.
+        const double r = s.r_uniform;
+        double q0 = __builtin_inf(), q1 = __builtin_inf(), q2 = __builtin_inf(), q3 = __builtin_inf();
+        int i0 = -1, i1 = -1, i2 = -1, i3 = -1;
+        for (int i = 0; i < nc; ++i) {
+            const double cx = s.cx[i], cy = s.cy[i];
+            const double ax = (50.0 + x) - cx, bxx = (-50.0 + x) - cx;
+            const double ay = (-5.0 + y) - cy, byy = (5.0 + y) - cy;
+            const double mx = fmin(fabs(ax), fabs(bxx)), my = fmin(fabs(ay), fabs(byy));
+            const double q = mx * mx + my * my;
+            const bool l0 = (i0 < 0) || q < q0, l1 = (i1 < 0) || q < q1, l2 = (i2 < 0) || q < q2,
+                       l3 = (i3 < 0) || q < q3;
+            q3 = l2 ? q2 : (l3 ? q : q3);
+            i3 = l2 ? i2 : (l3 ? i : i3);
+            q2 = l1 ? q1 : (l2 ? q : q2);
+            i2 = l1 ? i1 : (l2 ? i : i2);
+            q1 = l0 ? q0 : (l1 ? q : q1);
+            i1 = l0 ? i0 : (l1 ? i : i1);
+            q0 = l0 ? q : q0;
+            i0 = l0 ? i : i0;
+        }
+        const double d0 = sqrt_dist(q0) - r, d1 = sqrt_dist(q1) - r, d2 = sqrt_dist(q2) - r,
+                     d3 = sqrt_dist(q3) - r;
+        const bool tie = ((i1 >= 0) & (d1 == d0)) | ((i2 >= 0) & (d2 == d1)) | ((i3 >= 0) & (d3 == d2)) |
+                         (x != x) | (y != y);
+        full = tie;
+        bd0 = i0 >= 0 ? d0 : bd0;
+        bd1 = i1 >= 0 ? d1 : bd1;
+        bd2 = i2 >= 0 ? d2 : bd2;
+        bi0 = i0;
+        bi1 = i1;
+        bi2 = i2;
+    }
+    if (full) {
+        bd0 = bd1 = bd2 = __builtin_inf();
+        bi0 = bi1 = bi2 = -1;
+    }
+    for (int i = 0; i < (full ? nc : 0); ++i) {
         const double cx = s.cx[i], cy = s.cy[i];
         const double ax = (50.0 + x) - cx, bxx = (-50.0 + x) - cx;
         const double ay = (-5.0 + y) - cy, byy = (5.0 + y) - cy;

@@ -374,3 +374,43 @@ def test_closest_point_grid_bitwise(d2):
     o_st2 = orc.get_state()[0]
     np.testing.assert_array_equal(st2[abi.S_PATH_ERR], o_st2[abi.S_PATH_ERR])
     venv.close()
+
+
+@pytest.mark.parametrize("radii", ["uniform", "mixed"])
+def test_sensing_ties_and_radii(d2, radii):
+    """Nearest-circle sensing: circles placed in mirror pairs (and a quad) around x = 600, frames on
+    the mirror axis, so pairs of circles are exactly equidistant -- the squared-distance top-3 must
+    fall back to the reference's index order on equal distances; with mixed radii the reference
+    loop runs throughout.  HIP vs the oracle, teacher-forced."""
+    import oracle
+    from drone2d_amd.config import make_cfg
+    from drone2d_amd.scenarios import Scenario
+
+    base = d2.Drone2dVecEnv(1, **_cfgkw("corridor")).scenarios[0]
+    cs = [(500.0, 600.0), (700.0, 600.0), (500.0, 800.0), (700.0, 800.0), (600.0, 400.0), (450.0, 700.0),
+          (750.0, 700.0), (600.0, 1000.0)]
+    r = [30.0] * len(cs) if radii == "uniform" else [30.0, 30.0, 25.0, 35.0, 30.0, 20.0, 20.0, 40.0]
+    circ = np.array([(x, y, rr) for (x, y), rr in zip(cs, r)])
+    scn = Scenario("mirror", base.wps, base.path, circ, (590.0, 610.0, 550.0, 850.0), base.spawn_angle)
+    n = 512
+    kw = dict(_cfgkw(), scenario=[scn])
+    venv = d2.Drone2dVecEnv(n, seed=5, auto_reset=False, **kw)
+    orc = oracle.OracleBatch(make_cfg(dict(kw), auto_reset=False), [scn.to_c()], n)
+    venv.reset()
+    orc.reset(5)
+    st, ist = (x.cpu().numpy() for x in venv.get_state())
+    rng = np.random.default_rng(3)
+    st[0] = 600.0                                   # frame exactly on the mirror axis
+    st[1] = rng.uniform(450.0, 950.0, n)
+    st[1][:64] = 700.0                              # ... and on the horizontal mirror line
+    st[2] = rng.uniform(-0.3, 0.3, n)
+    for f in (3, 4, 5, 9, 10, 11, 15, 16, 17):
+        st[f] = 0.0
+    c, s_ = np.cos(st[2]), np.sin(st[2])
+    st[6], st[7], st[8] = 600.0 - 40 * c, st[1] - 40 * s_, st[2]
+    st[12], st[13], st[14] = 600.0 + 40 * c, st[1] + 40 * s_, st[2]
+    venv.set_state(torch.as_tensor(st), torch.as_tensor(ist))
+    act = np.zeros((n, 2), np.float32)              # hover-ish: positions barely move
+    worst = compare_step(venv, orc, act)
+    assert worst < OBS_ATOL
+    venv.close()
