@@ -3,7 +3,7 @@
 # gpurun_out/configs_TAG.jsonl.  Each run has its own time limit; any failure ends the script.
 # Usage: bash tools/configs.sh TAG
 set -u
-TAG=${1:-r01}
+TAG=${1:-r02}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/configs_$TAG.jsonl
 : > "$OUT"

@@ -3,7 +3,7 @@
 # counters in separate passes (never combined with sys/runtime traces), on the eager step loop.
 # Usage: bash tools/profile.sh TAG     -> gpurun_out/prof_TAG/...
 set -u
-TAG=${1:-r01}
+TAG=${1:-r02}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p "$OUT"

@@ -11,7 +11,7 @@ cd /tmp
 for T in "$@"; do
   timeout -k 10 300 rocprofv3 --kernel-include-regex d2d_step_kernel -T --output-format csv -d "$OUT/$T" -o pmc \
     --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES -- \
-    python3 "$R/tools/variants.py" run "$T" --rounds 1 > "$OUT/$T.log" 2>&1 || { echo "STOP $T"; exit 1; }
+    python3 "$R/tools/variants.py" run "$T" --rounds 1 --steps 40 --warmup 300 > "$OUT/$T.log" 2>&1 || { echo "STOP $T"; exit 1; }
 done
 python3 - "$OUT" "$@" <<'PY'
 import csv, glob, os, sys
