@@ -125,6 +125,9 @@ struct StepArgs {
 #ifndef D2D_SPLIT
 #define D2D_SPLIT 1      // W3 re-checks the second half of W2's golden-march table (0: W2 alone)
 #endif
+#ifndef D2D_OBS_VEC
+#define D2D_OBS_VEC 1    // K1 stores its observation tile with 16-byte stores
+#endif
 #ifndef D2D_FILL_COMPACT
 #define D2D_FILL_COMPACT 1  // K4 compacts the envs that need a fill into the leading lanes
 #endif
@@ -280,7 +283,7 @@ struct K1Shared {
         struct {
             double pre[4][EPB];            // W0 -> W2: RewardVel
             double post[7][EPB];           // W2 -> W0: reward, pa, pp, dist, aa, coll, reach
-            float obs[EPB * D2D_OBS_DIM];  // the workgroup's obs rows
+            alignas(16) float obs[EPB * D2D_OBS_DIM];  // the workgroup's obs rows (16-B aligned: float4 stores)
         } p;                               // after f_gs
     } u;
 };
@@ -707,7 +710,16 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, Scn* s_scn, K1Shared&
         const int rows = max(0, min(EPB, a.n - e0));  // (D2D_ABLATE & 32: timing-only slot-order rows)
         const int words = rows * D2D_OBS_DIM;
         float* dst = a.obs + (size_t)e0 * D2D_OBS_DIM;
-        for (int k = threadIdx.x; k < words; k += K1_THREADS) dst[k] = sh.u.p.obs[k];
+        // a full tile is 64 x 27 floats = 432 float4 at a 16-B aligned offset (e0 * 108 B, e0 % 64
+        // == 0; the caller's obs buffer is a torch allocation): 16-byte stores
+        int k0 = 0;
+        if (D2D_OBS_VEC && rows == EPB && ((uintptr_t)a.obs & 15u) == 0) {
+            float4* d4 = reinterpret_cast<float4*>(dst);
+            const float4* s4 = reinterpret_cast<const float4*>(sh.u.p.obs);
+            for (int k = threadIdx.x; k < words / 4; k += K1_THREADS) d4[k] = s4[k];
+            k0 = words;
+        }
+        for (int k = k0 + threadIdx.x; k < words; k += K1_THREADS) dst[k] = sh.u.p.obs[k];
     }
     if (wave == 0 && valid) {
         path_err = sh.pe[0][lane];
