@@ -722,6 +722,22 @@ __device__ __forceinline__ double closest_u_tab(const Scn& s, const BrTab& T, co
 // split point of the two-wave re-check: the first wave checks steps [1, bt_split), the second
 // [bt_split, len) (from its own window, bt_window)
 __device__ __forceinline__ int bt_split(const BrTab& T) { return max(4, (T.len[0] + 3) / 2); }
+// three-way split: part p in {0, 1, 2} checks steps [bt_third(p), bt_third(p + 1)) (bt_third(0) = 1,
+// bt_third(3) = BT_K), as the fill kernel splits it
+__device__ __forceinline__ int bt_third(const BrTab& T, int p) {
+    const int third = (T.len[0] + 2) / 3;
+    return p == 0 ? 1 : (p >= 3 ? BT_K : 1 + p * third);
+}
+// the window before step k0 for a search that followed the table so far, from the snapshot's probe
+// indices (valid for every k0, also before step 4 of a kind-0 march)
+template <bool LT>
+__device__ __forceinline__ void bt_window_snap(const BrTab& T, const BtHot* hot, BtLane& L, int k0, double px,
+                                               double py) {
+    const BtSnap& W = T.snap[L.kind][k0];
+    L.fa = bt_dist<LT>(hot, L.kind, W.j_fulc, px, py);
+    L.fb = bt_dist<LT>(hot, L.kind, W.j_nfc, px, py);
+    L.fc = bt_dist<LT>(hot, L.kind, W.j_xf, px, py);
+}
 
 // ------------------------------------------------------------------------------ bodies / physics
 // One cpSpaceStep(1/60) of the Drone.py body/joint configuration, split in

@@ -122,6 +122,9 @@ struct StepArgs {
 #ifndef D2D_STRADDLE_LDS
 #define D2D_STRADDLE_LDS 1  // a grouped-layout workgroup straddling two scenarios stages both in LDS
 #endif
+#ifndef D2D_SPLIT3
+#define D2D_SPLIT3 0     // 1: W2, W1 and W3 re-check one third each of the golden-march table (needs D2D_SPLIT)
+#endif
 #ifndef D2D_SPLIT
 #define D2D_SPLIT 1      // W3 re-checks the second half of W2's golden-march table (0: W2 alone)
 #endif
@@ -273,7 +276,7 @@ struct K1Shared {
                               // then W2 -> W0: LA-lock bit after the path role
     uint32_t ep[EPB];         // W0 -> W1, W3: episode counter (the state's copy changes at a reset)
     double sina[EPB];         // W0 -> W2: sin of the post-step frame angle (AA reward)
-    uint32_t f_done, f_ca, f_gs, f_pre, f_ver;
+    uint32_t f_done, f_ca, f_gs, f_pre, f_ver, f_ver1;
     double pe[2][EPB];        // W3 -> W0: path_err, total_reward (prefetched for the epilogue)
     union {
         struct {
@@ -327,6 +330,7 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, Scn* s_scn, K1Shared&
         if (LTAB) hots = stage_hot<K1_THREADS>(a, reinterpret_cast<BtHot*>(s_scn + ncopy), s0, ncopy);
     }
     if (wave == 0) sh.scn[lane] = (valid && a.env_scn && a.n_scn > 1) ? a.env_scn[ie] : s0;
+    if (D2D_SPLIT3 && wave == 0) sh.pflags[lane] = 0x7fffffffu;  // W1 and W3 min their table parts in
     // state loads issued before the staging barrier, so their HBM latency overlaps the staging:
     // W0 the whole state + action, the other roles the frame
     Body PB[3]{};
@@ -362,6 +366,7 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, Scn* s_scn, K1Shared&
         sh.f_gs = 0u;
         sh.f_pre = 0u;
         sh.f_ver = 0u;
+        sh.f_ver1 = 0u;
     }
     __syncthreads();
     STAMP(1);
@@ -493,9 +498,30 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, Scn* s_scn, K1Shared&
         flag_raise(sh.f_pre);
     } else if (wave == 1) {
         // ---------------------------------------------------------------- sensing
-        D2D_SETPRIO(D2D_PRIO_W1);
         float row[19];
         bool need = false;
+        if (D2D_SPLIT3) {
+            // the middle third of W2's golden-march re-check first, at W2's priority (its critical path)
+            __builtin_amdgcn_s_setprio(D2D_PRIO_W2);
+            if (valid && !(D2D_ABL & 4) && !(D2D_ABLATE & 1) && a.brt) {
+                const BrTab& T = a.brt[sh.scn[lane]];
+                const BtHot* hot = LTAB ? hots + sh.scn[lane] : &T.hot;
+                Body F = (D2D_PREFETCH & 2) ? PB[0] : load_frame(a, i);
+                advance_position(F);
+                BtLane L = bt_start<LTAB>(T, hot, F.px, F.py);
+                const int k0 = bt_third(T, 1), k1 = bt_third(T, 2);
+                if (k0 < min(k1, L.len)) {
+                    if (k0 >= 4) bt_window<LTAB>(hot, L, k0, F.px, F.py);
+                else bt_window_snap<LTAB>(T, hot, L, k0, F.px, F.py);
+                    bt_verify<LTAB>(hot, L, k0, k1, F.px, F.py);
+                }
+                atomicMin(&sh.pflags[lane], (uint32_t)L.dev);
+            }
+            flag_raise(sh.f_ver1);
+            __builtin_amdgcn_s_setprio(D2D_PRIO_W1);
+        } else {
+            D2D_SETPRIO(D2D_PRIO_W1);
+        }
         if (valid && !(D2D_ABL & 2)) {
             Body F = (D2D_PREFETCH & 2) ? PB[0] : load_frame(a, i);
             advance_position(F);
@@ -567,8 +593,9 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, Scn* s_scn, K1Shared&
                 // golden-march re-check of steps [1, split); W3 checks [split, len) meanwhile
                 const BtHot* hot = LTAB ? hots + sh.scn[lane] : &T->hot;
                 BtLane L = bt_start<LTAB>(*T, hot, F.px, F.py);
-                bt_verify<LTAB>(hot, L, 1, bt_split(*T), F.px, F.py);
+                bt_verify<LTAB>(hot, L, 1, D2D_SPLIT3 ? bt_third(*T, 1) : bt_split(*T), F.px, F.py);
                 flag_wait(sh.f_ver);
+                if (D2D_SPLIT3) flag_wait(sh.f_ver1);
                 L.dev = min(L.dev, (int)sh.pflags[lane]);
                 int iu;
                 const double u = bt_finish<LTAB>(S, *T, hot, L.kind, L.dev, F.px, F.py, iu);
@@ -632,12 +659,14 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, Scn* s_scn, K1Shared&
             Body F = load_frame(a, i);
             advance_position(F);
             BtLane L = bt_start<LTAB>(T, hot, F.px, F.py);
-            const int k0 = bt_split(T);
+            const int k0 = D2D_SPLIT3 ? bt_third(T, 2) : bt_split(T);
             if (k0 < L.len) {
-                bt_window<LTAB>(hot, L, k0, F.px, F.py);
+                if (k0 >= 4) bt_window<LTAB>(hot, L, k0, F.px, F.py);
+                else bt_window_snap<LTAB>(T, hot, L, k0, F.px, F.py);
                 bt_verify<LTAB>(hot, L, k0, BT_K, F.px, F.py);
             }
-            sh.pflags[lane] = (uint32_t)L.dev;
+            if (D2D_SPLIT3) atomicMin(&sh.pflags[lane], (uint32_t)L.dev);
+            else sh.pflags[lane] = (uint32_t)L.dev;
         }
         flag_raise(sh.f_ver);
         if (D2D_SPLIT) __builtin_amdgcn_s_setprio(D2D_PRIO_W3);
