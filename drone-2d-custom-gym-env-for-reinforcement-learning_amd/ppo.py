@@ -49,11 +49,15 @@ class PPOConfig:
     vf_coef: float = 0.5
     max_grad_norm: float = 0.5
     normalize_advantage: bool = True
+    graph: bool = True              # GPU, one rank: the minibatch update replayed as one HIP graph
 
     @classmethod
     def gpu_defaults(cls, **over) -> "PPOConfig":
         """Short rollouts over many envs (65 536 x 16 = 1 M samples per update), big minibatches."""
         return cls(**dict(dict(n_steps=16, batch_size=32768), **over))
+
+
+_HALF_LOG_2PI = 0.5 * math.log(2.0 * math.pi)
 
 
 class ActorCritic(nn.Module):
@@ -82,12 +86,20 @@ class ActorCritic(nn.Module):
         return mean, value
 
     def dist(self, mean: torch.Tensor) -> torch.distributions.Normal:
-        return torch.distributions.Normal(mean, torch.ones_like(mean) * self.log_std.exp())
+        return torch.distributions.Normal(mean, torch.ones_like(mean) * self.log_std.exp(), validate_args=False)
+
+    def log_prob(self, mean: torch.Tensor, actions: torch.Tensor) -> torch.Tensor:
+        """Diagonal-Gaussian log density summed over the action dims (SB3 DiagGaussianDistribution),
+        written out so it captures into a HIP graph (torch.distributions validates on the host)."""
+        z = (actions - mean) * torch.exp(-self.log_std)
+        return (-0.5 * z * z - self.log_std - _HALF_LOG_2PI).sum(-1)
+
+    def entropy(self, n: int) -> torch.Tensor:
+        return (0.5 + _HALF_LOG_2PI + self.log_std).sum().expand(n)
 
     def evaluate_actions(self, obs: torch.Tensor, actions: torch.Tensor):
         mean, value = self(obs)
-        d = self.dist(mean)
-        return value, d.log_prob(actions).sum(-1), d.entropy().sum(-1)
+        return value, self.log_prob(mean, actions), self.entropy(obs.shape[0])
 
     @torch.no_grad()
     def predict_values(self, obs: torch.Tensor) -> torch.Tensor:
@@ -135,13 +147,25 @@ class PPO:
         self.device = torch.device(device) if device is not None else torch.device(venv.device)
         torch.manual_seed(seed)
         self.policy = (policy or ActorCritic()).to(self.device)
-        self.opt = torch.optim.Adam(self.policy.parameters(), lr=self.cfg.learning_rate, eps=1e-5)
+        self.world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+        self.use_graph = bool(self.cfg.graph and self.device.type == "cuda" and self.world == 1)
+        self.opt = torch.optim.Adam(self.policy.parameters(), lr=self.cfg.learning_rate, eps=1e-5,
+                                    capturable=self.use_graph)
         self.gen = torch.Generator(device=self.device).manual_seed(seed)
         self.n_envs = int(venv.num_envs)
         self._last_obs = None
         self._last_episode_starts = None
         self.num_timesteps = 0
-        self.world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+        # the rollout lands in fixed buffers (a captured update reads them at fixed addresses)
+        M = self.cfg.n_steps * self.n_envs
+        dev = self.device
+        self._flat = (torch.empty(M, 27, device=dev), torch.empty(M, 2, device=dev), torch.empty(M, device=dev),
+                      torch.empty(M, device=dev), torch.empty(M, device=dev))
+        z = torch.zeros((), device=dev)
+        self._acc = {"policy_loss": z.clone(), "value_loss": z.clone(), "entropy": z.clone(),
+                     "clip_fraction": z.clone()}
+        self._graph = None
+        self._gidx = None
 
     # ------------------------------------------------------------------ rollout
     @torch.no_grad()
@@ -163,7 +187,7 @@ class PPO:
             mean, value = self.policy(obs)
             std = self.policy.log_std.exp()
             actions = mean + std * torch.randn(mean.shape, device=dev, generator=self.gen)
-            logp = self.policy.dist(mean).log_prob(actions).sum(-1)
+            logp = self.policy.log_prob(mean, actions)
             clipped = actions.clamp(-1.0, 1.0)  # SB3 clips to the Box bounds for the env only
             new_obs, rew, term, trunc, info = self.venv.step(clipped)
             rew = rew.to(dev).float()
@@ -189,54 +213,87 @@ class PPO:
         last_values = self.policy.predict_values(self._last_obs)
         adv, ret = compute_gae(rew_b, val_b, start_b, last_values, self._last_episode_starts, self.cfg.gamma,
                                self.cfg.gae_lambda)
-        self._buf = (obs_b.reshape(T * N, 27), act_b.reshape(T * N, 2), logp_b.reshape(-1), adv.reshape(-1),
-                     ret.reshape(-1), val_b.reshape(-1))
+        for dst, src in zip(self._flat, (obs_b.reshape(T * N, 27), act_b.reshape(T * N, 2), logp_b.reshape(-1),
+                                         adv.reshape(-1), ret.reshape(-1))):
+            dst.copy_(src)
         self.num_timesteps += T * N
         f, r = float(finished), float(ret_sum)
         return {"episodes": f, "mean_return": r / f if f else float("nan")}
 
     # ------------------------------------------------------------------ update
-    def train(self) -> dict:
-        obs, act, old_logp, adv_all, ret, _ = self._buf
-        M, bs, c = obs.shape[0], self.cfg.batch_size, self.cfg.clip_range
+    def _minibatch(self, idx: torch.Tensor, zero_grad: bool = True):
+        """One SB3 PPO gradient step on rollout samples ``idx`` (statistics accumulated on device)."""
+        obs, act, old_logp, adv_all, ret = self._flat
+        c = self.cfg.clip_range
         params = list(self.policy.parameters())
-        z = torch.zeros((), device=self.device)
-        acc = {"policy_loss": z.clone(), "value_loss": z.clone(), "entropy": z.clone(), "clip_fraction": z.clone()}
+        values, logp, entropy = self.policy.evaluate_actions(obs[idx], act[idx])
+        adv = adv_all[idx]
+        if self.cfg.normalize_advantage and idx.numel() > 1:
+            adv = (adv - adv.mean()) / (adv.std() + 1e-8)
+        ratio = torch.exp(logp - old_logp[idx])
+        pl = -torch.min(adv * ratio, adv * torch.clamp(ratio, 1 - c, 1 + c)).mean()
+        vl = torch.nn.functional.mse_loss(ret[idx], values)
+        el = -entropy.mean()
+        loss = pl + self.cfg.ent_coef * el + self.cfg.vf_coef * vl
+        if zero_grad:
+            self.opt.zero_grad(set_to_none=False)
+        loss.backward()
+        if self.world > 1:
+            # data-parallel PPO: average the gradients over the ranks (RCCL all-reduce)
+            flat = torch.cat([p.grad.reshape(-1) for p in params])
+            dist.all_reduce(flat)
+            flat /= self.world
+            o = 0
+            for p in params:
+                k = p.numel()
+                p.grad.copy_(flat[o:o + k].view_as(p))
+                o += k
+        torch.nn.utils.clip_grad_norm_(params, self.cfg.max_grad_norm)
+        self.opt.step()
+        with torch.no_grad():
+            self._acc["policy_loss"] += pl
+            self._acc["value_loss"] += vl
+            self._acc["entropy"] -= el
+            self._acc["clip_fraction"] += ((ratio - 1).abs() > c).float().mean()
+
+    def _capture(self):
+        """Record one full-size minibatch step as a HIP graph: forward, backward, grad clipping and
+        the (capturable) Adam step replay with no per-kernel launches from Python."""
+        bs = self.cfg.batch_size
+        self._gidx = torch.zeros(bs, dtype=torch.long, device=self.device)
+        saved = {k: v.clone() for k, v in self._acc.items()}
+        self.opt.zero_grad(set_to_none=True)  # backward inside the capture writes fresh gradients
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._minibatch(self._gidx, zero_grad=False)
+        for k, v in saved.items():  # capture does not execute: nothing to undo, but keep the sums exact
+            self._acc[k].copy_(v)
+        self._graph = g
+
+    def train(self) -> dict:
+        M, bs = self._flat[0].shape[0], self.cfg.batch_size
+        for v in self._acc.values():
+            v.zero_()
         n_upd = 0
+        warm = 0
         for _ in range(self.cfg.n_epochs):
             perm = torch.randperm(M, device=self.device, generator=self.gen)
             for s in range(0, M, bs):
                 idx = perm[s:s + bs]
-                values, logp, entropy = self.policy.evaluate_actions(obs[idx], act[idx])
-                adv = adv_all[idx]
-                if self.cfg.normalize_advantage and len(idx) > 1:
-                    adv = (adv - adv.mean()) / (adv.std() + 1e-8)
-                ratio = torch.exp(logp - old_logp[idx])
-                pl = -torch.min(adv * ratio, adv * torch.clamp(ratio, 1 - c, 1 + c)).mean()
-                vl = torch.nn.functional.mse_loss(ret[idx], values)
-                el = -entropy.mean()
-                loss = pl + self.cfg.ent_coef * el + self.cfg.vf_coef * vl
-                self.opt.zero_grad(set_to_none=False)
-                loss.backward()
-                if self.world > 1:
-                    # data-parallel PPO: average the gradients over the ranks (RCCL all-reduce)
-                    flat = torch.cat([p.grad.reshape(-1) for p in params])
-                    dist.all_reduce(flat)
-                    flat /= self.world
-                    o = 0
-                    for p in params:
-                        k = p.numel()
-                        p.grad.copy_(flat[o:o + k].view_as(p))
-                        o += k
-                torch.nn.utils.clip_grad_norm_(params, self.cfg.max_grad_norm)
-                self.opt.step()
-                with torch.no_grad():  # accumulated on the device: no host sync per minibatch
-                    acc["policy_loss"] += pl
-                    acc["value_loss"] += vl
-                    acc["entropy"] -= el
-                    acc["clip_fraction"] += ((ratio - 1).abs() > c).float().mean()
+                if self.use_graph and idx.numel() == bs:
+                    if self._graph is None and warm >= 3:
+                        # capture after a few eager steps (lazy optimiser state, allocator warm-up)
+                        torch.cuda.synchronize(self.device)
+                        self._capture()
+                    if self._graph is not None:
+                        self._gidx.copy_(idx)
+                        self._graph.replay()
+                        n_upd += 1
+                        continue
+                    warm += 1
+                self._minibatch(idx)
                 n_upd += 1
-        return {k: float(v) / max(n_upd, 1) for k, v in acc.items()}
+        return {k: float(v) / max(n_upd, 1) for k, v in self._acc.items()}
 
     def learn(self, total_timesteps: int, log=None) -> list[dict]:
         """Alternate rollouts and updates until ``total_timesteps`` env steps (this rank)."""

@@ -77,3 +77,23 @@ def test_ppo_on_hip_batch(d2):
     assert len(hist) == 3 and all(np.isfinite(h["value_loss"]) for h in hist)
     assert hist[-1]["env_steps_per_s"] > 0
     venv.close()
+
+
+@pytest.mark.gpu
+def test_ppo_graph_update_matches_eager(d2):
+    """The HIP-graph replayed minibatch step computes what the eager step computes."""
+    from drone2d_amd.ppo import PPO, PPOConfig
+
+    params = []
+    for graph in (False, True):
+        venv = d2.Drone2dVecEnv(4096, seed=1, **_kw(scenario="corridor"))
+        cfg = PPOConfig.gpu_defaults(n_steps=8, batch_size=4096, n_epochs=2)
+        cfg.graph = graph
+        algo = PPO(venv, cfg, seed=0)
+        assert algo.use_graph == graph
+        hist = algo.learn(8 * 4096)
+        assert (algo._graph is not None) == graph and np.isfinite(hist[-1]["value_loss"])
+        params.append([p.detach().clone() for p in algo.policy.parameters()])
+        venv.close()
+    for a, b in zip(*params):
+        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-5)

@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--pool", type=int, default=4096)
     ap.add_argument("--refresh", type=int, default=100, help="updates between curriculum pool refreshes")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--no-graph", action="store_true", help="eager minibatch updates (A/B against the HIP graph)")
     a = ap.parse_args()
 
     import torch
@@ -47,9 +48,11 @@ def main():
         kw.update(mode="curriculum", scenario="curriculum", sim_num=0, curriculum_pool=a.pool,
                   curriculum_seed=a.seed)
     venv = d2.Drone2dVecEnv(a.envs, seed=a.seed, **kw)
-    algo = PPO(venv, PPOConfig.gpu_defaults(n_steps=a.n_steps, batch_size=a.batch, n_epochs=a.epochs), seed=a.seed)
+    cfg = PPOConfig.gpu_defaults(n_steps=a.n_steps, batch_size=a.batch, n_epochs=a.epochs)
+    cfg.graph = not a.no_graph
+    algo = PPO(venv, cfg, seed=a.seed)
     os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
-    out = open(os.path.join(REPO, "gpurun_out", "ppo.jsonl"), "w")
+    out = open(os.path.join(REPO, "gpurun_out", "ppo%s.jsonl" % ("_eager" if a.no_graph else "")), "w")
     t0 = time.perf_counter()
     for u in range(a.updates):
         if a.curriculum and u and u % a.refresh == 0:
@@ -61,7 +64,7 @@ def main():
         print(line, flush=True)
         out.write(line + "\n")
     total = algo.num_timesteps / (time.perf_counter() - t0)
-    print(json.dumps({"envs": a.envs, "updates": a.updates, "timesteps": algo.num_timesteps,
+    print(json.dumps({"envs": a.envs, "updates": a.updates, "timesteps": algo.num_timesteps, "graph": algo.use_graph,
                       "env_steps_per_s_incl_learning": total}), flush=True)
     venv.close()
 
