@@ -10,6 +10,7 @@ shipped agents), loaded from the float32 weights extracted from an agent zip
 """
 from __future__ import annotations
 
+import json
 import os
 
 import numpy as np
@@ -53,9 +54,18 @@ class MlpActor(torch.nn.Module):
 
 
 def run_first_episodes(venv, policy: MlpActor, *, deterministic: bool = False, seed: int = 0,
-                       max_steps: int | None = None, n_obstacles: int | None = None) -> dict:
+                       max_steps: int | None = None, n_obstacles: int | None = None,
+                       flight_paths: bool = False) -> dict:
     """Step ``venv`` (with info rows) under ``policy`` until every env has finished its first
-    episode; per-episode records as the reference's test loop keeps them (main.py:273-281)."""
+    episode; per-episode records as the reference's test loop keeps them (main.py:273-281).
+
+    ``flight_paths``: also return each episode's ``info['flight_path']`` -- the frame position
+    after every step as (x, screen_height - y), one entry per env step including the last
+    (drone_2d_env.py:409-415, 984-986; saved as JSON by main.py:307-308).  The positions are decoded
+    from the observation (obs[6:8] = 2p/(W,H) - 1, the terminal observation on the last step), so
+    they carry the float32 observation's rounding (<= 1e-4 px at 1300 px) where the reference
+    records the fp64 body position; the buffer stays on the device (8 B per env-step) until the
+    episodes are done."""
     dev = venv.device
     gen = torch.Generator(device=dev).manual_seed(seed)
     policy = policy.to(dev)
@@ -65,17 +75,24 @@ def run_first_episodes(venv, policy: MlpActor, *, deterministic: bool = False, s
     rows = torch.zeros(n, abi.INFO_DIM, dtype=torch.float32, device=dev)
     cap = max_steps if max_steps is not None else int(venv.kwargs["n_steps"]) + 1
     nobs = n_obstacles if n_obstacles is not None else len(venv.scenarios[0].circles)
-    for _ in range(cap):
+    pos = torch.empty(cap, n, 2, dtype=torch.float32, device=dev) if flight_paths else None
+    steps = 0
+    for t in range(cap):
         a = policy.act(obs, deterministic=deterministic, generator=gen)
         obs, rew, term, trunc, info = venv.step(a)
-        new = (term | trunc) & ~finished
+        done = term | trunc
+        new = done & ~finished
         rows[new] = info[new]
-        finished |= term | trunc
+        if pos is not None:
+            pos[t] = torch.where(done[:, None], venv.terminal_obs[:, 6:8].to(dev), obs[:, 6:8])
+        steps = t + 1
+        finished |= done
         if bool(finished.all()):
             break
-    rows = rows[finished].cpu().numpy()
+    idx = torch.nonzero(finished).flatten()
+    rows = rows[idx].cpu().numpy()
     recs = [info_dicts(r, nobs) for r in rows]
-    return {
+    out = {
         "successes": int(sum(d["n_successful_runs"] == 1 for d in recs)),
         "fails": int(sum(d["n_failed_runs"] == 1 for d in recs)),
         "collisions": np.array([d["n_collisions"] for d in recs], np.int64),
@@ -84,6 +101,14 @@ def run_first_episodes(venv, policy: MlpActor, *, deterministic: bool = False, s
         "rewards": np.array([d["total_reward"] for d in recs], np.float64),
         "unfinished": int(n - len(recs)),
     }
+    if pos is not None:
+        w, h = float(venv.kwargs["screensize_x"]), float(venv.kwargs["screensize_y"])
+        xy = pos[:steps, idx].double().cpu().numpy()  # [steps, finished envs, 2]
+        x = (xy[..., 0] + 1.0) * w / 2.0
+        y = h - (xy[..., 1] + 1.0) * h / 2.0
+        out["flight_paths"] = [np.stack([x[:T, j], y[:T, j]], 1).tolist()
+                               for j, T in enumerate(out["time_spent"])]
+    return out
 
 
 def summary(m: dict) -> dict:
@@ -97,10 +122,14 @@ def summary(m: dict) -> dict:
 
 
 def write_results(m: dict, out_dir: str, scenario: str, agent_nr: str, agent_path: str):
-    """The reference's per-scenario files: results.txt + collisions/rewards/apes/time_spent .npy."""
+    """The reference's per-scenario files: results.txt + collisions/rewards/apes/time_spent .npy
+    (+ the ``flight_paths`` JSON when ``m`` carries them), main.py:307-326."""
     os.makedirs(out_dir, exist_ok=True)
     for k in ("collisions", "rewards", "apes", "time_spent"):
         np.save(os.path.join(out_dir, f"{k}.npy"), m[k])
+    if "flight_paths" in m:
+        with open(os.path.join(out_dir, "flight_paths"), "w") as f:
+            json.dump(m["flight_paths"], f)
     s = summary(m)
     with open(os.path.join(out_dir, f"{scenario}_{agent_nr}_results.txt"), "w") as f:
         for k in ("Successes", "Fails", "Collisions", "Success rate", "Collision rate", "Average APE",

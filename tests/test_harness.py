@@ -102,3 +102,42 @@ def test_actor_matches_npz_mlp(d2):
     ref = np.clip(h @ w["action_net_weight"].T + w["action_net_bias"], -1, 1)
     got = pol.act(torch.from_numpy(x), deterministic=True).numpy()
     np.testing.assert_allclose(got, ref, atol=1e-5)
+
+
+class _Recording(OracleVecBackend):
+    """Oracle batch that also keeps the fp64 frame position after every step (before auto-reset
+    for the envs still running; done envs are reset inside the step, so their last position is
+    not in the state)."""
+
+    def step(self, actions):
+        out = super().step(actions)
+        st, _ = self.orc.get_state()
+        self.trace.append(st[0:2].T.copy())
+        return out
+
+
+def test_flight_paths(d2, tmp_path):
+    """info['flight_path'] per episode: one (x, H - y) entry per env step, the reference's JSON
+    layout (main.py:278, 307-308; drone_2d_env.py:409-415, 984-986), positions within float32
+    observation rounding of the fp64 body position."""
+    from drone2d_amd import harness
+    from drone2d_amd.config import ENV_TEST_CONFIG
+
+    n = 12
+    pol = harness.MlpActor.from_npz(os.path.join(GOLD, "agent_17_90.npz"))
+    be = _Recording(n, seed=4, **dict(ENV_TEST_CONFIG, scenario="corridor"))
+    be.trace = []
+    m = harness.run_first_episodes(be, pol, seed=4, flight_paths=True)
+    be.close()
+    H = float(ENV_TEST_CONFIG["screensize_y"])
+    assert m["unfinished"] == 0 and len(m["flight_paths"]) == n
+    for i, (fp, T) in enumerate(zip(m["flight_paths"], m["time_spent"])):
+        assert len(fp) == T and all(len(p) == 2 for p in fp)
+        ref = np.array([[x, H - y] for x, y in (be.trace[t][i] for t in range(T - 1))])
+        np.testing.assert_allclose(np.array(fp[:-1]), ref.reshape(-1, 2), rtol=0, atol=2e-4)
+        if T > 1:  # the last entry is the terminal position: one step from the one before
+            assert np.hypot(*(np.array(fp[-1]) - np.array(fp[-2]))) < 40.0
+    s = harness.write_results(m, str(tmp_path), "corridor", "17", "x")
+    back = json.load(open(tmp_path / "flight_paths"))
+    assert [len(p) for p in back] == list(m["time_spent"]) and back[0][0] == m["flight_paths"][0][0]
+    assert s["Successes"] + s["Fails"] == n

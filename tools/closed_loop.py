@@ -37,6 +37,8 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--scenarios", default=",".join(SCENARIOS))
     ap.add_argument("--config", default="test", choices=["test", "train"])
+    ap.add_argument("--flight-paths", action="store_true",
+                    help="also write the reference's flight_paths JSON per scenario (~24 B per env-step)")
     a = ap.parse_args()
     import torch  # noqa: F401
 
@@ -58,7 +60,7 @@ def main():
     for scn in a.scenarios.split(","):
         t0 = time.perf_counter()
         venv = d2.Drone2dVecEnv(a.envs, seed=a.seed, with_info=True, **dict(base, scenario=scn))
-        m = harness.run_first_episodes(venv, pol, seed=a.seed)
+        m = harness.run_first_episodes(venv, pol, seed=a.seed, flight_paths=a.flight_paths)
         venv.close()
         s = harness.write_results(m, os.path.join(REPO, "gpurun_out", "Tests", "agent_17_" + a.config, scn), scn, "17",
                                   ref["agent"])
