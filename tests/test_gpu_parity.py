@@ -11,7 +11,7 @@ import pytest
 import torch
 
 from conftest import SCENARIOS, load_golden
-from parity_util import OBS_ATOL, compare_step, make_pair
+from parity_util import OBS_ATOL, REW_ATOL, REW_RTOL, compare_step, make_pair
 
 pytestmark = pytest.mark.gpu
 
@@ -413,4 +413,48 @@ def test_sensing_ties_and_radii(d2, radii):
     act = np.zeros((n, 2), np.float32)              # hover-ish: positions barely move
     worst = compare_step(venv, orc, act)
     assert worst < OBS_ATOL
+    venv.close()
+
+
+def test_config5_size_on_one_gpu_windows(d2):
+    """BASELINE configs[4]'s whole 524 288-env mixed batch (8 x 65 536, env i on scenario i mod 7)
+    in ONE handle: 8 192 workgroups, i.e. eight rounds of the one-round 65 536-env launch.  Three
+    windows (the first envs, an unaligned middle span, the last envs) are checked against oracle
+    batches keyed by the same global env ids, teacher-forced every step with auto-reset on."""
+    import oracle
+    from drone2d_amd import shard
+    from drone2d_amd.config import make_cfg
+
+    n = 8 * FULL
+    kw = _cfgkw(SCENARIOS)
+    venv = shard.make_shard_venv(n, 0, 1, seed=21, **kw)
+    obs = venv.reset().clone()
+    m = 384
+    wins = [0, n // 2 + 37, n - m]
+    orcs = []
+    for o in wins:
+        cfg = make_cfg(dict(kw), auto_reset=True, env_id_base=o)
+        orc = oracle.OracleBatch(cfg, [s.to_c() for s in venv.scenarios], m,
+                                 env_scenario=venv.env_scenario[o:o + m])
+        np.testing.assert_allclose(obs[o:o + m].cpu().numpy(), orc.reset(21), atol=OBS_ATOL)
+        orcs.append(orc)
+    rng = np.random.default_rng(5)
+    dones = 0
+    for t in range(40):
+        st, ist = venv.get_state()
+        for o, orc in zip(wins, orcs):
+            orc.set_state(st[:, o:o + m].cpu().numpy().copy(), ist[:, o:o + m].cpu().numpy().copy())
+        act = rng.uniform(-1, 1, (n, 2)).astype(np.float32)
+        obs, rew, term, trunc, info = venv.step(torch.as_tensor(act, device=venv.device))
+        assert torch.isfinite(obs).all() and torch.isfinite(rew).all()
+        for o, orc in zip(wins, orcs):
+            o_obs, o_rew, o_term, _, _ = orc.step(act[o:o + m])
+            np.testing.assert_array_equal(term[o:o + m].cpu().numpy(), o_term)
+            np.testing.assert_allclose(rew[o:o + m].cpu().numpy(), o_rew, rtol=REW_RTOL, atol=REW_ATOL)
+            np.testing.assert_allclose(obs[o:o + m].cpu().numpy(), o_obs, rtol=0, atol=OBS_ATOL)
+            dones += int(o_term.sum())
+        if t == 0:
+            assert not term.all()
+    stats = venv.episode_stats()
+    assert torch.isfinite(stats).all() and stats[1] > 0
     venv.close()
