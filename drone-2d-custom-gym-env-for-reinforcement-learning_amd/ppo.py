@@ -151,7 +151,12 @@ class PPO:
         self.use_graph = bool(self.cfg.graph and self.device.type == "cuda" and self.world == 1)
         self.opt = torch.optim.Adam(self.policy.parameters(), lr=self.cfg.learning_rate, eps=1e-5,
                                     capturable=self.use_graph)
-        self.gen = torch.Generator(device=self.device).manual_seed(seed)
+        if self.world > 1:
+            # one policy on every rank: rank 0's initial parameters; each rank its own noise stream
+            for p in self.policy.parameters():
+                dist.broadcast(p.data, 0)
+        rank = dist.get_rank() if self.world > 1 else 0
+        self.gen = torch.Generator(device=self.device).manual_seed(seed + 1_000_003 * rank)
         self.n_envs = int(venv.num_envs)
         self._last_obs = None
         self._last_episode_starts = None

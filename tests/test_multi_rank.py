@@ -148,3 +148,48 @@ def _check(got, obs, rew, stats):
     np.testing.assert_array_equal(got["stats"][[1, 2, 3, 4]].numpy(), stats[[1, 2, 3, 4]].numpy())
     np.testing.assert_allclose(got["stats"].numpy(), stats.numpy(), rtol=1e-12, atol=1e-9)
     assert stats[1] > 0  # episodes finished
+
+
+def _ppo_worker(rank, world, port, out_dir):
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    for p in (here, os.path.dirname(here), os.path.join(os.path.dirname(here), "oracle")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import drone2d_amd  # noqa: F401
+    from drone2d_amd import shard
+    from drone2d_amd.ppo import PPO, PPOConfig
+    from oracle_backend import OracleVecBackend
+
+    shard.init_process_group_from_env("gloo")
+    off, cnt = shard.shard_range(64, world, rank)
+    be = OracleVecBackend(cnt, seed=5, env_id_offset=off, **dict(_kw(), scenario="corridor"))
+    # rank-dependent init seed on purpose: PPO broadcasts rank 0's parameters
+    algo = PPO(be, PPOConfig(n_steps=8, batch_size=64, n_epochs=2), seed=rank, device="cpu")
+    hist = algo.learn(2 * 8 * cnt)
+    assert len(hist) == 2 and all(np.isfinite(h["value_loss"]) for h in hist)
+    flat = torch.cat([p.detach().reshape(-1) for p in algo.policy.parameters()])
+    torch.save(flat, os.path.join(out_dir, f"ppo_{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+    be.close()
+
+
+def test_two_rank_ppo_keeps_one_policy(tmp_path, d2):
+    """Data-parallel PPO over gloo: each rank rolls out its own env shard, gradients are averaged
+    over the ranks every minibatch, so after two updates both ranks hold the same parameters."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_ppo_worker, args=(r, world, port, str(tmp_path))) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    a = torch.load(os.path.join(tmp_path, "ppo_0.pt"), weights_only=True)
+    b = torch.load(os.path.join(tmp_path, "ppo_1.pt"), weights_only=True)
+    assert torch.equal(a, b)
