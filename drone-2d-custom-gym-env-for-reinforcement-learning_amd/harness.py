@@ -59,7 +59,9 @@ def run_first_episodes(venv, policy: MlpActor, *, deterministic: bool = False, s
     """Step ``venv`` (with info rows) under ``policy`` until every env has finished its first
     episode; per-episode records as the reference's test loop keeps them (main.py:273-281).
 
-    ``flight_paths``: also return each episode's ``info['flight_path']`` -- the frame position
+    ``flight_paths``: also return ``flight_xy`` [steps, episodes, 2] (NaN past each episode's
+    end; ``flight_path_lists`` turns it into the JSON value), each episode's
+    ``info['flight_path']`` -- the frame position
     after every step as (x, screen_height - y), one entry per env step including the last
     (drone_2d_env.py:409-415, 984-986; saved as JSON by main.py:307-308).  The positions are decoded
     from the observation (obs[6:8] = 2p/(W,H) - 1, the terminal observation on the last step), so
@@ -104,11 +106,17 @@ def run_first_episodes(venv, policy: MlpActor, *, deterministic: bool = False, s
     if pos is not None:
         w, h = float(venv.kwargs["screensize_x"]), float(venv.kwargs["screensize_y"])
         xy = pos[:steps, idx].double().cpu().numpy()  # [steps, finished envs, 2]
-        x = (xy[..., 0] + 1.0) * w / 2.0
-        y = h - (xy[..., 1] + 1.0) * h / 2.0
-        out["flight_paths"] = [np.stack([x[:T, j], y[:T, j]], 1).tolist()
-                               for j, T in enumerate(out["time_spent"])]
+        fl = np.stack([(xy[..., 0] + 1.0) * w / 2.0, h - (xy[..., 1] + 1.0) * h / 2.0], -1)
+        fl[np.arange(steps)[:, None] >= out["time_spent"][None, :]] = np.nan  # after each episode's end
+        out["flight_xy"] = fl
     return out
+
+
+def flight_path_lists(m: dict) -> list:
+    """``m["flight_xy"]`` as the reference's ``flight_paths`` JSON value: one list of [x, y] per
+    episode, ``env_steps`` entries long (main.py:278, 307-308)."""
+    fl = m["flight_xy"]
+    return [fl[:T, j].tolist() for j, T in enumerate(m["time_spent"])]
 
 
 def summary(m: dict) -> dict:
@@ -127,9 +135,9 @@ def write_results(m: dict, out_dir: str, scenario: str, agent_nr: str, agent_pat
     os.makedirs(out_dir, exist_ok=True)
     for k in ("collisions", "rewards", "apes", "time_spent"):
         np.save(os.path.join(out_dir, f"{k}.npy"), m[k])
-    if "flight_paths" in m:
+    if "flight_xy" in m:
         with open(os.path.join(out_dir, "flight_paths"), "w") as f:
-            json.dump(m["flight_paths"], f)
+            json.dump(flight_path_lists(m), f)
     s = summary(m)
     with open(os.path.join(out_dir, f"{scenario}_{agent_nr}_results.txt"), "w") as f:
         for k in ("Successes", "Fails", "Collisions", "Success rate", "Collision rate", "Average APE",
@@ -139,4 +147,4 @@ def write_results(m: dict, out_dir: str, scenario: str, agent_nr: str, agent_pat
     return s
 
 
-__all__ = ["MlpActor", "run_first_episodes", "summary", "write_results"]
+__all__ = ["MlpActor", "run_first_episodes", "flight_path_lists", "summary", "write_results"]

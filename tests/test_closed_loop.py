@@ -83,9 +83,10 @@ def test_flight_paths_on_hip(d2):
     H = float(kw["screensize_y"])
     xmin, xmax, ymin, ymax = scn.spawn
     tx, ty = float(scn.wps[-1][0]), H - float(scn.wps[-1][1])
-    assert m["unfinished"] == 0 and len(m["flight_paths"]) == 1000
+    fps = harness.flight_path_lists(m)
+    assert m["unfinished"] == 0 and len(fps) == 1000
     n_succ = 0
-    for fp, T, col in zip(m["flight_paths"], m["time_spent"], m["collisions"]):
+    for fp, T, col in zip(fps, m["time_spent"], m["collisions"]):
         assert len(fp) == T
         x0, y0 = fp[0]
         assert xmin - 2 <= x0 <= xmax + 2 and H - ymax - 2 <= y0 <= H - ymin + 2
@@ -93,3 +94,37 @@ def test_flight_paths_on_hip(d2):
         if abs(xl - tx) < 20 and abs(yl - ty) < 20:
             n_succ += 1
     assert n_succ >= m["successes"] > 0
+
+
+@pytest.mark.parametrize("scn", ["corridor", "large", "S_corridor"])
+def test_flight_positions_match_reference(d2, scn):
+    """Where the drone is along its flights: the frame position after t steps (over the episodes
+    still flying) and at the end, against the flight_paths the reference recorded for the same
+    agent (run17see3/res/<scn>/flight_paths, reduced in tests/golden/agent_17_90_flights.npz by
+    make_flight_fixture.py): two-sample KS, p > 1e-3 for x and y at every t."""
+    import numpy as np
+    from scipy.stats import ks_2samp
+
+    from drone2d_amd import harness
+    from drone2d_amd.config import ENV_TEST_CONFIG
+
+    fl = np.load(os.path.join(HERE, "golden", "agent_17_90_flights.npz"))
+    pol = harness.MlpActor.from_npz(os.path.join(HERE, "golden", "agent_17_90.npz"))
+    venv = d2.Drone2dVecEnv(4000, seed=3, with_info=True, **dict(ENV_TEST_CONFIG, scenario=scn))
+    m = harness.run_first_episodes(venv, pol, seed=3, flight_paths=True)
+    venv.close()
+    fxy = m["flight_xy"]
+    ref_at = fl[f"{scn}__at"]
+    checked = 0
+    for j, t in enumerate(fl["times"]):
+        ours = fxy[t - 1][~np.isnan(fxy[t - 1, :, 0])]
+        ref = ref_at[:, j][~np.isnan(ref_at[:, j, 0])]
+        if len(ours) < 20 or len(ref) < 20:
+            continue
+        for c in (0, 1):
+            assert ks_2samp(ours[:, c], ref[:, c]).pvalue > 1e-3, (scn, int(t), c)
+        checked += 1
+    last = fxy[m["time_spent"] - 1, np.arange(fxy.shape[1])]
+    for c in (0, 1):
+        assert ks_2samp(last[:, c], fl[f"{scn}__final"][:, c]).pvalue > 1e-3, (scn, "final", c)
+    assert checked >= 5

@@ -130,8 +130,9 @@ def test_flight_paths(d2, tmp_path):
     m = harness.run_first_episodes(be, pol, seed=4, flight_paths=True)
     be.close()
     H = float(ENV_TEST_CONFIG["screensize_y"])
-    assert m["unfinished"] == 0 and len(m["flight_paths"]) == n
-    for i, (fp, T) in enumerate(zip(m["flight_paths"], m["time_spent"])):
+    fps = harness.flight_path_lists(m)
+    assert m["unfinished"] == 0 and len(fps) == n
+    for i, (fp, T) in enumerate(zip(fps, m["time_spent"])):
         assert len(fp) == T and all(len(p) == 2 for p in fp)
         ref = np.array([[x, H - y] for x, y in (be.trace[t][i] for t in range(T - 1))])
         np.testing.assert_allclose(np.array(fp[:-1]), ref.reshape(-1, 2), rtol=0, atol=2e-4)
@@ -139,5 +140,5 @@ def test_flight_paths(d2, tmp_path):
             assert np.hypot(*(np.array(fp[-1]) - np.array(fp[-2]))) < 40.0
     s = harness.write_results(m, str(tmp_path), "corridor", "17", "x")
     back = json.load(open(tmp_path / "flight_paths"))
-    assert [len(p) for p in back] == list(m["time_spent"]) and back[0][0] == m["flight_paths"][0][0]
+    assert [len(p) for p in back] == list(m["time_spent"]) and back[0][0] == fps[0][0]
     assert s["Successes"] + s["Fails"] == n

@@ -10,7 +10,9 @@ collision rates with the reference's own 100-run results (tests/golden/agent_17_
 
 Besides the rates, the per-episode distributions (flight time, APE, total reward) are compared with
 the reference's own saved arrays (tests/golden/agent_17_90_episodes.npz): z of the mean difference
-and the two-sample KS p-value.  ``--config`` picks the env kwargs: the reference's current
+and the two-sample KS p-value; and the positions along the flights (after 1-400 steps and at the
+end) with the reference's recorded flight paths (tests/golden/agent_17_90_flights.npz).
+``--config`` picks the env kwargs: the reference's current
 env_test_config (default) or its env_train_config (run17see3/env_train_config.txt): the two differ
 in reward weights only (initial_throw / n_fall_steps are inert in the reference), so the flight time
 and APE distributions must not move between them while the total rewards tell which configuration
@@ -31,6 +33,32 @@ sys.path.insert(0, REPO)
 SCENARIOS = ["perpendicular", "parallel", "S_parallel", "corridor", "S_corridor", "large", "impossible"]
 
 
+def flight_ks(fxy, time_spent, flights, scn):
+    """Two-sample KS of the frame position (x and screen y) after t steps, over the episodes still
+    flying at t, and of the final position, against the reference's own flight_paths of agent 17
+    (tests/golden/agent_17_90_flights.npz)."""
+    import numpy as np
+    from scipy.stats import ks_2samp
+
+    res = {}
+    ref_at, ref_fin = flights[f"{scn}__at"], flights[f"{scn}__final"]
+    for j, t in enumerate(flights["times"]):
+        t = int(t)
+        if t > fxy.shape[0]:
+            break
+        ours = fxy[t - 1][~np.isnan(fxy[t - 1, :, 0])]
+        ref = ref_at[:, j][~np.isnan(ref_at[:, j, 0])]
+        if len(ours) < 20 or len(ref) < 20:
+            continue
+        res[f"t{t}"] = {"n": [len(ours), len(ref)],
+                        "ks_p_x": float(ks_2samp(ours[:, 0], ref[:, 0]).pvalue),
+                        "ks_p_y": float(ks_2samp(ours[:, 1], ref[:, 1]).pvalue)}
+    last = fxy[np.asarray(time_spent) - 1, np.arange(fxy.shape[1])]
+    res["final"] = {"ks_p_x": float(ks_2samp(last[:, 0], ref_fin[:, 0]).pvalue),
+                    "ks_p_y": float(ks_2samp(last[:, 1], ref_fin[:, 1]).pvalue)}
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--envs", type=int, default=2000)
@@ -38,7 +66,7 @@ def main():
     ap.add_argument("--scenarios", default=",".join(SCENARIOS))
     ap.add_argument("--config", default="test", choices=["test", "train"])
     ap.add_argument("--flight-paths", action="store_true",
-                    help="also write the reference's flight_paths JSON per scenario (~24 B per env-step)")
+                    help="also write the reference's flight_paths JSON per scenario (large: ~24 B per env-step)")
     a = ap.parse_args()
     import torch  # noqa: F401
 
@@ -51,6 +79,7 @@ def main():
     from scipy.stats import ks_2samp
 
     eps = np.load(os.path.join(REPO, "tests", "golden", "agent_17_90_episodes.npz"))
+    flights = np.load(os.path.join(REPO, "tests", "golden", "agent_17_90_flights.npz"))
     if a.config == "test":
         base = dict(ENV_TEST_CONFIG)
     else:
@@ -60,8 +89,9 @@ def main():
     for scn in a.scenarios.split(","):
         t0 = time.perf_counter()
         venv = d2.Drone2dVecEnv(a.envs, seed=a.seed, with_info=True, **dict(base, scenario=scn))
-        m = harness.run_first_episodes(venv, pol, seed=a.seed, flight_paths=a.flight_paths)
+        m = harness.run_first_episodes(venv, pol, seed=a.seed, flight_paths=True)
         venv.close()
+        fxy = m.pop("flight_xy") if not a.flight_paths else m["flight_xy"]
         s = harness.write_results(m, os.path.join(REPO, "gpurun_out", "Tests", "agent_17_" + a.config, scn), scn, "17",
                                   ref["agent"])
         r = ref["results"][scn]
@@ -78,6 +108,9 @@ def main():
             out[scn][k] = {"ours": float(x.mean()), "ref": float(y.mean()),
                            "z": float((x.mean() - y.mean()) / max(se_m, 1e-12)),
                            "ks_p": float(ks_2samp(x, y).pvalue)}
+        if f"{scn}__at" in flights:
+            # where the drone is after t steps / at the end, against the reference's recorded flights
+            out[scn]["flight"] = flight_ks(fxy, m["time_spent"], flights, scn)
         print(scn, json.dumps(out[scn]), flush=True)
     os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
     json.dump({"config": a.config, "envs": a.envs, "seed": a.seed, "scenarios": out},
