@@ -138,6 +138,9 @@ constexpr int FILL_SPB = 128;  // K4 split path: slots per block (~26 fills per 
 #ifndef D2D_FILL_SPLIT
 #define D2D_FILL_SPLIT 1  // K4: the block's four waves share each round of 64 envs (fill_split)
 #endif
+#ifndef D2D_FILL_SENSE_LATE
+#define D2D_FILL_SENSE_LATE 1  // K4 split: wave 0's sensor part after the first barrier
+#endif
 #ifndef D2D_FILL_PERIOD
 #define D2D_FILL_PERIOD 16  // K4 after every this many steps (0: never; every reset synchronous)
 #endif
@@ -154,9 +157,21 @@ constexpr int FILL_SPB = 128;  // K4 split path: slots per block (~26 fills per 
                 ((uint64_t)__builtin_amdgcn_s_getreg((3 << 11) | 20) << 32) |                          \
                 (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);                                   \
     } while (0)
+// K4: the same per wave, at offset D2D_FSTAMP_BASE of the buffer (0 start, 1 staged + compacted,
+// 2 spawn state, 3 the wave's first part, 4 first barrier, 5 continuation, 6 path part, 7 end)
+#define D2D_FSTAMP_BASE 65536
+#define FSTAMP(k)                                                                                      \
+    do {                                                                                               \
+        if (a.stamps && (threadIdx.x & 63) == 0)                                                       \
+            a.stamps[D2D_FSTAMP_BASE + (size_t)(blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + (k)] =      \
+                __builtin_amdgcn_s_memtime();                                                          \
+    } while (0)
 #else
 #define STAMP(k) \
     do {         \
+    } while (0)
+#define FSTAMP(k) \
+    do {          \
     } while (0)
 #endif
 
@@ -901,15 +916,16 @@ __device__ __forceinline__ void fill_split(const StepArgs& a, const Scn* scns, c
         const BrTab* T = brtab(a, si);
         double sp[7];
         spawn_state(a, S, ie, (uint32_t)ep, sp);
+        if (r0 == 0) FSTAMP(2);
         float* c = a.rc_obs + (size_t)i * D2D_OBS_DIM;
-        if (wave == 0) {
+        if (wave == 0 && !D2D_FILL_SENSE_LATE) {
             double so[19];
             sensor_obs(a.cfg, S, Body{sp[0], sp[1], sp[2], 0.0, 0.0, 0.0}, so);
             if (act) {
 #pragma unroll
                 for (int k = 0; k < 19; ++k) c[k] = (float)so[k];
             }
-        } else if (T) {
+        } else if (wave != 0 && T) {
             const int w = wave - 1;
             BtLane L = bt_start<false>(*T, &T->hot, sp[0], sp[1]);
             // steps [1, b1), [b1, b2), [b2, BT_K)
@@ -930,7 +946,18 @@ __device__ __forceinline__ void fill_split(const StepArgs& a, const Scn* scns, c
             }
             devp[w][lane] = L.dev;
         }
+        if (r0 == 0) FSTAMP(3);
         __syncthreads();
+        if (r0 == 0) FSTAMP(4);
+        if (wave == 0 && D2D_FILL_SENSE_LATE) {
+            // the sensor part is independent of the path search: off the barrier's critical path
+            double so[19];
+            sensor_obs(a.cfg, S, Body{sp[0], sp[1], sp[2], 0.0, 0.0, 0.0}, so);
+            if (act) {
+#pragma unroll
+                for (int k = 0; k < 19; ++k) c[k] = (float)so[k];
+            }
+        }
         if (wave == 1) {
             double o[8];
             uint32_t f = 0;
@@ -939,7 +966,9 @@ __device__ __forceinline__ void fill_split(const StepArgs& a, const Scn* scns, c
                 const int dev = min(devp[0][lane], min(devp[1][lane], devp[2][lane]));
                 int iu;
                 const double u = bt_finish<false>(S, *T, &T->hot, kind, dev, sp[0], sp[1], iu);
+                if (r0 == 0) FSTAMP(5);
                 path_obs_u(a.cfg, S, sp[0], sp[1], sp[2], u, f, o, iu);
+                if (r0 == 0) FSTAMP(6);
             } else {
                 path_obs(a.cfg, S, nullptr, sp[0], sp[1], sp[2], f, o);
             }
@@ -964,6 +993,7 @@ __global__ __launch_bounds__(BLOCK) void d2d_fill_kernel(StepArgs a) {
     extern __shared__ __attribute__((aligned(16))) Scn s_scn[];
     __shared__ int list[BLOCK];
     __shared__ int cnt[BLOCK / 64];
+    FSTAMP(0);
     const Scn* scns = stage_scenarios<LDS, BLOCK>(a, s_scn);
     const int n = a.ns;
     // slots per block: BLOCK, or FILL_SPB with the split path (about one 64-env round per block)
@@ -996,7 +1026,13 @@ __global__ __launch_bounds__(BLOCK) void d2d_fill_kernel(StepArgs a) {
     }
     }
     if (D2D_FILL_SPLIT && D2D_FILL_COMPACT) {
+        FSTAMP(1);
         fill_split(a, scns, list, total);
+        FSTAMP(7);
+#ifdef D2D_STAMPS
+        if (a.stamps && threadIdx.x == 0)  // the block's number of fills after the stamps
+            a.stamps[D2D_FSTAMP_BASE + (size_t)gridDim.x * 32 + blockIdx.x] = (uint64_t)total;
+#endif
         return;
     }
     const int32_t ep = fld(a.ist, D2D_I_EPISODE, n, i);

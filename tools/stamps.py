@@ -106,9 +106,55 @@ def run(scenario, n, steps_warm, lib=LIB):
     return res
 
 
+def run_fill(scenario, n, steps_warm, lib=LIB):
+    """K4's phase stamps (wave 0 sensing, waves 1-3 table re-check thirds, wave 1 continuation and
+    path part) for one fill launch after ``steps_warm`` steps, in cycles from the block's stamp 0."""
+    import numpy as np
+    import torch
+
+    import drone2d_amd as d2
+    from drone2d_amd.config import ENV_TRAIN_CONFIG
+
+    venv = d2.Drone2dVecEnv(n, seed=3, with_info=False, native_lib=lib, **dict(ENV_TRAIN_CONFIG, scenario=scenario))
+    lib = venv._lib
+    lib.d2d_debug_stamps.argtypes = [C.c_void_p, C.c_void_p]
+    nb = (n + 127) // 128
+    base = 65536
+    buf = torch.zeros(base + nb * 32 + nb, dtype=torch.int64, device=venv.device)
+    venv.reset()
+    k = 0
+    while k < steps_warm or (k % 16) != 15:
+        venv.step(torch.rand(n, 2, device=venv.device) * 2 - 1)
+        k += 1
+    lib.d2d_debug_stamps(venv._h, C.c_void_p(buf.data_ptr()))
+    venv.step(torch.rand(n, 2, device=venv.device) * 2 - 1)  # the 16th: K1 then K4
+    torch.cuda.synchronize()
+    b = buf.cpu().numpy()
+    s = b[base:base + nb * 32].reshape(nb, 4, 8).astype(np.int64)
+    tot = b[base + nb * 32:base + nb * 33]
+    live = s[:, 0, 7] != 0  # blocks with work ran fill_split
+    s, tot = s[live], tot[live]
+    t0 = s[:, :, 0].min()
+    res = {"scenario": scenario, "envs": n, "blocks_with_fills": int(live.sum()),
+           "fills_per_block": [int(np.median(tot)), int(tot.max())],
+           "kernel_span_cycles": int(s[:, :, 7].max() - t0),
+           "block_start_spread": int(s[:, 0, 0].max() - t0)}
+    names = {1: "staged", 2: "spawn", 3: "part1", 4: "barrier1", 5: "continuation", 6: "path", 7: "end"}
+    for w in range(4):
+        r = {}
+        for k, nm in names.items():
+            if w != 1 and k in (5, 6):
+                continue
+            d = s[:, w, k] - s[:, w, 0]
+            r[nm] = [int(np.median(d)), int(np.percentile(d, 95)), int(d.max())]
+        res[f"wave{w}"] = r
+    print(json.dumps(res, indent=1))
+    return res
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("mode", choices=["build", "run"])
+    ap.add_argument("mode", choices=["build", "run", "fill"])
     ap.add_argument("--scenario", default="corridor")
     ap.add_argument("--envs", type=int, default=65536)
     ap.add_argument("--warm", type=int, default=40)
@@ -118,6 +164,10 @@ if __name__ == "__main__":
     a = ap.parse_args()
     if a.mode == "build":
         build(a.tag, a.defines)
+    elif a.mode == "fill":
+        out = [run_fill(s, a.envs, a.warm, lib_path(a.tag)) for s in a.scenario.split(",")]
+        os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+        json.dump(out, open(os.path.join(REPO, "gpurun_out", "fill_stamps.json"), "w"), indent=1)
     else:
         lib = lib_path(a.tag)
         out = [run(a.scenario, a.envs, a.warm, lib)]
