@@ -11,6 +11,10 @@ SRC = os.path.join(PKG_DIR, "csrc", "d2d_hip.hip")
 HDRS = [os.path.join(PKG_DIR, "csrc", "d2d_device.h"), os.path.join(PKG_DIR, "csrc", "d2d_kernels.h"),
         os.path.join(REPO, "include", "drone2d.h")]
 OUT = os.path.join(PKG_DIR, "_lib", "libdrone2d_hip.so")
+# the PPO update's fused element-wise kernels (include/d2d_ppo.h)
+PPO_SRC = os.path.join(PKG_DIR, "csrc", "d2d_ppo.hip")
+PPO_HDRS = [os.path.join(REPO, "include", "d2d_ppo.h")]
+PPO_OUT = os.path.join(PKG_DIR, "_lib", "libd2d_ppo.so")
 
 # -ffp-contract=off: the kernels follow the reference's NumPy evaluation order (explicit fma() only
 # where NumPy/OpenBLAS fuses); no fast-math: IEEE inf/NaN semantics are part of the contract.
@@ -25,21 +29,27 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found")
 
 
-def needs_build() -> bool:
-    if not os.path.exists(OUT):
+def needs_build(out: str = OUT, src: str = SRC, hdrs=None) -> bool:
+    if not os.path.exists(out):
         return True
-    t = os.path.getmtime(OUT)
-    return any(os.path.getmtime(p) > t for p in [SRC, *HDRS])
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(p) > t for p in [src, *(HDRS if hdrs is None else hdrs)])
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not needs_build():
-        return OUT
-    os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    tmp = OUT + ".tmp"
-    cmd = [hipcc(), *HIPCC_FLAGS, "-I", os.path.join(REPO, "include"), SRC, "-o", tmp]
+def _compile(src: str, out: str, verbose: bool):
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    tmp = out + ".tmp"
+    cmd = [hipcc(), *HIPCC_FLAGS, "-I", os.path.join(REPO, "include"), src, "-o", tmp]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
-    os.replace(tmp, OUT)
+    os.replace(tmp, out)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    """Both in-tree libraries: the env (libdrone2d_hip.so) and the PPO update kernels (libd2d_ppo.so)."""
+    if force or needs_build():
+        _compile(SRC, OUT, verbose)
+    if force or needs_build(PPO_OUT, PPO_SRC, PPO_HDRS):
+        _compile(PPO_SRC, PPO_OUT, verbose)
     return OUT

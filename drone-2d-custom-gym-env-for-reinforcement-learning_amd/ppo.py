@@ -50,6 +50,7 @@ class PPOConfig:
     max_grad_norm: float = 0.5
     normalize_advantage: bool = True
     graph: bool = True              # GPU, one rank: the minibatch update replayed as one HIP graph
+    manual: bool = True             # MLP backward + Adam written out over flat buffers (ManualStep)
 
     @classmethod
     def gpu_defaults(cls, **over) -> "PPOConfig":
@@ -117,6 +118,252 @@ class ActorCritic(nn.Module):
         return m
 
 
+_PPO_LIB = None
+
+
+def ppo_native():
+    """ctypes binding of libd2d_ppo.so (include/d2d_ppo.h), loaded once; no fallback on a GPU."""
+    global _PPO_LIB
+    if _PPO_LIB is None:
+        import ctypes as C
+        import os
+
+        from . import _native  # noqa: F401  (torch owns the HIP runtime first)
+
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libd2d_ppo.so")
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} not found: the HIP extension is not built "
+                               "(run `python -c 'import __graft_entry__ as g; g.build()'`)")
+        lib = C.CDLL(path)
+        vp, i32, i64, f32 = C.c_void_p, C.c_int32, C.c_int64, C.c_float
+        sig = {
+            "d2d_ppo_abi_version": [],
+            "d2d_ppo_adv_stats": [i32, vp, vp, vp, vp],
+            "d2d_ppo_head": [i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, f32, f32, vp, vp, vp, vp],
+            "d2d_ppo_head_finish": [i32, i32, vp, vp, f32, vp, vp, vp, vp, vp, vp],
+            "d2d_ppo_tanh_grad": [i64, vp, vp, vp],
+            "d2d_ppo_adam": [i32, vp, vp, vp, vp, vp, f32, f32, f32, f32, f32, vp],
+            "d2d_ppo_wgrad": [i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp, vp, vp],
+            "d2d_ppo_wgrad_chunks": [i32],
+        }
+        for name, args in sig.items():
+            fn = getattr(lib, name)
+            fn.restype, fn.argtypes = C.c_int32, args
+        if lib.d2d_ppo_abi_version() != 1:
+            raise RuntimeError("libd2d_ppo.so ABI mismatch")
+        _PPO_LIB = lib
+    return _PPO_LIB
+
+
+def _ok(rc: int, what: str):
+    if rc != 0:
+        raise RuntimeError(f"{what}: hipError {rc}")
+
+
+def _wgrad(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, rows: int = 512):
+    """out = a^T b for a [M, p], b [M, q] (a weight gradient: the sum over the minibatch's samples).
+    With K = M in the tens of thousands and a tiny p x q output, one GEMM runs on a handful of
+    workgroups; split the sample axis into M / rows chunks (one batched GEMM) and add them up."""
+    M = a.shape[0]
+    if M % rows or M < 4 * rows:
+        torch.mm(a.t(), b, out=out)
+        return
+    S = M // rows
+    torch.sum(torch.bmm(a.reshape(S, rows, a.shape[1]).transpose(1, 2), b.reshape(S, rows, b.shape[1])), 0, out=out)
+
+
+class ManualStep:
+    """One SB3 PPO minibatch step (``PPO._minibatch``'s loss, gradient, clipping and Adam) with the
+    backward pass of the two 27-64-64 tanh MLPs written out instead of recorded by autograd, over
+    flat parameter / gradient / Adam-moment buffers (the module's parameters become views of them):
+    about 60 kernels per minibatch instead of ~190, the weight gradients (sums over 32 768 samples
+    into 64 x 27 ... 1 x 64 outputs) as split-K batched GEMMs instead of GEMMs that run on a few
+    workgroups, and nothing that waits for the host -- the whole step captures into one HIP graph.
+
+    Gradients of the loss (SB3 PPO.train, stable_baselines3/ppo/ppo.py 2.1):
+      ratio = exp(logp - old_logp), s1 = adv ratio, s2 = adv clamp(ratio, 1 - c, 1 + c)
+      d(-mean min(s1, s2)) / d logp_i = -adv_i [s1_i <= s2_i] ratio_i / M   (ties: autograd splits
+        the gradient between the two equal branches, whose derivatives are then both adv_i)
+      d logp / d mean = z / sigma, d logp / d log_std = z^2 - 1 (z = (a - mean) / sigma);
+      entropy bonus: d(-ent_coef mean H) / d log_std = -ent_coef; value: vf_coef * -2 (R - V) / M.
+    Adam as torch.optim.Adam (lerp first moment, bias corrections, eps outside the square root)."""
+
+    def __init__(self, policy: ActorCritic, cfg: PPOConfig, device):
+        self.pol, self.cfg = policy, cfg
+        params = list(policy.parameters())
+        n = sum(p.numel() for p in params)
+        self.P = torch.zeros(n, device=device)
+        self.G = torch.zeros(n, device=device)
+        self.m = torch.zeros(n, device=device)
+        self.v = torch.zeros(n, device=device)
+        self.t = torch.zeros((), device=device)
+        # the fused element-wise kernels on a GPU (libd2d_ppo.so, loud if missing); torch ops on CPU
+        self.lib = ppo_native() if torch.device(device).type == "cuda" else None
+        self._ws = self._partial = self._wpart = None
+        o = 0
+        for p in params:
+            k = p.numel()
+            self.P[o:o + k].copy_(p.data.reshape(-1))
+            p.data = self.P[o:o + k].view_as(p)
+            p.grad = self.G[o:o + k].view_as(p)
+            o += k
+
+    def step(self, idx, rollout, acc: dict, world: int = 1):
+        self.grad(idx, rollout, acc)
+        self.apply(world)
+
+    def grad(self, idx, rollout, acc: dict):
+        """The loss gradient of minibatch ``idx`` of ``rollout`` = (obs, actions, old log-probs,
+        advantages, returns) into ``G``; statistics added to ``acc``."""
+        cfg, pol = self.cfg, self.pol
+        pn, vn = pol.mlp_extractor.policy_net, pol.mlp_extractor.value_net
+        W1p, W2p, W1v, W2v = pn[0].weight, pn[2].weight, vn[0].weight, vn[2].weight
+        W3p, W3v, ls = pol.action_net.weight, pol.value_net.weight, pol.log_std
+        obs_all, act_all, ol_all, adv_all, ret_all = rollout
+        X = obs_all[idx]
+        M, c = X.shape[0], cfg.clip_range
+        # forward (nn.Linear = addmm)
+        h1p = torch.tanh(torch.addmm(pn[0].bias, X, W1p.t()))
+        h2p = torch.tanh(torch.addmm(pn[2].bias, h1p, W2p.t()))
+        mean = torch.addmm(pol.action_net.bias, h2p, W3p.t())
+        h1v = torch.tanh(torch.addmm(vn[0].bias, X, W1v.t()))
+        h2v = torch.tanh(torch.addmm(vn[2].bias, h1v, W2v.t()))
+        V = torch.addmm(pol.value_net.bias, h2v, W3v.t()).squeeze(1)
+        if self.lib is not None:
+            g_mean, g_V = self._head_hip(idx, mean, V, rollout, acc)
+            tg = self._tanh_grad_hip
+        else:
+            g_mean, g_V = self._head_torch(mean, V, act_all[idx], ol_all[idx], adv_all[idx], ret_all[idx], acc)
+            tg = self._tanh_grad_torch
+        # backward: the layer-output gradients, then every weight / bias gradient
+        g2p = tg(h2p, torch.mm(g_mean, W3p))
+        g2v = tg(h2v, g_V[:, None] * W3v)
+        g1p = tg(h1p, torch.mm(g2p, W2p))
+        g1v = tg(h1v, torch.mm(g2v, W2v))
+        layers = ((g_mean, h2p, pol.action_net), (g_V[:, None], h2v, pol.value_net), (g2p, h1p, pn[2]),
+                  (g2v, h1v, vn[2]), (g1p, X, pn[0]), (g1v, X, vn[0]))
+        if self.lib is not None:
+            self._wgrad_hip(M, layers)
+            self._head_finish_hip(M, acc)  # after the reduce, which covers log_std's slots too
+        else:
+            for a, b, lin in layers:
+                _wgrad(a, b, lin.weight.grad)
+                torch.sum(a, 0, out=lin.bias.grad)
+
+    def _wgrad_hip(self, M, layers):
+        """All six weight / bias gradients in one libd2d_ppo.so launch (+ its reduce) into G."""
+        import ctypes as C
+
+        nc = self.lib.d2d_ppo_wgrad_chunks(M)
+        row_len = self.G.numel()  # all of G: log_std's slots (no problem covers them) are rewritten after
+        if self._wpart is None or self._wpart.numel() < nc * row_len:
+            self._wpart = torch.empty(nc * row_len, device=self.P.device)
+        n = len(layers)
+        base = self.G.data_ptr()
+        arr = lambda ty, v: (ty * n)(*v)  # noqa: E731
+        a_p = arr(C.c_void_p, [a.data_ptr() for a, _, _ in layers])
+        b_p = arr(C.c_void_p, [b.data_ptr() for _, b, _ in layers])
+        lda = arr(C.c_int32, [a.stride(0) for a, _, _ in layers])
+        ldb = arr(C.c_int32, [b.stride(0) for _, b, _ in layers])
+        pp = arr(C.c_int32, [a.shape[1] for a, _, _ in layers])
+        qq = arr(C.c_int32, [b.shape[1] for _, b, _ in layers])
+        wo = arr(C.c_int32, [(lin.weight.grad.data_ptr() - base) // 4 for _, _, lin in layers])
+        bo = arr(C.c_int32, [(lin.bias.grad.data_ptr() - base) // 4 for _, _, lin in layers])
+        for a, b, _ in layers:
+            assert a.stride(1) == 1 and b.stride(1) == 1 and a.shape[0] == b.shape[0] == M
+        _ok(self.lib.d2d_ppo_wgrad(M, n, a_p, lda, b_p, ldb, pp, qq, wo, bo, row_len, self._wpart.data_ptr(),
+                                   base, self._stream()), "d2d_ppo_wgrad")
+
+    @staticmethod
+    def _tanh_grad_torch(h, g):
+        return g.mul_(1.0 - h * h)
+
+    def _tanh_grad_hip(self, h, g):
+        _ok(self.lib.d2d_ppo_tanh_grad(g.numel(), h.data_ptr(), g.data_ptr(), self._stream()), "d2d_ppo_tanh_grad")
+        return g
+
+    def _stream(self):
+        return torch.cuda.current_stream(self.P.device).cuda_stream
+
+    def _head_hip(self, idx, mean, V, rollout, acc):
+        """The loss head in libd2d_ppo.so: advantage statistics, per-sample gradients, reductions."""
+        cfg, lib, st = self.cfg, self.lib, self._stream()
+        _, act_all, ol_all, adv_all, ret_all = rollout
+        M = idx.numel()
+        nb = (M + 255) // 256
+        if self._ws is None or self._partial.shape[0] < nb:
+            self._ws = torch.zeros(nb, 2, dtype=torch.float64, device=self.P.device)
+            self._partial = torch.zeros(nb, 5, device=self.P.device)
+        g_mean = torch.empty(M, 2, device=self.P.device)
+        g_V = torch.empty(M, device=self.P.device)
+        norm = int(cfg.normalize_advantage and M > 1)
+        if norm:
+            _ok(lib.d2d_ppo_adv_stats(M, idx.data_ptr(), adv_all.data_ptr(), self._ws.data_ptr(), st), "adv_stats")
+        ls = self.pol.log_std
+        _ok(lib.d2d_ppo_head(M, idx.data_ptr(), mean.data_ptr(), V.data_ptr(), act_all.data_ptr(), ol_all.data_ptr(),
+                             adv_all.data_ptr(), ret_all.data_ptr(), ls.data_ptr(), self._ws.data_ptr(), norm,
+                             cfg.clip_range, cfg.vf_coef, g_mean.data_ptr(), g_V.data_ptr(), self._partial.data_ptr(),
+                             st), "d2d_ppo_head")
+        return g_mean, g_V
+
+    def _head_finish_hip(self, M, acc):
+        """log_std's gradient and the minibatch statistics from the head's partial sums."""
+        ls, nb = self.pol.log_std, (M + 255) // 256
+        _ok(self.lib.d2d_ppo_head_finish(M, nb, self._partial.data_ptr(), ls.data_ptr(), self.cfg.ent_coef,
+                                         ls.grad.data_ptr(), acc["policy_loss"].data_ptr(),
+                                         acc["value_loss"].data_ptr(), acc["entropy"].data_ptr(),
+                                         acc["clip_fraction"].data_ptr(), self._stream()), "d2d_ppo_head_finish")
+
+    def _head_torch(self, mean, V, A, OL, ADV, R, acc):
+        cfg, ls = self.cfg, self.pol.log_std
+        M, c = mean.shape[0], cfg.clip_range
+        isig = torch.exp(-ls)
+        z = (A - mean) * isig
+        logp = (-0.5 * z * z - ls - _HALF_LOG_2PI).sum(1)
+        adv = ADV
+        if cfg.normalize_advantage and M > 1:
+            adv = (ADV - ADV.mean()) / (ADV.std() + 1e-8)
+        ratio = torch.exp(logp - OL)
+        s1 = adv * ratio
+        s2 = adv * torch.clamp(ratio, 1 - c, 1 + c)
+        pl = -torch.minimum(s1, s2).mean()
+        err = R - V
+        vl = (err * err).mean()
+        g_lp = torch.where(s1 <= s2, adv, 0.0) * ratio * (-1.0 / M)  # d loss / d logp
+        gz = g_lp[:, None] * z
+        g_mean = gz * isig
+        g_V = err * (-2.0 * cfg.vf_coef / M)
+        torch.sum(gz * z - g_lp[:, None], 0, out=ls.grad)
+        ls.grad.sub_(cfg.ent_coef)
+        acc["policy_loss"] += pl
+        acc["value_loss"] += vl
+        acc["entropy"] += (0.5 + _HALF_LOG_2PI + ls).sum()
+        acc["clip_fraction"] += ((ratio - 1).abs() > c).float().mean()
+        return g_mean, g_V
+
+    def apply(self, world: int = 1):
+        """Rank-mean of ``G`` (RCCL), clip_grad_norm_, Adam step on ``P``."""
+        cfg, G = self.cfg, self.G
+        if world > 1:
+            dist.all_reduce(G)  # data-parallel PPO: mean gradient over the ranks (RCCL)
+            G.div_(world)
+        if self.lib is not None:
+            _ok(self.lib.d2d_ppo_adam(G.numel(), self.P.data_ptr(), G.data_ptr(), self.m.data_ptr(),
+                                      self.v.data_ptr(), self.t.data_ptr(), cfg.learning_rate, 0.9, 0.999, 1e-5,
+                                      cfg.max_grad_norm, self._stream()), "d2d_ppo_adam")
+            return
+        # clip_grad_norm_(max_grad_norm): scale by min(1, max / (||g|| + 1e-6))
+        G.mul_(torch.clamp(cfg.max_grad_norm / (torch.linalg.vector_norm(G) + 1e-6), max=1.0))
+        # Adam(lr, betas (0.9, 0.999), eps 1e-5)
+        b1, b2, eps = 0.9, 0.999, 1e-5
+        self.t.add_(1.0)
+        self.m.lerp_(G, 1.0 - b1)
+        self.v.mul_(b2).addcmul_(G, G, value=1.0 - b2)
+        bc1 = 1.0 - torch.pow(b1, self.t)
+        bc2s = torch.sqrt(1.0 - torch.pow(b2, self.t))
+        self.P.sub_(self.m * (cfg.learning_rate / bc1) / (self.v.sqrt() / bc2s + eps))
+
+
 def compute_gae(rewards, values, episode_starts, last_values, last_dones, gamma, gae_lambda):
     """SB3 ``RolloutBuffer.compute_returns_and_advantage``: tensors [T, N] (episode_starts[t] = the
     env started a new episode at step t), last_* [N]; returns (advantages, returns)."""
@@ -149,12 +396,13 @@ class PPO:
         self.policy = (policy or ActorCritic()).to(self.device)
         self.world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
         self.use_graph = bool(self.cfg.graph and self.device.type == "cuda" and self.world == 1)
-        self.opt = torch.optim.Adam(self.policy.parameters(), lr=self.cfg.learning_rate, eps=1e-5,
-                                    capturable=self.use_graph)
         if self.world > 1:
             # one policy on every rank: rank 0's initial parameters; each rank its own noise stream
             for p in self.policy.parameters():
                 dist.broadcast(p.data, 0)
+        self.manual = ManualStep(self.policy, self.cfg, self.device) if self.cfg.manual else None
+        self.opt = None if self.manual else torch.optim.Adam(self.policy.parameters(), lr=self.cfg.learning_rate,
+                                                             eps=1e-5, capturable=self.use_graph)
         rank = dist.get_rank() if self.world > 1 else 0
         self.gen = torch.Generator(device=self.device).manual_seed(seed + 1_000_003 * rank)
         self.n_envs = int(venv.num_envs)
@@ -229,6 +477,10 @@ class PPO:
     def _minibatch(self, idx: torch.Tensor, zero_grad: bool = True):
         """One SB3 PPO gradient step on rollout samples ``idx`` (statistics accumulated on device)."""
         obs, act, old_logp, adv_all, ret = self._flat
+        if self.manual is not None:
+            with torch.no_grad():
+                self.manual.step(idx, self._flat, self._acc, self.world)
+            return
         c = self.cfg.clip_range
         params = list(self.policy.parameters())
         values, logp, entropy = self.policy.evaluate_actions(obs[idx], act[idx])
@@ -267,7 +519,8 @@ class PPO:
         bs = self.cfg.batch_size
         self._gidx = torch.zeros(bs, dtype=torch.long, device=self.device)
         saved = {k: v.clone() for k, v in self._acc.items()}
-        self.opt.zero_grad(set_to_none=True)  # backward inside the capture writes fresh gradients
+        if self.opt is not None:
+            self.opt.zero_grad(set_to_none=True)  # backward inside the capture writes fresh gradients
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             self._minibatch(self._gidx, zero_grad=False)
@@ -321,4 +574,4 @@ class PPO:
         return hist
 
 
-__all__ = ["PPOConfig", "ActorCritic", "PPO", "compute_gae"]
+__all__ = ["PPOConfig", "ActorCritic", "ManualStep", "PPO", "compute_gae"]

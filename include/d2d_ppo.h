@@ -1,0 +1,72 @@
+/* d2d_ppo.h -- C ABI of libd2d_ppo.so: the fused element-wise parts of one PPO minibatch update
+ * (drone2d_amd.ppo.ManualStep).  The reference trains with
+ * Stable-Baselines3 2.1's PPO.train (main.py:181-210); these kernels restate its loss head, the
+ * tanh backward and clip_grad_norm_ + torch.optim.Adam over one flat parameter buffer.
+ *
+ * All pointers are device pointers (float32 unless stated), every call is stream-ordered on
+ * `stream` (a hipStream_t; NULL = the default stream) and launches without synchronising, so a
+ * sequence of calls captures into a HIP graph.  Return value: 0, or a hipError_t code.
+ */
+#ifndef D2D_PPO_H
+#define D2D_PPO_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define D2D_PPO_ABI_VERSION 1
+#define D2D_PPO_HEAD_BLOCK 256
+
+int32_t d2d_ppo_abi_version(void);
+
+/* Advantage statistics of the minibatch (SB3 normalize_advantage: mean and unbiased std of
+ * adv[idx[0..m)]): per-workgroup double partial sums ws[2 b] = sum, ws[2 b + 1] = sum of squares,
+ * b < ceil(m / D2D_PPO_HEAD_BLOCK); d2d_ppo_head finishes them. */
+int32_t d2d_ppo_adv_stats(int32_t m, const int64_t* idx, const float* adv, double* ws, void* stream);
+
+/* The loss head for minibatch sample i (rollout row idx[i]): Gaussian log-density of act under
+ * (mean[i], exp(log_std)), ratio = exp(logp - old_logp), clipped surrogate, squared value error;
+ * writes d loss / d mean (g_mean [m][2]) and d loss / d value (g_v [m]) and per-workgroup partial
+ * sums partial[b][5] = (sum min(s1, s2), sum (R - V)^2, #|ratio - 1| > clip, sum dL/dlogp (z0^2 - 1),
+ * sum dL/dlogp (z1^2 - 1)).  normalize != 0: advantages normalised with ws (d2d_ppo_adv_stats).
+ * Grid: ceil(m / D2D_PPO_HEAD_BLOCK) workgroups. */
+int32_t d2d_ppo_head(int32_t m, const int64_t* idx, const float* mean, const float* value, const float* act,
+                     const float* old_logp, const float* adv, const float* ret, const float* log_std,
+                     const double* ws, int32_t normalize, float clip, float vf_coef, float* g_mean, float* g_v,
+                     float* partial, void* stream);
+
+/* Reduces the head's partials: log_std_grad[d] = sum_b partial[b][3 + d] - ent_coef, and adds the
+ * minibatch statistics to acc[0..3] (policy loss, value loss, entropy, clip fraction).  One
+ * workgroup. */
+int32_t d2d_ppo_head_finish(int32_t m, int32_t n_blocks, const float* partial, const float* log_std, float ent_coef,
+                            float* log_std_grad, float* acc_pl, float* acc_vl, float* acc_ent, float* acc_clip,
+                            void* stream);
+
+/* g[i] *= 1 - h[i]^2 for i < n (the tanh backward, in place). */
+int32_t d2d_ppo_tanh_grad(int64_t n, const float* h, float* g, void* stream);
+
+/* clip_grad_norm_(max_norm) then one torch.optim.Adam step (betas b1, b2, eps; bias corrections
+ * from the step counter *t, which is incremented) over n parameters p with gradients g and
+ * moments m1, m2.  One workgroup (n is the policy's ~10 k parameters). */
+int32_t d2d_ppo_adam(int32_t n, float* p, float* g, float* m1, float* m2, float* t, float lr, float b1, float b2,
+                     float eps, float max_norm, void* stream);
+
+/* Weight and bias gradients of up to D2D_PPO_WGRAD_MAX linear layers in one launch (+ one reduce):
+ * for problem k, g[w_off[k] + i q + j] = sum_r a_k[r][i] b_k[r][j] (i < p[k], j < q[k]; rows r < m;
+ * a_k row stride lda[k], b_k ldb[k]; p, q <= 64) and g[b_off[k] + i] = sum_r a_k[r][i].  `a` and `b`
+ * are host arrays of device pointers.  partial: device scratch of
+ * d2d_ppo_wgrad_chunks(m) x row_len floats; g[0 .. row_len) is overwritten (entries no problem
+ * covers become 0). */
+#define D2D_PPO_WGRAD_MAX 8
+int32_t d2d_ppo_wgrad(int32_t m, int32_t n_problems, const float* const* a, const int32_t* lda, const float* const* b,
+                      const int32_t* ldb, const int32_t* p, const int32_t* q, const int32_t* w_off,
+                      const int32_t* b_off, int32_t row_len, float* partial, float* g, void* stream);
+int32_t d2d_ppo_wgrad_chunks(int32_t m);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* D2D_PPO_H */

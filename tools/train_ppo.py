@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--refresh", type=int, default=100, help="updates between curriculum pool refreshes")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-graph", action="store_true", help="eager minibatch updates (A/B against the HIP graph)")
+    ap.add_argument("--autograd", action="store_true", help="autograd + torch Adam update (A/B against ManualStep)")
     a = ap.parse_args()
 
     import torch
@@ -50,9 +51,11 @@ def main():
     venv = d2.Drone2dVecEnv(a.envs, seed=a.seed, **kw)
     cfg = PPOConfig.gpu_defaults(n_steps=a.n_steps, batch_size=a.batch, n_epochs=a.epochs)
     cfg.graph = not a.no_graph
+    cfg.manual = not a.autograd
     algo = PPO(venv, cfg, seed=a.seed)
     os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
-    out = open(os.path.join(REPO, "gpurun_out", "ppo%s.jsonl" % ("_eager" if a.no_graph else "")), "w")
+    tag = ("_eager" if a.no_graph else "") + ("_autograd" if a.autograd else "")
+    out = open(os.path.join(REPO, "gpurun_out", f"ppo{tag}.jsonl"), "w")
     t0 = time.perf_counter()
     for u in range(a.updates):
         if a.curriculum and u and u % a.refresh == 0:
@@ -64,7 +67,7 @@ def main():
         print(line, flush=True)
         out.write(line + "\n")
     total = algo.num_timesteps / (time.perf_counter() - t0)
-    print(json.dumps({"envs": a.envs, "updates": a.updates, "timesteps": algo.num_timesteps, "graph": algo.use_graph,
+    print(json.dumps({"envs": a.envs, "updates": a.updates, "timesteps": algo.num_timesteps, "graph": algo.use_graph, "manual": cfg.manual,
                       "env_steps_per_s_incl_learning": total}), flush=True)
     venv.close()
 
