@@ -406,8 +406,6 @@ class PPO:
         rank = dist.get_rank() if self.world > 1 else 0
         self.gen = torch.Generator(device=self.device).manual_seed(seed + 1_000_003 * rank)
         self.n_envs = int(venv.num_envs)
-        self._last_obs = None
-        self._last_episode_starts = None
         self.num_timesteps = 0
         # the rollout lands in fixed buffers (a captured update reads them at fixed addresses)
         M = self.cfg.n_steps * self.n_envs
@@ -419,58 +417,90 @@ class PPO:
                      "clip_fraction": z.clone()}
         self._graph = None
         self._gidx = None
+        self._ro = None          # rollout buffers (_alloc_rollout)
+        self._ro_graph = None    # the captured rollout (GPU)
+        self._ro_warm = False
 
     # ------------------------------------------------------------------ rollout
-    @torch.no_grad()
-    def collect_rollouts(self) -> dict:
+    def _alloc_rollout(self):
         T, N, dev = self.cfg.n_steps, self.n_envs, self.device
-        if self._last_obs is None:
-            self._last_obs = self.venv.reset().to(dev).clone()
-            self._last_episode_starts = torch.ones(N, dtype=torch.bool, device=dev)
-        obs_b = torch.empty(T, N, 27, device=dev)
-        act_b = torch.empty(T, N, 2, device=dev)
-        logp_b = torch.empty(T, N, device=dev)
-        val_b = torch.empty(T, N, device=dev)
-        rew_b = torch.empty(T, N, device=dev)
-        start_b = torch.empty(T, N, dtype=torch.bool, device=dev)
-        finished = torch.zeros((), dtype=torch.float64, device=dev)
-        ret_sum = torch.zeros((), dtype=torch.float64, device=dev)
+        f64 = dict(dtype=torch.float64, device=dev)
+        self._ro = {"obs": torch.empty(T + 1, N, 27, device=dev), "act": torch.empty(T, N, 2, device=dev),
+                    "logp": torch.empty(T, N, device=dev), "val": torch.empty(T, N, device=dev),
+                    "rew": torch.empty(T, N, device=dev), "done": torch.empty(T, N, dtype=torch.bool, device=dev),
+                    "start0": torch.empty(N, dtype=torch.bool, device=dev),
+                    "noise": torch.empty(T, N, 2, device=dev), "fin": torch.zeros((), **f64),
+                    "ret": torch.zeros((), **f64)}
+        # time-limit truncations are bootstrapped with V(terminal obs); the reference never truncates
+        self._truncates = bool(getattr(getattr(self.venv, "cfg", None), "timeup_truncates", 1))
+
+    @torch.no_grad()
+    def _rollout_body(self):
+        """n_steps policy + env steps into the rollout buffers, then GAE into the flat buffers.
+        Reads obs[0], start0 and noise; leaves the next rollout's obs[0] / start0 in place.  No host
+        synchronisation: on a GPU the whole body is one captured HIP graph."""
+        from . import abi
+
+        R, pol, T, dev = self._ro, self.policy, self.cfg.n_steps, self.device
+        std = pol.log_std.exp()
         for t in range(T):
-            obs = self._last_obs
-            mean, value = self.policy(obs)
-            std = self.policy.log_std.exp()
-            actions = mean + std * torch.randn(mean.shape, device=dev, generator=self.gen)
-            logp = self.policy.log_prob(mean, actions)
-            clipped = actions.clamp(-1.0, 1.0)  # SB3 clips to the Box bounds for the env only
-            new_obs, rew, term, trunc, info = self.venv.step(clipped)
+            mean, value = pol(R["obs"][t])
+            actions = mean + std * R["noise"][t]
+            logp = pol.log_prob(mean, actions)
+            # SB3 clips to the Box bounds for the env only; the buffer keeps the unclipped action
+            new_obs, rew, term, trunc, info = self.venv.step(actions.clamp(-1.0, 1.0))
             rew = rew.to(dev).float()
             trunc = trunc.to(dev)
             done = term.to(dev) | trunc
-            if bool(trunc.any()):
-                # time-limit truncation: bootstrap with the value of the terminal observation
-                tv = self.policy.predict_values(self.venv.terminal_obs.to(dev))
+            if self._truncates:
+                tv = pol.predict_values(self.venv.terminal_obs.to(dev))
                 rew = torch.where(trunc, rew + self.cfg.gamma * tv, rew)
-            obs_b[t] = obs
-            act_b[t] = actions
-            logp_b[t] = logp
-            val_b[t] = value
-            rew_b[t] = rew
-            start_b[t] = self._last_episode_starts
-            self._last_obs = new_obs.to(dev).clone()
-            self._last_episode_starts = done
+            R["obs"][t + 1].copy_(new_obs)
+            R["act"][t].copy_(actions)
+            R["logp"][t].copy_(logp)
+            R["val"][t].copy_(value)
+            R["rew"][t].copy_(rew)
+            R["done"][t].copy_(done)
             if info is not None:
-                from . import abi
-
-                finished += done.sum()
-                ret_sum += torch.where(done, info[:, abi.INFO_TOTREW].to(dev).double(), 0.0).sum()
-        last_values = self.policy.predict_values(self._last_obs)
-        adv, ret = compute_gae(rew_b, val_b, start_b, last_values, self._last_episode_starts, self.cfg.gamma,
+                R["fin"] += done.sum()
+                R["ret"] += torch.where(done, info[:, abi.INFO_TOTREW].to(dev).double(), 0.0).sum()
+        last_values = pol.predict_values(R["obs"][T])
+        starts = torch.cat([R["start0"][None], R["done"][:-1]])
+        adv, ret = compute_gae(R["rew"], R["val"], starts, last_values, R["done"][T - 1], self.cfg.gamma,
                                self.cfg.gae_lambda)
-        for dst, src in zip(self._flat, (obs_b.reshape(T * N, 27), act_b.reshape(T * N, 2), logp_b.reshape(-1),
-                                         adv.reshape(-1), ret.reshape(-1))):
+        N = self.n_envs
+        for dst, src in zip(self._flat, (R["obs"][:T].reshape(T * N, 27), R["act"].reshape(T * N, 2),
+                                         R["logp"].reshape(-1), adv.reshape(-1), ret.reshape(-1))):
             dst.copy_(src)
+        R["obs"][0].copy_(R["obs"][T])
+        R["start0"].copy_(R["done"][T - 1])
+
+    def collect_rollouts(self) -> dict:
+        T, N = self.cfg.n_steps, self.n_envs
+        if self._ro is None:
+            self._alloc_rollout()
+            self._ro["obs"][0].copy_(self.venv.reset().to(self.device))
+            self._ro["start0"].fill_(True)
+        R = self._ro
+        R["fin"].zero_()
+        R["ret"].zero_()
+        torch.randn(R["noise"].shape, generator=self.gen, device=self.device, out=R["noise"])
+        graph_ok = self.cfg.graph and self.device.type == "cuda" and T % 2 == 0
+        if graph_ok and self._ro_graph is None and self._ro_warm:
+            # second rollout: capture (the first one ran eagerly: library and allocator warm-up);
+            # T even, so the env's double-buffered outputs are back at their start after a replay
+            torch.cuda.synchronize(self.device)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._rollout_body()
+            self._ro_graph = g
+        if self._ro_graph is not None:
+            self._ro_graph.replay()
+        else:
+            self._rollout_body()
+            self._ro_warm = True
         self.num_timesteps += T * N
-        f, r = float(finished), float(ret_sum)
+        f, r = float(R["fin"]), float(R["ret"])
         return {"episodes": f, "mean_return": r / f if f else float("nan")}
 
     # ------------------------------------------------------------------ update

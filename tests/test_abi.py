@@ -162,3 +162,28 @@ def test_spawn_uniforms_range(oracle_mod):
     u = np.array([oracle_mod.spawn_uniforms(7, i, e) for i in range(200) for e in range(3)])
     assert u.min() >= 0 and u.max() < 1
     assert abs(u.mean() - 0.5) < 0.05
+
+
+def test_ppo_library_exports_every_header_symbol(d2):
+    """libd2d_ppo.so (include/d2d_ppo.h, the PPO update's kernels): every declared entry point is
+    exported and bound; argument checks run before any device call."""
+    import ctypes as C
+
+    from drone2d_amd import _build, ppo
+
+    _build.build()
+    src = re.sub(r"/\*.*?\*/", "", open(os.path.join(REPO, "include", "d2d_ppo.h")).read(), flags=re.S)
+    fns = sorted(set(re.findall(r"\b(d2d_ppo_[a-z_]+)\s*\(", src)))
+    assert len(fns) >= 8
+    lib = ppo.ppo_native()
+    for f in fns:
+        assert hasattr(lib, f), f
+        assert getattr(lib, f).argtypes is not None, f  # declared in ppo_native's signatures
+    assert lib.d2d_ppo_abi_version() == 1
+    assert b"gfx950" in open(_build.PPO_OUT, "rb").read()
+    # out-of-range shapes are refused (hipErrorInvalidValue = 1) without a launch
+    assert lib.d2d_ppo_adam(1 << 20, None, None, None, None, None, 1e-3, 0.9, 0.999, 1e-5, 0.5, None) == 1
+    one = (C.c_int32 * 1)(65)
+    ptr = (C.c_void_p * 1)(None)
+    assert lib.d2d_ppo_wgrad(64, 1, ptr, one, ptr, one, one, one, one, one, 100, None, None, None) == 1
+    assert lib.d2d_ppo_wgrad(0, 1, ptr, one, ptr, one, one, one, one, one, 100, None, None, None) == 0

@@ -168,3 +168,28 @@ def test_manual_step_matches_autograd(d2, M):
 def test_manual_step_hip_matches_autograd(d2, M):
     """The same with libd2d_ppo.so's fused head / tanh-backward / Adam kernels on the GPU."""
     _manual_vs_autograd(M, "cuda")
+
+
+@pytest.mark.gpu
+def test_rollout_graph_matches_eager(d2):
+    """The captured rollout (policy + env step + GAE replayed as one HIP graph) fills the same
+    buffers as the eager loop, bit for bit, over three consecutive rollouts."""
+    from drone2d_amd.ppo import PPO, PPOConfig
+
+    outs = []
+    for graph in (False, True):
+        venv = d2.Drone2dVecEnv(2048, seed=4, with_info=True, **_kw(scenario="corridor"))
+        cfg = PPOConfig.gpu_defaults(n_steps=8, batch_size=4096)
+        cfg.graph = graph
+        algo = PPO(venv, cfg, seed=2)
+        rec = []
+        for _ in range(3):
+            st = algo.collect_rollouts()
+            rec.append(([t.clone() for t in algo._flat], st))
+        assert (algo._ro_graph is not None) == graph
+        outs.append(rec)
+        venv.close()
+    for (fa, sa), (fb, sb) in zip(*outs):
+        for a, b in zip(fa, fb):
+            assert torch.equal(a, b)
+        assert sa["episodes"] == sb["episodes"]
