@@ -36,10 +36,14 @@ def needs_build(out: str = OUT, src: str = SRC, hdrs=None) -> bool:
     return any(os.path.getmtime(p) > t for p in [src, *(HDRS if hdrs is None else hdrs)])
 
 
-def _compile(src: str, out: str, verbose: bool):
+# the PPO update is float32 training arithmetic with no reference rounding to follow: contracted FMAs
+PPO_FLAGS = [f if f != "-ffp-contract=off" else "-ffp-contract=fast" for f in HIPCC_FLAGS]
+
+
+def _compile(src: str, out: str, verbose: bool, flags=None):
     os.makedirs(os.path.dirname(out), exist_ok=True)
     tmp = out + ".tmp"
-    cmd = [hipcc(), *HIPCC_FLAGS, "-I", os.path.join(REPO, "include"), src, "-o", tmp]
+    cmd = [hipcc(), *(flags or HIPCC_FLAGS), "-I", os.path.join(REPO, "include"), src, "-o", tmp]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
@@ -51,5 +55,5 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if force or needs_build():
         _compile(SRC, OUT, verbose)
     if force or needs_build(PPO_OUT, PPO_SRC, PPO_HDRS):
-        _compile(PPO_SRC, PPO_OUT, verbose)
+        _compile(PPO_SRC, PPO_OUT, verbose, PPO_FLAGS)
     return OUT

@@ -1,7 +1,6 @@
-// Fused element-wise parts of one PPO minibatch update (include/d2d_ppo.h; drone2d_amd.ppo.ManualStep).
-// SB3 2.1 PPO.train's loss head, the tanh backward and clip_grad_norm_ + Adam, each as one launch
-// instead of the ~80 small element-wise kernels the same math costs as separate torch ops.  The
-// GEMMs of the two 27-64-64 MLPs stay on hipBLASLt (torch.addmm / bmm).
+// One PPO minibatch update in seven launches (include/d2d_ppo.h; drone2d_amd.ppo.ManualStep): SB3 2.1
+// PPO.train's loss, its gradient through the policy and value MLPs (27-64-64 tanh), clip_grad_norm_
+// and Adam, instead of ~190 autograd / optimiser kernels.
 #include <hip/hip_runtime.h>
 
 #include <cmath>
@@ -45,65 +44,6 @@ __global__ __launch_bounds__(D2D_PPO_HEAD_BLOCK) void adv_stats_kernel(int m, co
     }
 }
 
-__global__ __launch_bounds__(D2D_PPO_HEAD_BLOCK) void head_kernel(int m, const int64_t* idx, const float* mean,
-                                                                  const float* value, const float* act,
-                                                                  const float* old_logp, const float* adv,
-                                                                  const float* ret, const float* log_std,
-                                                                  const double* ws, int normalize, float clip,
-                                                                  float vf_coef, float* g_mean, float* g_v,
-                                                                  float* partial) {
-    __shared__ double red[D2D_PPO_HEAD_BLOCK / 64];
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    float adv_mean = 0.0f, adv_inv = 1.0f;
-    if (normalize) {
-        // mean and unbiased std of the minibatch's advantages from adv_stats_kernel's partials
-        const int nb = gridDim.x;
-        double s = 0.0, q = 0.0;
-        for (int b = threadIdx.x; b < nb; b += blockDim.x) {
-            s += ws[2 * b];
-            q += ws[2 * b + 1];
-        }
-        s = block_sum(s, red);
-        q = block_sum(q, red);
-        const double mu = s / m, var = (q - s * mu) / (m > 1 ? m - 1 : 1);
-        adv_mean = (float)mu;
-        adv_inv = 1.0f / ((float)sqrt(var > 0.0 ? var : 0.0) + 1e-8f);
-    }
-    double p_min = 0.0, p_err = 0.0, p_clip = 0.0, p_l0 = 0.0, p_l1 = 0.0;
-    if (i < m) {
-        const int64_t j = idx[i];
-        const float ls0 = log_std[0], ls1 = log_std[1];
-        const float is0 = expf(-ls0), is1 = expf(-ls1);
-        const float z0 = (act[2 * j] - mean[2 * i]) * is0, z1 = (act[2 * j + 1] - mean[2 * i + 1]) * is1;
-        const float logp = (-0.5f * z0 * z0 - ls0 - HALF_LOG_2PI) + (-0.5f * z1 * z1 - ls1 - HALF_LOG_2PI);
-        const float a = normalize ? (adv[j] - adv_mean) * adv_inv : adv[j];
-        const float ratio = expf(logp - old_logp[j]);
-        const float s1 = a * ratio, s2 = a * fminf(fmaxf(ratio, 1.0f - clip), 1.0f + clip);
-        // d(-mean min(s1, s2)) / d logp: the unclipped branch's a * ratio where it is the minimum
-        // (ties: both branches' derivatives are a * ratio)
-        const float g_lp = (s1 <= s2) ? a * ratio * (-1.0f / m) : 0.0f;
-        g_mean[2 * i] = g_lp * z0 * is0;
-        g_mean[2 * i + 1] = g_lp * z1 * is1;
-        const float err = ret[j] - value[i];
-        g_v[i] = err * (-2.0f * vf_coef / m);
-        p_min = fminf(s1, s2);
-        p_err = (double)err * err;
-        p_clip = fabsf(ratio - 1.0f) > clip ? 1.0 : 0.0;
-        p_l0 = (double)g_lp * (z0 * z0 - 1.0f);
-        p_l1 = (double)g_lp * (z1 * z1 - 1.0f);
-    }
-    const double v0 = block_sum(p_min, red), v1 = block_sum(p_err, red), v2 = block_sum(p_clip, red);
-    const double v3 = block_sum(p_l0, red), v4 = block_sum(p_l1, red);
-    if (threadIdx.x == 0) {
-        float* o = partial + (size_t)blockIdx.x * 5;
-        o[0] = (float)v0;
-        o[1] = (float)v1;
-        o[2] = (float)v2;
-        o[3] = (float)v3;
-        o[4] = (float)v4;
-    }
-}
-
 __global__ __launch_bounds__(256) void head_finish_kernel(int m, int nb, const float* partial, const float* log_std,
                                                           float ent_coef, float* ls_grad, float* acc_pl,
                                                           float* acc_vl, float* acc_ent, float* acc_clip) {
@@ -126,11 +66,227 @@ __global__ __launch_bounds__(256) void head_finish_kernel(int m, int nb, const f
     }
 }
 
-__global__ void tanh_grad_kernel(int64_t n, const float* h, float* g) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) {
-        const float x = h[i];
-        g[i] = g[i] * (1.0f - x * x);
+// ------------------------------------------------------------------ per-sample MLP passes
+// One thread per (sample, net): blockIdx.y = 0 the policy net (27-64-64 tanh -> 2), 1 the value net
+// (-> 1).  The weights are wave-uniform (scalar loads); the activations are rows of [m][64] arrays.
+struct MlpNet {
+    const float* w1;  // [64][27]
+    const float* b1;  // [64]
+    const float* w2;  // [64][64]
+    const float* b2;  // [64]
+    const float* w3;  // [od][64]
+    const float* b3;  // [od]
+    float* h1;        // [m][64]
+    float* h2;        // [m][64]
+    float* out;       // [m][od]: the action mean (od = 2) or the value (od = 1)
+    float* g1;        // [m][64] layer-1 output gradient (backward)
+    float* g2;        // [m][64]
+    float* gout;      // [m][od] d loss / d out
+    int od;
+};
+struct MlpPair {
+    MlpNet net[2];
+};
+constexpr int MLP_BLOCK = 256, OBS = 27, HID = 64;
+// the weights through the constant address space: wave-uniform loads become scalar loads (SGPR
+// operands of the FMAs) instead of one vector load per weight
+using CW = const __attribute__((address_space(4))) float*;
+__device__ __forceinline__ CW cw(const float* p) { return (CW)p; }
+
+// W1^T [27][64] and W2^T [64][64] of the workgroup's net staged in LDS, and each thread's layer input
+// as an LDS column: the forward pass takes input unit k outermost (a rolled loop), updates 64
+// independent accumulators and reads the weight row of k as LDS broadcasts
+constexpr int WT_NET = OBS * HID + HID * HID;
+__global__ __launch_bounds__(MLP_BLOCK) void mlp_forward_kernel(MlpPair P, int m, const int64_t* __restrict__ idx,
+                                                                const float* __restrict__ obs,
+                                                                float* __restrict__ xg) {
+    __shared__ __attribute__((aligned(16))) float wt[WT_NET];
+    __shared__ float col[HID][MLP_BLOCK];  // the layer input of every thread (x: rows 0..26, then h1)
+    const MlpNet& N = P.net[blockIdx.y];
+    for (int e = threadIdx.x; e < WT_NET; e += MLP_BLOCK) {
+        if (e < OBS * HID) {
+            const int k = e / HID, j = e % HID;
+            wt[e] = N.w1[j * OBS + k];
+        } else {
+            const int f = e - OBS * HID, k = f / HID, j = f % HID;
+            wt[e] = N.w2[j * HID + k];
+        }
+    }
+    const int t = threadIdx.x;
+    const int i = blockIdx.x * MLP_BLOCK + t;
+    const bool live = i < m;
+    const int64_t row = live ? idx[i] : 0;
+    for (int k = 0; k < OBS; ++k) {
+        const float v = live ? obs[row * OBS + k] : 0.0f;
+        col[k][t] = v;
+        if (blockIdx.y == 0 && live) xg[(size_t)i * OBS + k] = v;  // the gathered minibatch observations
+    }
+    __syncthreads();
+    const CW b1 = cw(N.b1), b2 = cw(N.b2), w3 = cw(N.w3), b3 = cw(N.b3);
+    float acc[HID];
+    // layer 1: h1[j] = tanh(b1[j] + sum_k W1[j][k] x[k])
+#pragma unroll
+    for (int j = 0; j < HID; ++j) acc[j] = b1[j];
+#pragma unroll 1
+    for (int k = 0; k < OBS; ++k) {
+        const float xv = col[k][t];
+        const float4* w = reinterpret_cast<const float4*>(wt + k * HID);
+#pragma unroll
+        for (int j4 = 0; j4 < HID / 4; ++j4) {
+            const float4 wv = w[j4];
+            acc[4 * j4] += wv.x * xv;
+            acc[4 * j4 + 1] += wv.y * xv;
+            acc[4 * j4 + 2] += wv.z * xv;
+            acc[4 * j4 + 3] += wv.w * xv;
+        }
+    }
+    __syncthreads();  // every thread has read its x column before h1 overwrites rows 0..26
+#pragma unroll
+    for (int j = 0; j < HID; ++j) {
+        acc[j] = tanhf(acc[j]);
+        col[j][t] = acc[j];
+    }
+    if (live) {
+#pragma unroll
+        for (int j = 0; j < HID; j += 4)
+            *reinterpret_cast<float4*>(N.h1 + (size_t)i * HID + j) =
+                make_float4(acc[j], acc[j + 1], acc[j + 2], acc[j + 3]);
+    }
+    // layer 2 (each thread reads only its own column: no barrier needed)
+#pragma unroll
+    for (int j = 0; j < HID; ++j) acc[j] = b2[j];
+#pragma unroll 1
+    for (int k = 0; k < HID; ++k) {
+        const float hv = col[k][t];
+        const float4* w = reinterpret_cast<const float4*>(wt + OBS * HID + k * HID);
+#pragma unroll
+        for (int j4 = 0; j4 < HID / 4; ++j4) {
+            const float4 wv = w[j4];
+            acc[4 * j4] += wv.x * hv;
+            acc[4 * j4 + 1] += wv.y * hv;
+            acc[4 * j4 + 2] += wv.z * hv;
+            acc[4 * j4 + 3] += wv.w * hv;
+        }
+    }
+    if (!live) return;
+    float o0 = b3[0], o1 = N.od == 2 ? b3[1] : 0.0f;
+#pragma unroll
+    for (int j = 0; j < HID; ++j) {
+        acc[j] = tanhf(acc[j]);
+        o0 += w3[j] * acc[j];
+        if (N.od == 2) o1 += w3[HID + j] * acc[j];
+    }
+#pragma unroll
+    for (int j = 0; j < HID; j += 4)
+        *reinterpret_cast<float4*>(N.h2 + (size_t)i * HID + j) = make_float4(acc[j], acc[j + 1], acc[j + 2], acc[j + 3]);
+    if (N.od == 2) {
+        N.out[2 * i] = o0;
+        N.out[2 * i + 1] = o1;
+    } else {
+        N.out[i] = o0;
+    }
+}
+
+// the loss head (policy: the clipped surrogate's d/d mean; value: the squared error's d/d V) and the
+// backward pass to the two hidden layers' output gradients; per-workgroup partial sums
+// (sum min(s1, s2), sum (R - V)^2, #clipped, sum dL/dlogp (z0^2 - 1), sum dL/dlogp (z1^2 - 1)):
+// policy blocks fill [b][0, 2, 3, 4], value blocks [nb + b][1]
+__global__ __launch_bounds__(MLP_BLOCK) void mlp_backward_kernel(MlpPair P, int m, const int64_t* __restrict__ idx,
+                                                                 const float* __restrict__ act,
+                                                                 const float* __restrict__ old_logp,
+                                                                 const float* __restrict__ adv,
+                                                                 const float* __restrict__ ret,
+                                                                 const float* __restrict__ log_std,
+                                                                 const double* __restrict__ ws, int normalize,
+                                                                 float clip, float vf_coef,
+                                                                 float* __restrict__ partial) {
+    __shared__ double red[MLP_BLOCK / 64];
+    const MlpNet& N = P.net[blockIdx.y];
+    const CW w2 = cw(N.w2), w3 = cw(N.w3);
+    const int i = blockIdx.x * MLP_BLOCK + threadIdx.x;
+    const bool live = i < m;
+    double q[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+    float go0 = 0.0f, go1 = 0.0f;
+    if (blockIdx.y == 0) {
+        float adv_mean = 0.0f, adv_inv = 1.0f;
+        if (normalize) {
+            const int nb = gridDim.x;
+            double s = 0.0, sq = 0.0;
+            for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+                s += ws[2 * b];
+                sq += ws[2 * b + 1];
+            }
+            s = block_sum(s, red);
+            sq = block_sum(sq, red);
+            const double mu = s / m, var = (sq - s * mu) / (m > 1 ? m - 1 : 1);
+            adv_mean = (float)mu;
+            adv_inv = 1.0f / ((float)sqrt(var > 0.0 ? var : 0.0) + 1e-8f);
+        }
+        if (live) {
+            const int64_t j = idx[i];
+            const float ls0 = log_std[0], ls1 = log_std[1];
+            const float is0 = expf(-ls0), is1 = expf(-ls1);
+            const float z0 = (act[2 * j] - N.out[2 * i]) * is0, z1 = (act[2 * j + 1] - N.out[2 * i + 1]) * is1;
+            const float logp = (-0.5f * z0 * z0 - ls0 - HALF_LOG_2PI) + (-0.5f * z1 * z1 - ls1 - HALF_LOG_2PI);
+            const float a = normalize ? (adv[j] - adv_mean) * adv_inv : adv[j];
+            const float ratio = expf(logp - old_logp[j]);
+            const float s1 = a * ratio, s2 = a * fminf(fmaxf(ratio, 1.0f - clip), 1.0f + clip);
+            const float g_lp = (s1 <= s2) ? a * ratio * (-1.0f / m) : 0.0f;
+            go0 = g_lp * z0 * is0;
+            go1 = g_lp * z1 * is1;
+            N.gout[2 * i] = go0;
+            N.gout[2 * i + 1] = go1;
+            q[0] = fminf(s1, s2);
+            q[2] = fabsf(ratio - 1.0f) > clip ? 1.0 : 0.0;
+            q[3] = (double)g_lp * (z0 * z0 - 1.0f);
+            q[4] = (double)g_lp * (z1 * z1 - 1.0f);
+        }
+    } else if (live) {
+        const float err = ret[idx[i]] - N.out[i];
+        go0 = err * (-2.0f * vf_coef / m);
+        N.gout[i] = go0;
+        q[1] = (double)err * err;
+    }
+    double t[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) t[k] = block_sum(q[k], red);
+    if (threadIdx.x == 0) {
+        float* o = partial + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 5;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) o[k] = (float)t[k];
+    }
+    if (!live) return;
+    // g2 = (gout W3) * (1 - h2^2), g1 = (g2 W2) * (1 - h1^2)
+    float g2[HID];
+    const float* h2 = N.h2 + (size_t)i * HID;
+#pragma unroll
+    for (int j = 0; j < HID; j += 4) {
+        const float4 hv = *reinterpret_cast<const float4*>(h2 + j);
+        const float hh[4] = {hv.x, hv.y, hv.z, hv.w};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            float d = go0 * w3[j + u];
+            if (N.od == 2) d += go1 * w3[HID + j + u];
+            g2[j + u] = d * (1.0f - hh[u] * hh[u]);
+        }
+        *reinterpret_cast<float4*>(N.g2 + (size_t)i * HID + j) = make_float4(g2[j], g2[j + 1], g2[j + 2], g2[j + 3]);
+    }
+    // g1[k] = (sum_j g2[j] W2[j][k]) (1 - h1[k]^2): output unit j outermost, W2's rows streamed
+    float g1[HID];
+#pragma unroll
+    for (int k = 0; k < HID; ++k) g1[k] = 0.0f;
+#pragma unroll
+    for (int j = 0; j < HID; ++j) {
+#pragma unroll
+        for (int k = 0; k < HID; ++k) g1[k] += g2[j] * w2[j * HID + k];
+    }
+    const float* h1 = N.h1 + (size_t)i * HID;
+#pragma unroll
+    for (int k = 0; k < HID; k += 4) {
+        const float4 hv = *reinterpret_cast<const float4*>(h1 + k);
+        *reinterpret_cast<float4*>(N.g1 + (size_t)i * HID + k) =
+            make_float4(g1[k] * (1.0f - hv.x * hv.x), g1[k + 1] * (1.0f - hv.y * hv.y),
+                        g1[k + 2] * (1.0f - hv.z * hv.z), g1[k + 3] * (1.0f - hv.w * hv.w));
     }
 }
 
@@ -200,10 +356,21 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradProblems P, int m, int 
     const int r0 = blockIdx.x * WG_ROWS, r1 = min(m, r0 + WG_ROWS);
     for (int rt = r0; rt < r1; rt += WG_TILE) {
         __syncthreads();
-        for (int e = threadIdx.x; e < WG_TILE * 64; e += 256) {
-            const int r = e >> 6, c = e & 63, row = rt + r;
-            ta[r][c] = (row < r1 && c < p) ? pr.a[(size_t)row * pr.lda + c] : 0.0f;
-            tb[r][c] = (row < r1 && c < q) ? pr.b[(size_t)row * pr.ldb + c] : 0.0f;
+        if (p == 64 && pr.lda == 64 && q == 64 && pr.ldb == 64 && rt + WG_TILE <= r1) {
+            // full 64 x 64 tiles of dense rows: 16-byte loads
+            for (int e = threadIdx.x; e < WG_TILE * 16; e += 256) {
+                const int r = e >> 4, c = (e & 15) * 4;
+                *reinterpret_cast<float4*>(&ta[r][c]) =
+                    *reinterpret_cast<const float4*>(pr.a + (size_t)(rt + r) * 64 + c);
+                *reinterpret_cast<float4*>(&tb[r][c]) =
+                    *reinterpret_cast<const float4*>(pr.b + (size_t)(rt + r) * 64 + c);
+            }
+        } else {
+            for (int e = threadIdx.x; e < WG_TILE * 64; e += 256) {
+                const int r = e >> 6, c = e & 63, row = rt + r;
+                ta[r][c] = (row < r1 && c < p) ? pr.a[(size_t)row * pr.lda + c] : 0.0f;
+                tb[r][c] = (row < r1 && c < q) ? pr.b[(size_t)row * pr.ldb + c] : 0.0f;
+            }
         }
         __syncthreads();
         if (pi < p && qi < q) {
@@ -217,9 +384,11 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradProblems P, int m, int 
 #pragma unroll
                     for (int y = 0; y < 4; ++y) acc[x][y] += a4[x] * b4[y];
                 }
-                if (qi == 0) {
+            }
+            if (qi == 0) {  // the bias: this thread's 4 rows of a, summed over the tile
+                for (int r = 0; r < WG_TILE; ++r) {
 #pragma unroll
-                    for (int x = 0; x < 4; ++x) bsum[x] += a4[x];
+                    for (int x = 0; x < 4; ++x) bsum[x] += ta[r][pi + x];
                 }
             }
         }
@@ -236,14 +405,20 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradProblems P, int m, int 
     }
 }
 
-// g[e] = sum over the n_chunks rows of partial[.][e], e < row_len
+// g[e] = sum over the n_chunks rows of partial[.][e], e < row_len: 64 elements per workgroup, the
+// chunks split over the workgroup's four waves
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(int n_chunks, int row_len, const float* __restrict__ partial,
                                                            float* __restrict__ g) {
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= row_len) return;
+    __shared__ float red[4][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int e = blockIdx.x * 64 + lane;
     float s = 0.0f;
-    for (int c = 0; c < n_chunks; ++c) s += partial[(size_t)c * row_len + e];
-    g[e] = s;
+    if (e < row_len) {
+        for (int c = w; c < n_chunks; c += 4) s += partial[(size_t)c * row_len + e];
+    }
+    red[w][lane] = s;
+    __syncthreads();
+    if (w == 0 && e < row_len) g[e] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
 }
 
 inline int32_t rc(hipError_t e) { return e == hipSuccess ? 0 : (int32_t)e; }
@@ -261,30 +436,12 @@ int32_t d2d_ppo_adv_stats(int32_t m, const int64_t* idx, const float* adv, doubl
     return rc(hipGetLastError());
 }
 
-int32_t d2d_ppo_head(int32_t m, const int64_t* idx, const float* mean, const float* value, const float* act,
-                     const float* old_logp, const float* adv, const float* ret, const float* log_std,
-                     const double* ws, int32_t normalize, float clip, float vf_coef, float* g_mean, float* g_v,
-                     float* partial, void* stream) {
-    if (m <= 0) return 0;
-    const int nb = (m + D2D_PPO_HEAD_BLOCK - 1) / D2D_PPO_HEAD_BLOCK;
-    hipLaunchKernelGGL(head_kernel, dim3(nb), dim3(D2D_PPO_HEAD_BLOCK), 0, (hipStream_t)stream, m, idx, mean, value,
-                       act, old_logp, adv, ret, log_std, ws, normalize, clip, vf_coef, g_mean, g_v, partial);
-    return rc(hipGetLastError());
-}
-
 int32_t d2d_ppo_head_finish(int32_t m, int32_t n_blocks, const float* partial, const float* log_std, float ent_coef,
                             float* log_std_grad, float* acc_pl, float* acc_vl, float* acc_ent, float* acc_clip,
                             void* stream) {
     if (m <= 0) return 0;
     hipLaunchKernelGGL(head_finish_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, m, n_blocks, partial, log_std,
                        ent_coef, log_std_grad, acc_pl, acc_vl, acc_ent, acc_clip);
-    return rc(hipGetLastError());
-}
-
-int32_t d2d_ppo_tanh_grad(int64_t n, const float* h, float* g, void* stream) {
-    if (n <= 0) return 0;
-    hipLaunchKernelGGL(tanh_grad_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, n, h,
-                       g);
     return rc(hipGetLastError());
 }
 
@@ -311,11 +468,44 @@ int32_t d2d_ppo_wgrad(int32_t m, int32_t n_problems, const float* const* a, cons
     hipLaunchKernelGGL(wgrad_kernel, dim3(nc, n_problems), dim3(256), 0, (hipStream_t)stream, P, m, row_len, partial);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return (int32_t)e;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((row_len + 255) / 256), dim3(256), 0, (hipStream_t)stream, nc,
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((row_len + 63) / 64), dim3(256), 0, (hipStream_t)stream, nc,
                        row_len, partial, g);
     return rc(hipGetLastError());
 }
 
 int32_t d2d_ppo_wgrad_chunks(int32_t m) { return (m + WG_ROWS - 1) / WG_ROWS; }
+
+static MlpPair make_pair(const float* const* w, float* const* buf) {
+    MlpPair P{};
+    for (int n = 0; n < 2; ++n) {
+        const float* const* W = w + 6 * n;
+        float* const* B = buf + 5 * n;
+        P.net[n] = MlpNet{W[0], W[1], W[2], W[3], W[4], W[5], B[0], B[1], B[2], B[3], B[4], nullptr, n == 0 ? 2 : 1};
+    }
+    return P;
+}
+
+int32_t d2d_ppo_mlp_forward(int32_t m, const int64_t* idx, const float* obs, const float* const* weights,
+                            float* const* bufs, float* xg, void* stream) {
+    if (m <= 0) return 0;
+    MlpPair P = make_pair(weights, bufs);
+    hipLaunchKernelGGL(mlp_forward_kernel, dim3((m + MLP_BLOCK - 1) / MLP_BLOCK, 2), dim3(MLP_BLOCK), 0,
+                       (hipStream_t)stream, P, m, idx, obs, xg);
+    return rc(hipGetLastError());
+}
+
+int32_t d2d_ppo_mlp_backward(int32_t m, const int64_t* idx, const float* act, const float* old_logp, const float* adv,
+                             const float* ret, const float* log_std, const double* ws, int32_t normalize, float clip,
+                             float vf_coef, const float* const* weights, float* const* bufs, float* const* gout,
+                             float* partial, void* stream) {
+    if (m <= 0) return 0;
+    MlpPair P = make_pair(weights, bufs);
+    P.net[0].gout = gout[0];
+    P.net[1].gout = gout[1];
+    hipLaunchKernelGGL(mlp_backward_kernel, dim3((m + MLP_BLOCK - 1) / MLP_BLOCK, 2), dim3(MLP_BLOCK), 0,
+                       (hipStream_t)stream, P, m, idx, act, old_logp, adv, ret, log_std, ws, normalize, clip, vf_coef,
+                       partial);
+    return rc(hipGetLastError());
+}
 
 }  // extern "C"

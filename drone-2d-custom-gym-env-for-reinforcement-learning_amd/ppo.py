@@ -139,12 +139,12 @@ def ppo_native():
         sig = {
             "d2d_ppo_abi_version": [],
             "d2d_ppo_adv_stats": [i32, vp, vp, vp, vp],
-            "d2d_ppo_head": [i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, i32, f32, f32, vp, vp, vp, vp],
             "d2d_ppo_head_finish": [i32, i32, vp, vp, f32, vp, vp, vp, vp, vp, vp],
-            "d2d_ppo_tanh_grad": [i64, vp, vp, vp],
             "d2d_ppo_adam": [i32, vp, vp, vp, vp, vp, f32, f32, f32, f32, f32, vp],
             "d2d_ppo_wgrad": [i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp, vp, vp],
             "d2d_ppo_wgrad_chunks": [i32],
+            "d2d_ppo_mlp_forward": [i32, vp, vp, vp, vp, vp, vp],
+            "d2d_ppo_mlp_backward": [i32, vp, vp, vp, vp, vp, vp, vp, i32, f32, f32, vp, vp, vp, vp, vp],
         }
         for name, args in sig.items():
             fn = getattr(lib, name)
@@ -175,10 +175,12 @@ def _wgrad(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, rows: int = 512)
 class ManualStep:
     """One SB3 PPO minibatch step (``PPO._minibatch``'s loss, gradient, clipping and Adam) with the
     backward pass of the two 27-64-64 tanh MLPs written out instead of recorded by autograd, over
-    flat parameter / gradient / Adam-moment buffers (the module's parameters become views of them):
-    about 60 kernels per minibatch instead of ~190, the weight gradients (sums over 32 768 samples
-    into 64 x 27 ... 1 x 64 outputs) as split-K batched GEMMs instead of GEMMs that run on a few
-    workgroups, and nothing that waits for the host -- the whole step captures into one HIP graph.
+    flat parameter / gradient / Adam-moment buffers (the module's parameters become views of them),
+    and nothing that waits for the host -- the whole step captures into one HIP graph.  On a GPU
+    it is seven libd2d_ppo.so launches (advantage statistics, both MLPs forward with one thread per
+    sample and net, loss head + backward to the hidden-layer gradients, all weight / bias gradients
+    + their reduce, log_std's gradient and the statistics, clip + Adam) instead of ~190 autograd /
+    optimiser kernels; on the CPU the same math in torch ops (split-K weight gradients).
 
     Gradients of the loss (SB3 PPO.train, stable_baselines3/ppo/ppo.py 2.1):
       ratio = exp(logp - old_logp), s1 = adv ratio, s2 = adv clamp(ratio, 1 - c, 1 + c)
@@ -200,6 +202,7 @@ class ManualStep:
         # the fused element-wise kernels on a GPU (libd2d_ppo.so, loud if missing); torch ops on CPU
         self.lib = ppo_native() if torch.device(device).type == "cuda" else None
         self._ws = self._partial = self._wpart = None
+        self._bufM = -1
         o = 0
         for p in params:
             k = p.numel()
@@ -220,6 +223,9 @@ class ManualStep:
         W1p, W2p, W1v, W2v = pn[0].weight, pn[2].weight, vn[0].weight, vn[2].weight
         W3p, W3v, ls = pol.action_net.weight, pol.value_net.weight, pol.log_std
         obs_all, act_all, ol_all, adv_all, ret_all = rollout
+        if self.lib is not None:
+            self._grad_hip(idx, rollout, acc)
+            return
         X = obs_all[idx]
         M, c = X.shape[0], cfg.clip_range
         # forward (nn.Linear = addmm)
@@ -229,12 +235,8 @@ class ManualStep:
         h1v = torch.tanh(torch.addmm(vn[0].bias, X, W1v.t()))
         h2v = torch.tanh(torch.addmm(vn[2].bias, h1v, W2v.t()))
         V = torch.addmm(pol.value_net.bias, h2v, W3v.t()).squeeze(1)
-        if self.lib is not None:
-            g_mean, g_V = self._head_hip(idx, mean, V, rollout, acc)
-            tg = self._tanh_grad_hip
-        else:
-            g_mean, g_V = self._head_torch(mean, V, act_all[idx], ol_all[idx], adv_all[idx], ret_all[idx], acc)
-            tg = self._tanh_grad_torch
+        g_mean, g_V = self._head_torch(mean, V, act_all[idx], ol_all[idx], adv_all[idx], ret_all[idx], acc)
+        tg = self._tanh_grad_torch
         # backward: the layer-output gradients, then every weight / bias gradient
         g2p = tg(h2p, torch.mm(g_mean, W3p))
         g2v = tg(h2v, g_V[:, None] * W3v)
@@ -242,13 +244,57 @@ class ManualStep:
         g1v = tg(h1v, torch.mm(g2v, W2v))
         layers = ((g_mean, h2p, pol.action_net), (g_V[:, None], h2v, pol.value_net), (g2p, h1p, pn[2]),
                   (g2v, h1v, vn[2]), (g1p, X, pn[0]), (g1v, X, vn[0]))
-        if self.lib is not None:
-            self._wgrad_hip(M, layers)
-            self._head_finish_hip(M, acc)  # after the reduce, which covers log_std's slots too
-        else:
-            for a, b, lin in layers:
-                _wgrad(a, b, lin.weight.grad)
-                torch.sum(a, 0, out=lin.bias.grad)
+        for a, b, lin in layers:
+            _wgrad(a, b, lin.weight.grad)
+            torch.sum(a, 0, out=lin.bias.grad)
+
+    def _grad_hip(self, idx, rollout, acc):
+        """libd2d_ppo.so: advantage statistics, both MLPs forward (one thread per sample and net),
+        loss head + backward to the hidden-layer gradients, all weight / bias gradients, log_std's."""
+        import ctypes as C
+
+        cfg, pol, lib, st = self.cfg, self.pol, self.lib, self._stream()
+        obs_all, act_all, ol_all, adv_all, ret_all = rollout
+        M, dev = idx.numel(), self.P.device
+        nb = (M + 255) // 256
+        if self._bufM != M:
+            e = lambda *sh: torch.empty(*sh, device=dev)  # noqa: E731
+            self._hb = {"h1p": e(M, 64), "h2p": e(M, 64), "mean": e(M, 2), "g1p": e(M, 64), "g2p": e(M, 64),
+                        "h1v": e(M, 64), "h2v": e(M, 64), "val": e(M, 1), "g1v": e(M, 64), "g2v": e(M, 64),
+                        "xg": e(M, 27), "gm": e(M, 2), "gv": e(M, 1)}
+            self._ws = torch.zeros(nb, 2, dtype=torch.float64, device=dev)
+            self._partial = torch.zeros(2 * nb, 5, device=dev)
+            self._bufM = M
+        hb = self._hb
+        pn, vn = pol.mlp_extractor.policy_net, pol.mlp_extractor.value_net
+        ws = [pn[0].weight, pn[0].bias, pn[2].weight, pn[2].bias, pol.action_net.weight, pol.action_net.bias,
+              vn[0].weight, vn[0].bias, vn[2].weight, vn[2].bias, pol.value_net.weight, pol.value_net.bias]
+        wptr = (C.c_void_p * 12)(*[w.data_ptr() for w in ws])
+        bptr = (C.c_void_p * 10)(*[hb[k].data_ptr() for k in ("h1p", "h2p", "mean", "g1p", "g2p",
+                                                              "h1v", "h2v", "val", "g1v", "g2v")])
+        gptr = (C.c_void_p * 2)(hb["gm"].data_ptr(), hb["gv"].data_ptr())
+        norm = int(cfg.normalize_advantage and M > 1)
+        if norm:
+            _ok(lib.d2d_ppo_adv_stats(M, idx.data_ptr(), adv_all.data_ptr(), self._ws.data_ptr(), st), "adv_stats")
+        _ok(lib.d2d_ppo_mlp_forward(M, idx.data_ptr(), obs_all.data_ptr(), wptr, bptr, hb["xg"].data_ptr(), st),
+            "d2d_ppo_mlp_forward")
+        _ok(lib.d2d_ppo_mlp_backward(M, idx.data_ptr(), act_all.data_ptr(), ol_all.data_ptr(), adv_all.data_ptr(),
+                                     ret_all.data_ptr(), pol.log_std.data_ptr(), self._ws.data_ptr(), norm,
+                                     cfg.clip_range, cfg.vf_coef, wptr, bptr, gptr, self._partial.data_ptr(), st),
+            "d2d_ppo_mlp_backward")
+        layers = ((hb["gm"], hb["h2p"], pol.action_net), (hb["gv"], hb["h2v"], pol.value_net),
+                  (hb["g2p"], hb["h1p"], pn[2]), (hb["g2v"], hb["h1v"], vn[2]), (hb["g1p"], hb["xg"], pn[0]),
+                  (hb["g1v"], hb["xg"], vn[0]))
+        self._wgrad_hip(M, layers)
+        ls = pol.log_std
+        _ok(lib.d2d_ppo_head_finish(M, 2 * nb, self._partial.data_ptr(), ls.data_ptr(), cfg.ent_coef,
+                                    ls.grad.data_ptr(), acc["policy_loss"].data_ptr(), acc["value_loss"].data_ptr(),
+                                    acc["entropy"].data_ptr(), acc["clip_fraction"].data_ptr(), st),
+            "d2d_ppo_head_finish")
+
+    @staticmethod
+    def _tanh_grad_torch(h, g):
+        return g.mul_(1.0 - h * h)
 
     def _wgrad_hip(self, M, layers):
         """All six weight / bias gradients in one libd2d_ppo.so launch (+ its reduce) into G."""
@@ -274,45 +320,8 @@ class ManualStep:
         _ok(self.lib.d2d_ppo_wgrad(M, n, a_p, lda, b_p, ldb, pp, qq, wo, bo, row_len, self._wpart.data_ptr(),
                                    base, self._stream()), "d2d_ppo_wgrad")
 
-    @staticmethod
-    def _tanh_grad_torch(h, g):
-        return g.mul_(1.0 - h * h)
-
-    def _tanh_grad_hip(self, h, g):
-        _ok(self.lib.d2d_ppo_tanh_grad(g.numel(), h.data_ptr(), g.data_ptr(), self._stream()), "d2d_ppo_tanh_grad")
-        return g
-
     def _stream(self):
         return torch.cuda.current_stream(self.P.device).cuda_stream
-
-    def _head_hip(self, idx, mean, V, rollout, acc):
-        """The loss head in libd2d_ppo.so: advantage statistics, per-sample gradients, reductions."""
-        cfg, lib, st = self.cfg, self.lib, self._stream()
-        _, act_all, ol_all, adv_all, ret_all = rollout
-        M = idx.numel()
-        nb = (M + 255) // 256
-        if self._ws is None or self._partial.shape[0] < nb:
-            self._ws = torch.zeros(nb, 2, dtype=torch.float64, device=self.P.device)
-            self._partial = torch.zeros(nb, 5, device=self.P.device)
-        g_mean = torch.empty(M, 2, device=self.P.device)
-        g_V = torch.empty(M, device=self.P.device)
-        norm = int(cfg.normalize_advantage and M > 1)
-        if norm:
-            _ok(lib.d2d_ppo_adv_stats(M, idx.data_ptr(), adv_all.data_ptr(), self._ws.data_ptr(), st), "adv_stats")
-        ls = self.pol.log_std
-        _ok(lib.d2d_ppo_head(M, idx.data_ptr(), mean.data_ptr(), V.data_ptr(), act_all.data_ptr(), ol_all.data_ptr(),
-                             adv_all.data_ptr(), ret_all.data_ptr(), ls.data_ptr(), self._ws.data_ptr(), norm,
-                             cfg.clip_range, cfg.vf_coef, g_mean.data_ptr(), g_V.data_ptr(), self._partial.data_ptr(),
-                             st), "d2d_ppo_head")
-        return g_mean, g_V
-
-    def _head_finish_hip(self, M, acc):
-        """log_std's gradient and the minibatch statistics from the head's partial sums."""
-        ls, nb = self.pol.log_std, (M + 255) // 256
-        _ok(self.lib.d2d_ppo_head_finish(M, nb, self._partial.data_ptr(), ls.data_ptr(), self.cfg.ent_coef,
-                                         ls.grad.data_ptr(), acc["policy_loss"].data_ptr(),
-                                         acc["value_loss"].data_ptr(), acc["entropy"].data_ptr(),
-                                         acc["clip_fraction"].data_ptr(), self._stream()), "d2d_ppo_head_finish")
 
     def _head_torch(self, mean, V, A, OL, ADV, R, acc):
         cfg, ls = self.cfg, self.pol.log_std

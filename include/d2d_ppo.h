@@ -1,7 +1,8 @@
-/* d2d_ppo.h -- C ABI of libd2d_ppo.so: the fused element-wise parts of one PPO minibatch update
+/* d2d_ppo.h -- C ABI of libd2d_ppo.so: one PPO minibatch update in seven launches
  * (drone2d_amd.ppo.ManualStep).  The reference trains with
  * Stable-Baselines3 2.1's PPO.train (main.py:181-210); these kernels restate its loss head, the
- * tanh backward and clip_grad_norm_ + torch.optim.Adam over one flat parameter buffer.
+ * backward pass through the two MLPs and clip_grad_norm_ + torch.optim.Adam over one flat
+ * parameter buffer.
  *
  * All pointers are device pointers (float32 unless stated), every call is stream-ordered on
  * `stream` (a hipStream_t; NULL = the default stream) and launches without synchronising, so a
@@ -23,19 +24,8 @@ int32_t d2d_ppo_abi_version(void);
 
 /* Advantage statistics of the minibatch (SB3 normalize_advantage: mean and unbiased std of
  * adv[idx[0..m)]): per-workgroup double partial sums ws[2 b] = sum, ws[2 b + 1] = sum of squares,
- * b < ceil(m / D2D_PPO_HEAD_BLOCK); d2d_ppo_head finishes them. */
+ * b < ceil(m / D2D_PPO_HEAD_BLOCK); d2d_ppo_mlp_backward finishes them. */
 int32_t d2d_ppo_adv_stats(int32_t m, const int64_t* idx, const float* adv, double* ws, void* stream);
-
-/* The loss head for minibatch sample i (rollout row idx[i]): Gaussian log-density of act under
- * (mean[i], exp(log_std)), ratio = exp(logp - old_logp), clipped surrogate, squared value error;
- * writes d loss / d mean (g_mean [m][2]) and d loss / d value (g_v [m]) and per-workgroup partial
- * sums partial[b][5] = (sum min(s1, s2), sum (R - V)^2, #|ratio - 1| > clip, sum dL/dlogp (z0^2 - 1),
- * sum dL/dlogp (z1^2 - 1)).  normalize != 0: advantages normalised with ws (d2d_ppo_adv_stats).
- * Grid: ceil(m / D2D_PPO_HEAD_BLOCK) workgroups. */
-int32_t d2d_ppo_head(int32_t m, const int64_t* idx, const float* mean, const float* value, const float* act,
-                     const float* old_logp, const float* adv, const float* ret, const float* log_std,
-                     const double* ws, int32_t normalize, float clip, float vf_coef, float* g_mean, float* g_v,
-                     float* partial, void* stream);
 
 /* Reduces the head's partials: log_std_grad[d] = sum_b partial[b][3 + d] - ent_coef, and adds the
  * minibatch statistics to acc[0..3] (policy loss, value loss, entropy, clip fraction).  One
@@ -43,9 +33,6 @@ int32_t d2d_ppo_head(int32_t m, const int64_t* idx, const float* mean, const flo
 int32_t d2d_ppo_head_finish(int32_t m, int32_t n_blocks, const float* partial, const float* log_std, float ent_coef,
                             float* log_std_grad, float* acc_pl, float* acc_vl, float* acc_ent, float* acc_clip,
                             void* stream);
-
-/* g[i] *= 1 - h[i]^2 for i < n (the tanh backward, in place). */
-int32_t d2d_ppo_tanh_grad(int64_t n, const float* h, float* g, void* stream);
 
 /* clip_grad_norm_(max_norm) then one torch.optim.Adam step (betas b1, b2, eps; bias corrections
  * from the step counter *t, which is incremented) over n parameters p with gradients g and
@@ -64,6 +51,24 @@ int32_t d2d_ppo_wgrad(int32_t m, int32_t n_problems, const float* const* a, cons
                       const int32_t* ldb, const int32_t* p, const int32_t* q, const int32_t* w_off,
                       const int32_t* b_off, int32_t row_len, float* partial, float* g, void* stream);
 int32_t d2d_ppo_wgrad_chunks(int32_t m);
+
+/* The two MLPs (policy 27-64-64-2, value 27-64-64-1, tanh) per minibatch sample, one thread per
+ * (sample, net).  weights: 12 device pointers, per net (policy, then value): W1 [64][27], b1 [64],
+ * W2 [64][64], b2 [64], W3 [od][64], b3 [od].  bufs: 10 device pointers, per net: h1 [m][64],
+ * h2 [m][64], out [m][od] (the action mean / the value), g1 [m][64], g2 [m][64].
+ * mlp_forward: the rollout rows idx[0..m) of obs [.][27] through both nets (h1, h2, out) and the
+ * gathered observations into xg [m][27].  mlp_backward: the loss head below (gout[0] =
+ * d loss / d mean [m][2], gout[1] = d loss / d value [m]; partial[2][ceil(m / 256)][5], finished by
+ * d2d_ppo_head_finish with n_blocks = 2 ceil(m / 256)) and the hidden layers' output gradients g2, g1.
+ * The head: Gaussian log-density of act under (mean, exp(log_std)), ratio = exp(logp - old_logp),
+ * clipped surrogate with advantages normalised by d2d_ppo_adv_stats' partials (normalize != 0),
+ * squared value error scaled by vf_coef. */
+int32_t d2d_ppo_mlp_forward(int32_t m, const int64_t* idx, const float* obs, const float* const* weights,
+                            float* const* bufs, float* xg, void* stream);
+int32_t d2d_ppo_mlp_backward(int32_t m, const int64_t* idx, const float* act, const float* old_logp, const float* adv,
+                             const float* ret, const float* log_std, const double* ws, int32_t normalize, float clip,
+                             float vf_coef, const float* const* weights, float* const* bufs, float* const* gout,
+                             float* partial, void* stream);
 
 #ifdef __cplusplus
 }
