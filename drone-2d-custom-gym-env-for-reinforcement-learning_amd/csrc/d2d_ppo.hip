@@ -67,8 +67,8 @@ __global__ __launch_bounds__(256) void head_finish_kernel(int m, int nb, const f
 }
 
 // ------------------------------------------------------------------ per-sample MLP passes
-// One thread per (sample, net): blockIdx.y = 0 the policy net (27-64-64 tanh -> 2), 1 the value net
-// (-> 1).  The weights are wave-uniform (scalar loads); the activations are rows of [m][64] arrays.
+// blockIdx.y = 0: the policy net (27-64-64 tanh -> 2), 1: the value net (-> 1); the activations are
+// rows of [m][64] arrays.
 struct MlpNet {
     const float* w1;  // [64][27]
     const float* b1;  // [64]
@@ -93,15 +93,19 @@ constexpr int MLP_BLOCK = 256, OBS = 27, HID = 64;
 using CW = const __attribute__((address_space(4))) float*;
 __device__ __forceinline__ CW cw(const float* p) { return (CW)p; }
 
-// W1^T [27][64] and W2^T [64][64] of the workgroup's net staged in LDS, and each thread's layer input
-// as an LDS column: the forward pass takes input unit k outermost (a rolled loop), updates 64
-// independent accumulators and reads the weight row of k as LDS broadcasts
+// Two threads per (sample, net): thread t of a workgroup serves sample t / 2 of the workgroup's
+// MLP_SPB and owns output units [32 (t & 1), 32 (t & 1) + 32) of every layer; the layer inputs of a
+// sample (x, h1; g2 in the backward pass) are an LDS column both of its threads read.
+constexpr int MLP_SPB = MLP_BLOCK / 2, HALF = HID / 2;
 constexpr int WT_NET = OBS * HID + HID * HID;
+
+// W1^T [27][64] and W2^T [64][64] of the workgroup's net staged in LDS: input unit k outermost (a
+// rolled loop), 32 independent accumulators, the weight row of k read as LDS broadcasts
 __global__ __launch_bounds__(MLP_BLOCK) void mlp_forward_kernel(MlpPair P, int m, const int64_t* __restrict__ idx,
                                                                 const float* __restrict__ obs,
                                                                 float* __restrict__ xg) {
     __shared__ __attribute__((aligned(16))) float wt[WT_NET];
-    __shared__ float col[HID][MLP_BLOCK];  // the layer input of every thread (x: rows 0..26, then h1)
+    __shared__ float col[HID][MLP_SPB];  // the layer input of every sample (x: rows 0..26, then h1)
     const MlpNet& N = P.net[blockIdx.y];
     for (int e = threadIdx.x; e < WT_NET; e += MLP_BLOCK) {
         if (e < OBS * HID) {
@@ -112,27 +116,27 @@ __global__ __launch_bounds__(MLP_BLOCK) void mlp_forward_kernel(MlpPair P, int m
             wt[e] = N.w2[j * HID + k];
         }
     }
-    const int t = threadIdx.x;
-    const int i = blockIdx.x * MLP_BLOCK + t;
-    const bool live = i < m;
-    const int64_t row = live ? idx[i] : 0;
-    for (int k = 0; k < OBS; ++k) {
-        const float v = live ? obs[row * OBS + k] : 0.0f;
-        col[k][t] = v;
-        if (blockIdx.y == 0 && live) xg[(size_t)i * OBS + k] = v;  // the gathered minibatch observations
+    const int i0 = blockIdx.x * MLP_SPB;
+    for (int e = threadIdx.x; e < OBS * MLP_SPB; e += MLP_BLOCK) {
+        const int k = e / MLP_SPB, sl = e % MLP_SPB, i = i0 + sl;
+        const float v = i < m ? obs[idx[i] * OBS + k] : 0.0f;
+        col[k][sl] = v;
+        if (blockIdx.y == 0 && i < m) xg[(size_t)i * OBS + k] = v;  // the gathered minibatch observations
     }
     __syncthreads();
+    const int sl = threadIdx.x >> 1, u0 = (threadIdx.x & 1) * HALF;
+    const int i = i0 + sl;
     const CW b1 = cw(N.b1), b2 = cw(N.b2), w3 = cw(N.w3), b3 = cw(N.b3);
-    float acc[HID];
+    float acc[HALF];
     // layer 1: h1[j] = tanh(b1[j] + sum_k W1[j][k] x[k])
 #pragma unroll
-    for (int j = 0; j < HID; ++j) acc[j] = b1[j];
+    for (int j = 0; j < HALF; ++j) acc[j] = N.b1[u0 + j];
 #pragma unroll 1
     for (int k = 0; k < OBS; ++k) {
-        const float xv = col[k][t];
-        const float4* w = reinterpret_cast<const float4*>(wt + k * HID);
+        const float xv = col[k][sl];
+        const float4* w = reinterpret_cast<const float4*>(wt + k * HID + u0);
 #pragma unroll
-        for (int j4 = 0; j4 < HID / 4; ++j4) {
+        for (int j4 = 0; j4 < HALF / 4; ++j4) {
             const float4 wv = w[j4];
             acc[4 * j4] += wv.x * xv;
             acc[4 * j4 + 1] += wv.y * xv;
@@ -140,27 +144,28 @@ __global__ __launch_bounds__(MLP_BLOCK) void mlp_forward_kernel(MlpPair P, int m
             acc[4 * j4 + 3] += wv.w * xv;
         }
     }
-    __syncthreads();  // every thread has read its x column before h1 overwrites rows 0..26
+    __syncthreads();  // every x column has been read before h1 overwrites rows 0..26
 #pragma unroll
-    for (int j = 0; j < HID; ++j) {
+    for (int j = 0; j < HALF; ++j) {
         acc[j] = tanhf(acc[j]);
-        col[j][t] = acc[j];
+        col[u0 + j][sl] = acc[j];
     }
-    if (live) {
+    if (i < m) {
 #pragma unroll
-        for (int j = 0; j < HID; j += 4)
-            *reinterpret_cast<float4*>(N.h1 + (size_t)i * HID + j) =
+        for (int j = 0; j < HALF; j += 4)
+            *reinterpret_cast<float4*>(N.h1 + (size_t)i * HID + u0 + j) =
                 make_float4(acc[j], acc[j + 1], acc[j + 2], acc[j + 3]);
     }
-    // layer 2 (each thread reads only its own column: no barrier needed)
+    __syncthreads();  // both halves of h1 are in the column
+    // layer 2 and the output layer
 #pragma unroll
-    for (int j = 0; j < HID; ++j) acc[j] = b2[j];
+    for (int j = 0; j < HALF; ++j) acc[j] = N.b2[u0 + j];
 #pragma unroll 1
     for (int k = 0; k < HID; ++k) {
-        const float hv = col[k][t];
-        const float4* w = reinterpret_cast<const float4*>(wt + OBS * HID + k * HID);
+        const float hv = col[k][sl];
+        const float4* w = reinterpret_cast<const float4*>(wt + OBS * HID + k * HID + u0);
 #pragma unroll
-        for (int j4 = 0; j4 < HID / 4; ++j4) {
+        for (int j4 = 0; j4 < HALF / 4; ++j4) {
             const float4 wv = w[j4];
             acc[4 * j4] += wv.x * hv;
             acc[4 * j4 + 1] += wv.y * hv;
@@ -168,51 +173,61 @@ __global__ __launch_bounds__(MLP_BLOCK) void mlp_forward_kernel(MlpPair P, int m
             acc[4 * j4 + 3] += wv.w * hv;
         }
     }
-    if (!live) return;
-    float o0 = b3[0], o1 = N.od == 2 ? b3[1] : 0.0f;
+    float o0 = 0.0f, o1 = 0.0f;
 #pragma unroll
-    for (int j = 0; j < HID; ++j) {
+    for (int j = 0; j < HALF; ++j) {
         acc[j] = tanhf(acc[j]);
-        o0 += w3[j] * acc[j];
-        if (N.od == 2) o1 += w3[HID + j] * acc[j];
+        o0 += N.w3[u0 + j] * acc[j];
+        if (N.od == 2) o1 += N.w3[HID + u0 + j] * acc[j];
     }
+    o0 += __shfl_xor(o0, 1, 64);  // the sample's other half (adjacent lane)
+    o1 += __shfl_xor(o1, 1, 64);
+    if (i >= m) return;
 #pragma unroll
-    for (int j = 0; j < HID; j += 4)
-        *reinterpret_cast<float4*>(N.h2 + (size_t)i * HID + j) = make_float4(acc[j], acc[j + 1], acc[j + 2], acc[j + 3]);
-    if (N.od == 2) {
-        N.out[2 * i] = o0;
-        N.out[2 * i + 1] = o1;
-    } else {
-        N.out[i] = o0;
+    for (int j = 0; j < HALF; j += 4)
+        *reinterpret_cast<float4*>(N.h2 + (size_t)i * HID + u0 + j) =
+            make_float4(acc[j], acc[j + 1], acc[j + 2], acc[j + 3]);
+    if (u0 == 0) {
+        if (N.od == 2) {
+            N.out[2 * i] = o0 + b3[0];
+            N.out[2 * i + 1] = o1 + b3[1];
+        } else {
+            N.out[i] = o0 + b3[0];
+        }
     }
+    (void)b1;
+    (void)b2;
+    (void)w3;
 }
 
 // the loss head (policy: the clipped surrogate's d/d mean; value: the squared error's d/d V) and the
 // backward pass to the two hidden layers' output gradients; per-workgroup partial sums
 // (sum min(s1, s2), sum (R - V)^2, #clipped, sum dL/dlogp (z0^2 - 1), sum dL/dlogp (z1^2 - 1)):
-// policy blocks fill [b][0, 2, 3, 4], value blocks [nb + b][1]
+// policy blocks fill [b][0, 2, 3, 4], value blocks [nb + b][1].  nbs: adv_stats_kernel's blocks.
 __global__ __launch_bounds__(MLP_BLOCK) void mlp_backward_kernel(MlpPair P, int m, const int64_t* __restrict__ idx,
                                                                  const float* __restrict__ act,
                                                                  const float* __restrict__ old_logp,
                                                                  const float* __restrict__ adv,
                                                                  const float* __restrict__ ret,
                                                                  const float* __restrict__ log_std,
-                                                                 const double* __restrict__ ws, int normalize,
-                                                                 float clip, float vf_coef,
+                                                                 const double* __restrict__ ws, int nbs,
+                                                                 int normalize, float clip, float vf_coef,
                                                                  float* __restrict__ partial) {
     __shared__ double red[MLP_BLOCK / 64];
+    __shared__ __attribute__((aligned(16))) float w2s[HID * HID];
+    __shared__ float gcol[HID][MLP_SPB];
     const MlpNet& N = P.net[blockIdx.y];
-    const CW w2 = cw(N.w2), w3 = cw(N.w3);
-    const int i = blockIdx.x * MLP_BLOCK + threadIdx.x;
+    for (int e = threadIdx.x; e < HID * HID; e += MLP_BLOCK) w2s[e] = N.w2[e];
+    const int sl = threadIdx.x >> 1, u0 = (threadIdx.x & 1) * HALF;
+    const int i = blockIdx.x * MLP_SPB + sl;
     const bool live = i < m;
     double q[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
     float go0 = 0.0f, go1 = 0.0f;
     if (blockIdx.y == 0) {
         float adv_mean = 0.0f, adv_inv = 1.0f;
         if (normalize) {
-            const int nb = gridDim.x;
             double s = 0.0, sq = 0.0;
-            for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+            for (int b = threadIdx.x; b < nbs; b += blockDim.x) {
                 s += ws[2 * b];
                 sq += ws[2 * b + 1];
             }
@@ -222,7 +237,7 @@ __global__ __launch_bounds__(MLP_BLOCK) void mlp_backward_kernel(MlpPair P, int 
             adv_mean = (float)mu;
             adv_inv = 1.0f / ((float)sqrt(var > 0.0 ? var : 0.0) + 1e-8f);
         }
-        if (live) {
+        if (live) {  // both halves compute the head; the first one records it
             const int64_t j = idx[i];
             const float ls0 = log_std[0], ls1 = log_std[1];
             const float is0 = expf(-ls0), is1 = expf(-ls1);
@@ -234,18 +249,22 @@ __global__ __launch_bounds__(MLP_BLOCK) void mlp_backward_kernel(MlpPair P, int 
             const float g_lp = (s1 <= s2) ? a * ratio * (-1.0f / m) : 0.0f;
             go0 = g_lp * z0 * is0;
             go1 = g_lp * z1 * is1;
-            N.gout[2 * i] = go0;
-            N.gout[2 * i + 1] = go1;
-            q[0] = fminf(s1, s2);
-            q[2] = fabsf(ratio - 1.0f) > clip ? 1.0 : 0.0;
-            q[3] = (double)g_lp * (z0 * z0 - 1.0f);
-            q[4] = (double)g_lp * (z1 * z1 - 1.0f);
+            if (u0 == 0) {
+                N.gout[2 * i] = go0;
+                N.gout[2 * i + 1] = go1;
+                q[0] = fminf(s1, s2);
+                q[2] = fabsf(ratio - 1.0f) > clip ? 1.0 : 0.0;
+                q[3] = (double)g_lp * (z0 * z0 - 1.0f);
+                q[4] = (double)g_lp * (z1 * z1 - 1.0f);
+            }
         }
     } else if (live) {
         const float err = ret[idx[i]] - N.out[i];
         go0 = err * (-2.0f * vf_coef / m);
-        N.gout[i] = go0;
-        q[1] = (double)err * err;
+        if (u0 == 0) {
+            N.gout[i] = go0;
+            q[1] = (double)err * err;
+        }
     }
     double t[5];
 #pragma unroll
@@ -255,36 +274,48 @@ __global__ __launch_bounds__(MLP_BLOCK) void mlp_backward_kernel(MlpPair P, int 
 #pragma unroll
         for (int k = 0; k < 5; ++k) o[k] = (float)t[k];
     }
-    if (!live) return;
-    // g2 = (gout W3) * (1 - h2^2), g1 = (g2 W2) * (1 - h1^2)
-    float g2[HID];
-    const float* h2 = N.h2 + (size_t)i * HID;
+    // g2 = (gout W3) * (1 - h2^2): this thread's 32 units, into the sample's LDS column
+    if (live) {
+        const float* h2 = N.h2 + (size_t)i * HID + u0;
 #pragma unroll
-    for (int j = 0; j < HID; j += 4) {
-        const float4 hv = *reinterpret_cast<const float4*>(h2 + j);
-        const float hh[4] = {hv.x, hv.y, hv.z, hv.w};
+        for (int j = 0; j < HALF; j += 4) {
+            const float4 hv = *reinterpret_cast<const float4*>(h2 + j);
+            const float hh[4] = {hv.x, hv.y, hv.z, hv.w};
+            float g[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            float d = go0 * w3[j + u];
-            if (N.od == 2) d += go1 * w3[HID + j + u];
-            g2[j + u] = d * (1.0f - hh[u] * hh[u]);
+            for (int u = 0; u < 4; ++u) {
+                float d = go0 * N.w3[u0 + j + u];
+                if (N.od == 2) d += go1 * N.w3[HID + u0 + j + u];
+                g[u] = d * (1.0f - hh[u] * hh[u]);
+                gcol[u0 + j + u][sl] = g[u];
+            }
+            *reinterpret_cast<float4*>(N.g2 + (size_t)i * HID + u0 + j) = make_float4(g[0], g[1], g[2], g[3]);
         }
-        *reinterpret_cast<float4*>(N.g2 + (size_t)i * HID + j) = make_float4(g2[j], g2[j + 1], g2[j + 2], g2[j + 3]);
     }
-    // g1[k] = (sum_j g2[j] W2[j][k]) (1 - h1[k]^2): output unit j outermost, W2's rows streamed
-    float g1[HID];
+    __syncthreads();  // W2 staged, both halves of g2 in the column
+    if (!live) return;
+    // g1[k] = (sum_j g2[j] W2[j][k]) (1 - h1[k]^2) for this thread's 32 units k
+    float g1[HALF];
 #pragma unroll
-    for (int k = 0; k < HID; ++k) g1[k] = 0.0f;
-#pragma unroll
+    for (int k = 0; k < HALF; ++k) g1[k] = 0.0f;
+#pragma unroll 1
     for (int j = 0; j < HID; ++j) {
+        const float gv = gcol[j][sl];
+        const float4* w = reinterpret_cast<const float4*>(w2s + j * HID + u0);
 #pragma unroll
-        for (int k = 0; k < HID; ++k) g1[k] += g2[j] * w2[j * HID + k];
+        for (int k4 = 0; k4 < HALF / 4; ++k4) {
+            const float4 wv = w[k4];
+            g1[4 * k4] += gv * wv.x;
+            g1[4 * k4 + 1] += gv * wv.y;
+            g1[4 * k4 + 2] += gv * wv.z;
+            g1[4 * k4 + 3] += gv * wv.w;
+        }
     }
-    const float* h1 = N.h1 + (size_t)i * HID;
+    const float* h1 = N.h1 + (size_t)i * HID + u0;
 #pragma unroll
-    for (int k = 0; k < HID; k += 4) {
+    for (int k = 0; k < HALF; k += 4) {
         const float4 hv = *reinterpret_cast<const float4*>(h1 + k);
-        *reinterpret_cast<float4*>(N.g1 + (size_t)i * HID + k) =
+        *reinterpret_cast<float4*>(N.g1 + (size_t)i * HID + u0 + k) =
             make_float4(g1[k] * (1.0f - hv.x * hv.x), g1[k + 1] * (1.0f - hv.y * hv.y),
                         g1[k + 2] * (1.0f - hv.z * hv.z), g1[k + 3] * (1.0f - hv.w * hv.w));
     }
@@ -489,10 +520,12 @@ int32_t d2d_ppo_mlp_forward(int32_t m, const int64_t* idx, const float* obs, con
                             float* const* bufs, float* xg, void* stream) {
     if (m <= 0) return 0;
     MlpPair P = make_pair(weights, bufs);
-    hipLaunchKernelGGL(mlp_forward_kernel, dim3((m + MLP_BLOCK - 1) / MLP_BLOCK, 2), dim3(MLP_BLOCK), 0,
+    hipLaunchKernelGGL(mlp_forward_kernel, dim3((m + MLP_SPB - 1) / MLP_SPB, 2), dim3(MLP_BLOCK), 0,
                        (hipStream_t)stream, P, m, idx, obs, xg);
     return rc(hipGetLastError());
 }
+
+int32_t d2d_ppo_mlp_partial_rows(int32_t m) { return 2 * ((m + MLP_SPB - 1) / MLP_SPB); }
 
 int32_t d2d_ppo_mlp_backward(int32_t m, const int64_t* idx, const float* act, const float* old_logp, const float* adv,
                              const float* ret, const float* log_std, const double* ws, int32_t normalize, float clip,
@@ -502,9 +535,10 @@ int32_t d2d_ppo_mlp_backward(int32_t m, const int64_t* idx, const float* act, co
     MlpPair P = make_pair(weights, bufs);
     P.net[0].gout = gout[0];
     P.net[1].gout = gout[1];
-    hipLaunchKernelGGL(mlp_backward_kernel, dim3((m + MLP_BLOCK - 1) / MLP_BLOCK, 2), dim3(MLP_BLOCK), 0,
-                       (hipStream_t)stream, P, m, idx, act, old_logp, adv, ret, log_std, ws, normalize, clip, vf_coef,
-                       partial);
+    const int nbs = (m + D2D_PPO_HEAD_BLOCK - 1) / D2D_PPO_HEAD_BLOCK;
+    hipLaunchKernelGGL(mlp_backward_kernel, dim3((m + MLP_SPB - 1) / MLP_SPB, 2), dim3(MLP_BLOCK), 0,
+                       (hipStream_t)stream, P, m, idx, act, old_logp, adv, ret, log_std, ws, nbs, normalize, clip,
+                       vf_coef, partial);
     return rc(hipGetLastError());
 }
 

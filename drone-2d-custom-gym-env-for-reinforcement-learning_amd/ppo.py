@@ -145,6 +145,7 @@ def ppo_native():
             "d2d_ppo_wgrad_chunks": [i32],
             "d2d_ppo_mlp_forward": [i32, vp, vp, vp, vp, vp, vp],
             "d2d_ppo_mlp_backward": [i32, vp, vp, vp, vp, vp, vp, vp, i32, f32, f32, vp, vp, vp, vp, vp],
+            "d2d_ppo_mlp_partial_rows": [i32],
         }
         for name, args in sig.items():
             fn = getattr(lib, name)
@@ -263,7 +264,8 @@ class ManualStep:
                         "h1v": e(M, 64), "h2v": e(M, 64), "val": e(M, 1), "g1v": e(M, 64), "g2v": e(M, 64),
                         "xg": e(M, 27), "gm": e(M, 2), "gv": e(M, 1)}
             self._ws = torch.zeros(nb, 2, dtype=torch.float64, device=dev)
-            self._partial = torch.zeros(2 * nb, 5, device=dev)
+            self._prow = lib.d2d_ppo_mlp_partial_rows(M)
+            self._partial = torch.zeros(self._prow, 5, device=dev)
             self._bufM = M
         hb = self._hb
         pn, vn = pol.mlp_extractor.policy_net, pol.mlp_extractor.value_net
@@ -287,7 +289,7 @@ class ManualStep:
                   (hb["g1v"], hb["xg"], vn[0]))
         self._wgrad_hip(M, layers)
         ls = pol.log_std
-        _ok(lib.d2d_ppo_head_finish(M, 2 * nb, self._partial.data_ptr(), ls.data_ptr(), cfg.ent_coef,
+        _ok(lib.d2d_ppo_head_finish(M, self._prow, self._partial.data_ptr(), ls.data_ptr(), cfg.ent_coef,
                                     ls.grad.data_ptr(), acc["policy_loss"].data_ptr(), acc["value_loss"].data_ptr(),
                                     acc["entropy"].data_ptr(), acc["clip_fraction"].data_ptr(), st),
             "d2d_ppo_head_finish")

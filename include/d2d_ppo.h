@@ -52,19 +52,20 @@ int32_t d2d_ppo_wgrad(int32_t m, int32_t n_problems, const float* const* a, cons
                       const int32_t* b_off, int32_t row_len, float* partial, float* g, void* stream);
 int32_t d2d_ppo_wgrad_chunks(int32_t m);
 
-/* The two MLPs (policy 27-64-64-2, value 27-64-64-1, tanh) per minibatch sample, one thread per
- * (sample, net).  weights: 12 device pointers, per net (policy, then value): W1 [64][27], b1 [64],
+/* The two MLPs (policy 27-64-64-2, value 27-64-64-1, tanh) per minibatch sample, two threads per
+ * (sample, net) each owning half of every layer's units.  weights: 12 device pointers, per net (policy, then value): W1 [64][27], b1 [64],
  * W2 [64][64], b2 [64], W3 [od][64], b3 [od].  bufs: 10 device pointers, per net: h1 [m][64],
  * h2 [m][64], out [m][od] (the action mean / the value), g1 [m][64], g2 [m][64].
  * mlp_forward: the rollout rows idx[0..m) of obs [.][27] through both nets (h1, h2, out) and the
  * gathered observations into xg [m][27].  mlp_backward: the loss head below (gout[0] =
- * d loss / d mean [m][2], gout[1] = d loss / d value [m]; partial[2][ceil(m / 256)][5], finished by
- * d2d_ppo_head_finish with n_blocks = 2 ceil(m / 256)) and the hidden layers' output gradients g2, g1.
+ * d loss / d mean [m][2], gout[1] = d loss / d value [m]; partial[d2d_ppo_mlp_partial_rows(m)][5],
+ * finished by d2d_ppo_head_finish with n_blocks = d2d_ppo_mlp_partial_rows(m)) and the hidden layers' output gradients g2, g1.
  * The head: Gaussian log-density of act under (mean, exp(log_std)), ratio = exp(logp - old_logp),
  * clipped surrogate with advantages normalised by d2d_ppo_adv_stats' partials (normalize != 0),
  * squared value error scaled by vf_coef. */
 int32_t d2d_ppo_mlp_forward(int32_t m, const int64_t* idx, const float* obs, const float* const* weights,
                             float* const* bufs, float* xg, void* stream);
+int32_t d2d_ppo_mlp_partial_rows(int32_t m);
 int32_t d2d_ppo_mlp_backward(int32_t m, const int64_t* idx, const float* act, const float* old_logp, const float* adv,
                              const float* ret, const float* log_std, const double* ws, int32_t normalize, float clip,
                              float vf_coef, const float* const* weights, float* const* bufs, float* const* gout,
