@@ -385,25 +385,29 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradProblems P, int m, int 
     float acc[4][4] = {};
     float bsum[4] = {0.0f, 0.0f, 0.0f, 0.0f};
     const int r0 = blockIdx.x * WG_ROWS, r1 = min(m, r0 + WG_ROWS);
+    // element v of this thread's share of a tile: row (tid + 256 v) / 64, column (tid + 256 v) % 64;
+    // the next tile is loaded into registers while the current one is multiplied
+    constexpr int PER = WG_TILE * 64 / 256;
+    float ra[PER], rb[PER];
+    auto fetch = [&](int rt) {
+#pragma unroll
+        for (int v = 0; v < PER; ++v) {
+            const int e = threadIdx.x + 256 * v, r = e >> 6, c = e & 63, row = rt + r;
+            ra[v] = (row < r1 && c < p) ? pr.a[(size_t)row * pr.lda + c] : 0.0f;
+            rb[v] = (row < r1 && c < q) ? pr.b[(size_t)row * pr.ldb + c] : 0.0f;
+        }
+    };
+    fetch(r0);
     for (int rt = r0; rt < r1; rt += WG_TILE) {
-        __syncthreads();
-        if (p == 64 && pr.lda == 64 && q == 64 && pr.ldb == 64 && rt + WG_TILE <= r1) {
-            // full 64 x 64 tiles of dense rows: 16-byte loads
-            for (int e = threadIdx.x; e < WG_TILE * 16; e += 256) {
-                const int r = e >> 4, c = (e & 15) * 4;
-                *reinterpret_cast<float4*>(&ta[r][c]) =
-                    *reinterpret_cast<const float4*>(pr.a + (size_t)(rt + r) * 64 + c);
-                *reinterpret_cast<float4*>(&tb[r][c]) =
-                    *reinterpret_cast<const float4*>(pr.b + (size_t)(rt + r) * 64 + c);
-            }
-        } else {
-            for (int e = threadIdx.x; e < WG_TILE * 64; e += 256) {
-                const int r = e >> 6, c = e & 63, row = rt + r;
-                ta[r][c] = (row < r1 && c < p) ? pr.a[(size_t)row * pr.lda + c] : 0.0f;
-                tb[r][c] = (row < r1 && c < q) ? pr.b[(size_t)row * pr.ldb + c] : 0.0f;
-            }
+        __syncthreads();  // the previous tile's products are done
+#pragma unroll
+        for (int v = 0; v < PER; ++v) {
+            const int e = threadIdx.x + 256 * v;
+            ta[e >> 6][e & 63] = ra[v];
+            tb[e >> 6][e & 63] = rb[v];
         }
         __syncthreads();
+        if (rt + WG_TILE < r1) fetch(rt + WG_TILE);
         if (pi < p && qi < q) {
 #pragma unroll 8
             for (int r = 0; r < WG_TILE; ++r) {
