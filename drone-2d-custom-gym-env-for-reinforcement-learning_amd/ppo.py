@@ -202,8 +202,8 @@ class ManualStep:
         self.t = torch.zeros((), device=device)
         # the fused element-wise kernels on a GPU (libd2d_ppo.so, loud if missing); torch ops on CPU
         self.lib = ppo_native() if torch.device(device).type == "cuda" else None
-        self._ws = self._partial = self._wpart = None
-        self._bufM = -1
+        self._wpart = None
+        self._bufs = {}  # minibatch size -> (work buffers, partial rows) of the HIP path
         o = 0
         for p in params:
             k = p.numel()
@@ -258,16 +258,18 @@ class ManualStep:
         obs_all, act_all, ol_all, adv_all, ret_all = rollout
         M, dev = idx.numel(), self.P.device
         nb = (M + 255) // 256
-        if self._bufM != M:
+        if M not in self._bufs:
+            # one set of work buffers per minibatch size, kept for the handle's life: a captured graph
+            # holds the full-size set's addresses while a ragged last minibatch runs eagerly on its own
             e = lambda *sh: torch.empty(*sh, device=dev)  # noqa: E731
-            self._hb = {"h1p": e(M, 64), "h2p": e(M, 64), "mean": e(M, 2), "g1p": e(M, 64), "g2p": e(M, 64),
-                        "h1v": e(M, 64), "h2v": e(M, 64), "val": e(M, 1), "g1v": e(M, 64), "g2v": e(M, 64),
-                        "xg": e(M, 27), "gm": e(M, 2), "gv": e(M, 1)}
-            self._ws = torch.zeros(nb, 2, dtype=torch.float64, device=dev)
-            self._prow = lib.d2d_ppo_mlp_partial_rows(M)
-            self._partial = torch.zeros(self._prow, 5, device=dev)
-            self._bufM = M
-        hb = self._hb
+            hb = {"h1p": e(M, 64), "h2p": e(M, 64), "mean": e(M, 2), "g1p": e(M, 64), "g2p": e(M, 64),
+                  "h1v": e(M, 64), "h2v": e(M, 64), "val": e(M, 1), "g1v": e(M, 64), "g2v": e(M, 64),
+                  "xg": e(M, 27), "gm": e(M, 2), "gv": e(M, 1),
+                  "ws": torch.zeros(nb, 2, dtype=torch.float64, device=dev)}
+            prow = lib.d2d_ppo_mlp_partial_rows(M)
+            hb["partial"] = torch.zeros(prow, 5, device=dev)
+            self._bufs[M] = (hb, prow)
+        hb, prow = self._bufs[M]
         pn, vn = pol.mlp_extractor.policy_net, pol.mlp_extractor.value_net
         ws = [pn[0].weight, pn[0].bias, pn[2].weight, pn[2].bias, pol.action_net.weight, pol.action_net.bias,
               vn[0].weight, vn[0].bias, vn[2].weight, vn[2].bias, pol.value_net.weight, pol.value_net.bias]
@@ -277,19 +279,19 @@ class ManualStep:
         gptr = (C.c_void_p * 2)(hb["gm"].data_ptr(), hb["gv"].data_ptr())
         norm = int(cfg.normalize_advantage and M > 1)
         if norm:
-            _ok(lib.d2d_ppo_adv_stats(M, idx.data_ptr(), adv_all.data_ptr(), self._ws.data_ptr(), st), "adv_stats")
+            _ok(lib.d2d_ppo_adv_stats(M, idx.data_ptr(), adv_all.data_ptr(), hb["ws"].data_ptr(), st), "adv_stats")
         _ok(lib.d2d_ppo_mlp_forward(M, idx.data_ptr(), obs_all.data_ptr(), wptr, bptr, hb["xg"].data_ptr(), st),
             "d2d_ppo_mlp_forward")
         _ok(lib.d2d_ppo_mlp_backward(M, idx.data_ptr(), act_all.data_ptr(), ol_all.data_ptr(), adv_all.data_ptr(),
-                                     ret_all.data_ptr(), pol.log_std.data_ptr(), self._ws.data_ptr(), norm,
-                                     cfg.clip_range, cfg.vf_coef, wptr, bptr, gptr, self._partial.data_ptr(), st),
+                                     ret_all.data_ptr(), pol.log_std.data_ptr(), hb["ws"].data_ptr(), norm,
+                                     cfg.clip_range, cfg.vf_coef, wptr, bptr, gptr, hb["partial"].data_ptr(), st),
             "d2d_ppo_mlp_backward")
         layers = ((hb["gm"], hb["h2p"], pol.action_net), (hb["gv"], hb["h2v"], pol.value_net),
                   (hb["g2p"], hb["h1p"], pn[2]), (hb["g2v"], hb["h1v"], vn[2]), (hb["g1p"], hb["xg"], pn[0]),
                   (hb["g1v"], hb["xg"], vn[0]))
         self._wgrad_hip(M, layers)
         ls = pol.log_std
-        _ok(lib.d2d_ppo_head_finish(M, self._prow, self._partial.data_ptr(), ls.data_ptr(), cfg.ent_coef,
+        _ok(lib.d2d_ppo_head_finish(M, prow, hb["partial"].data_ptr(), ls.data_ptr(), cfg.ent_coef,
                                     ls.grad.data_ptr(), acc["policy_loss"].data_ptr(), acc["value_loss"].data_ptr(),
                                     acc["entropy"].data_ptr(), acc["clip_fraction"].data_ptr(), st),
             "d2d_ppo_head_finish")

@@ -80,14 +80,16 @@ def test_ppo_on_hip_batch(d2):
 
 
 @pytest.mark.gpu
-def test_ppo_graph_update_matches_eager(d2):
-    """The HIP-graph replayed minibatch step computes what the eager step computes."""
+@pytest.mark.parametrize("bs", [4096, 12288])
+def test_ppo_graph_update_matches_eager(d2, bs):
+    """The HIP-graph replayed minibatch step computes what the eager step computes (bs = 12288:
+    every epoch ends with a ragged 8 192-sample minibatch that runs eagerly between replays)."""
     from drone2d_amd.ppo import PPO, PPOConfig
 
     params = []
     for graph in (False, True):
         venv = d2.Drone2dVecEnv(4096, seed=1, **_kw(scenario="corridor"))
-        cfg = PPOConfig.gpu_defaults(n_steps=8, batch_size=4096, n_epochs=2)
+        cfg = PPOConfig.gpu_defaults(n_steps=8, batch_size=bs, n_epochs=4 if bs > 4096 else 2)
         cfg.graph = graph
         algo = PPO(venv, cfg, seed=0)
         assert algo.use_graph == graph
