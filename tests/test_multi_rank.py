@@ -150,7 +150,7 @@ def _check(got, obs, rew, stats):
     assert stats[1] > 0  # episodes finished
 
 
-def _ppo_worker(rank, world, port, out_dir):
+def _ppo_worker(rank, world, port, out_dir, hip=False):
     import sys
 
     here = os.path.dirname(os.path.abspath(__file__))
@@ -165,26 +165,32 @@ def _ppo_worker(rank, world, port, out_dir):
     from oracle_backend import OracleVecBackend
 
     shard.init_process_group_from_env("gloo")
-    off, cnt = shard.shard_range(64, world, rank)
-    be = OracleVecBackend(cnt, seed=5, env_id_offset=off, **dict(_kw(), scenario="corridor"))
-    # rank-dependent init seed on purpose: PPO broadcasts rank 0's parameters
-    algo = PPO(be, PPOConfig(n_steps=8, batch_size=64, n_epochs=2), seed=rank, device="cpu")
+    if hip:  # each rank's HIP shard on cuda:0 of the one-GPU box; gradients all-reduced over gloo
+        off, cnt = shard.shard_range(4096, world, rank)
+        be = shard.make_shard_venv(4096, rank, world, device=torch.device("cuda", 0), seed=5,
+                                   **dict(_kw(), scenario="corridor"))
+        cfg = PPOConfig.gpu_defaults(n_steps=8, batch_size=4096, n_epochs=2)
+        algo = PPO(be, cfg, seed=rank)
+        assert algo.manual is not None and algo.manual.lib is not None and not algo.use_graph
+    else:
+        off, cnt = shard.shard_range(64, world, rank)
+        be = OracleVecBackend(cnt, seed=5, env_id_offset=off, **dict(_kw(), scenario="corridor"))
+        # rank-dependent init seed on purpose: PPO broadcasts rank 0's parameters
+        algo = PPO(be, PPOConfig(n_steps=8, batch_size=64, n_epochs=2), seed=rank, device="cpu")
     hist = algo.learn(2 * 8 * cnt)
     assert len(hist) == 2 and all(np.isfinite(h["value_loss"]) for h in hist)
-    flat = torch.cat([p.detach().reshape(-1) for p in algo.policy.parameters()])
+    flat = torch.cat([p.detach().reshape(-1) for p in algo.policy.parameters()]).cpu()
     torch.save(flat, os.path.join(out_dir, f"ppo_{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
     be.close()
 
 
-def test_two_rank_ppo_keeps_one_policy(tmp_path, d2):
-    """Data-parallel PPO over gloo: each rank rolls out its own env shard, gradients are averaged
-    over the ranks every minibatch, so after two updates both ranks hold the same parameters."""
+def _two_rank_ppo(tmp_path, hip):
     world = 2
     ctx = mp.get_context("spawn")
     port = _free_port()
-    procs = [ctx.Process(target=_ppo_worker, args=(r, world, port, str(tmp_path))) for r in range(world)]
+    procs = [ctx.Process(target=_ppo_worker, args=(r, world, port, str(tmp_path), hip)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -193,3 +199,16 @@ def test_two_rank_ppo_keeps_one_policy(tmp_path, d2):
     a = torch.load(os.path.join(tmp_path, "ppo_0.pt"), weights_only=True)
     b = torch.load(os.path.join(tmp_path, "ppo_1.pt"), weights_only=True)
     assert torch.equal(a, b)
+
+
+def test_two_rank_ppo_keeps_one_policy(tmp_path, d2):
+    """Data-parallel PPO over gloo: each rank rolls out its own env shard, gradients are averaged
+    over the ranks every minibatch, so after two updates both ranks hold the same parameters."""
+    _two_rank_ppo(tmp_path, hip=False)
+
+
+@pytest.mark.gpu
+def test_two_rank_ppo_hip_keeps_one_policy(tmp_path, d2):
+    """The same with each rank's HIP env shard and the libd2d_ppo.so update kernels (two processes
+    on the one GPU; the flat gradient buffer all-reduced over gloo before clip + Adam)."""
+    _two_rank_ppo(tmp_path, hip=True)
