@@ -178,7 +178,7 @@ class ManualStep:
     backward pass of the two 27-64-64 tanh MLPs written out instead of recorded by autograd, over
     flat parameter / gradient / Adam-moment buffers (the module's parameters become views of them),
     and nothing that waits for the host -- the whole step captures into one HIP graph.  On a GPU
-    it is seven libd2d_ppo.so launches (advantage statistics, both MLPs forward with one thread per
+    it is seven libd2d_ppo.so launches (advantage statistics, both MLPs forward with two threads per
     sample and net, loss head + backward to the hidden-layer gradients, all weight / bias gradients
     + their reduce, log_std's gradient and the statistics, clip + Adam) instead of ~190 autograd /
     optimiser kernels; on the CPU the same math in torch ops (split-K weight gradients).
@@ -202,7 +202,6 @@ class ManualStep:
         self.t = torch.zeros((), device=device)
         # the fused element-wise kernels on a GPU (libd2d_ppo.so, loud if missing); torch ops on CPU
         self.lib = ppo_native() if torch.device(device).type == "cuda" else None
-        self._wpart = None
         self._bufs = {}  # minibatch size -> (work buffers, partial rows) of the HIP path
         o = 0
         for p in params:
@@ -250,7 +249,7 @@ class ManualStep:
             torch.sum(a, 0, out=lin.bias.grad)
 
     def _grad_hip(self, idx, rollout, acc):
-        """libd2d_ppo.so: advantage statistics, both MLPs forward (one thread per sample and net),
+        """libd2d_ppo.so: advantage statistics, both MLPs forward (two threads per sample and net),
         loss head + backward to the hidden-layer gradients, all weight / bias gradients, log_std's."""
         import ctypes as C
 
@@ -268,6 +267,7 @@ class ManualStep:
                   "ws": torch.zeros(nb, 2, dtype=torch.float64, device=dev)}
             prow = lib.d2d_ppo_mlp_partial_rows(M)
             hb["partial"] = torch.zeros(prow, 5, device=dev)
+            hb["wpart"] = e(lib.d2d_ppo_wgrad_chunks(M) * self.G.numel())  # weight-gradient partial rows
             self._bufs[M] = (hb, prow)
         hb, prow = self._bufs[M]
         pn, vn = pol.mlp_extractor.policy_net, pol.mlp_extractor.value_net
@@ -289,7 +289,7 @@ class ManualStep:
         layers = ((hb["gm"], hb["h2p"], pol.action_net), (hb["gv"], hb["h2v"], pol.value_net),
                   (hb["g2p"], hb["h1p"], pn[2]), (hb["g2v"], hb["h1v"], vn[2]), (hb["g1p"], hb["xg"], pn[0]),
                   (hb["g1v"], hb["xg"], vn[0]))
-        self._wgrad_hip(M, layers)
+        self._wgrad_hip(M, layers, hb["wpart"])
         ls = pol.log_std
         _ok(lib.d2d_ppo_head_finish(M, prow, hb["partial"].data_ptr(), ls.data_ptr(), cfg.ent_coef,
                                     ls.grad.data_ptr(), acc["policy_loss"].data_ptr(), acc["value_loss"].data_ptr(),
@@ -300,14 +300,12 @@ class ManualStep:
     def _tanh_grad_torch(h, g):
         return g.mul_(1.0 - h * h)
 
-    def _wgrad_hip(self, M, layers):
+    def _wgrad_hip(self, M, layers, wpart):
         """All six weight / bias gradients in one libd2d_ppo.so launch (+ its reduce) into G."""
         import ctypes as C
 
-        nc = self.lib.d2d_ppo_wgrad_chunks(M)
         row_len = self.G.numel()  # all of G: log_std's slots (no problem covers them) are rewritten after
-        if self._wpart is None or self._wpart.numel() < nc * row_len:
-            self._wpart = torch.empty(nc * row_len, device=self.P.device)
+        assert wpart.numel() >= self.lib.d2d_ppo_wgrad_chunks(M) * row_len
         n = len(layers)
         base = self.G.data_ptr()
         arr = lambda ty, v: (ty * n)(*v)  # noqa: E731
@@ -321,8 +319,8 @@ class ManualStep:
         bo = arr(C.c_int32, [(lin.bias.grad.data_ptr() - base) // 4 for _, _, lin in layers])
         for a, b, _ in layers:
             assert a.stride(1) == 1 and b.stride(1) == 1 and a.shape[0] == b.shape[0] == M
-        _ok(self.lib.d2d_ppo_wgrad(M, n, a_p, lda, b_p, ldb, pp, qq, wo, bo, row_len, self._wpart.data_ptr(),
-                                   base, self._stream()), "d2d_ppo_wgrad")
+        _ok(self.lib.d2d_ppo_wgrad(M, n, a_p, lda, b_p, ldb, pp, qq, wo, bo, row_len, wpart.data_ptr(), base,
+                                   self._stream()), "d2d_ppo_wgrad")
 
     def _stream(self):
         return torch.cuda.current_stream(self.P.device).cuda_stream
