@@ -93,10 +93,13 @@ constexpr int MLP_BLOCK = 256, OBS = 27, HID = 64;
 using CW = const __attribute__((address_space(4))) float*;
 __device__ __forceinline__ CW cw(const float* p) { return (CW)p; }
 
-// Two threads per (sample, net): thread t of a workgroup serves sample t / 2 of the workgroup's
-// MLP_SPB and owns output units [32 (t & 1), 32 (t & 1) + 32) of every layer; the layer inputs of a
-// sample (x, h1; g2 in the backward pass) are an LDS column both of its threads read.
-constexpr int MLP_SPB = MLP_BLOCK / 2, HALF = HID / 2;
+// TPS threads per (sample, net): thread t of a workgroup serves sample t / TPS of the workgroup's
+// MLP_SPB and owns output units [UNITS (t % TPS), UNITS (t % TPS + 1)) of every layer; the layer
+// inputs of a sample (x, h1; g2 in the backward pass) are an LDS column all its threads read.
+#ifndef D2D_PPO_TPS
+#define D2D_PPO_TPS 4  // threads per (sample, net)
+#endif
+constexpr int TPS = D2D_PPO_TPS, MLP_SPB = MLP_BLOCK / TPS, UNITS = HID / TPS;
 constexpr int WT_NET = OBS * HID + HID * HID;
 
 // W1^T [27][64] and W2^T [64][64] of the workgroup's net staged in LDS: input unit k outermost (a
@@ -124,19 +127,19 @@ __global__ __launch_bounds__(MLP_BLOCK) void mlp_forward_kernel(MlpPair P, int m
         if (blockIdx.y == 0 && i < m) xg[(size_t)i * OBS + k] = v;  // the gathered minibatch observations
     }
     __syncthreads();
-    const int sl = threadIdx.x >> 1, u0 = (threadIdx.x & 1) * HALF;
+    const int sl = threadIdx.x / TPS, u0 = (threadIdx.x % TPS) * UNITS;
     const int i = i0 + sl;
     const CW b1 = cw(N.b1), b2 = cw(N.b2), w3 = cw(N.w3), b3 = cw(N.b3);
-    float acc[HALF];
+    float acc[UNITS];
     // layer 1: h1[j] = tanh(b1[j] + sum_k W1[j][k] x[k])
 #pragma unroll
-    for (int j = 0; j < HALF; ++j) acc[j] = N.b1[u0 + j];
+    for (int j = 0; j < UNITS; ++j) acc[j] = N.b1[u0 + j];
 #pragma unroll 1
     for (int k = 0; k < OBS; ++k) {
         const float xv = col[k][sl];
         const float4* w = reinterpret_cast<const float4*>(wt + k * HID + u0);
 #pragma unroll
-        for (int j4 = 0; j4 < HALF / 4; ++j4) {
+        for (int j4 = 0; j4 < UNITS / 4; ++j4) {
             const float4 wv = w[j4];
             acc[4 * j4] += wv.x * xv;
             acc[4 * j4 + 1] += wv.y * xv;
@@ -146,26 +149,26 @@ __global__ __launch_bounds__(MLP_BLOCK) void mlp_forward_kernel(MlpPair P, int m
     }
     __syncthreads();  // every x column has been read before h1 overwrites rows 0..26
 #pragma unroll
-    for (int j = 0; j < HALF; ++j) {
+    for (int j = 0; j < UNITS; ++j) {
         acc[j] = tanhf(acc[j]);
         col[u0 + j][sl] = acc[j];
     }
     if (i < m) {
 #pragma unroll
-        for (int j = 0; j < HALF; j += 4)
+        for (int j = 0; j < UNITS; j += 4)
             *reinterpret_cast<float4*>(N.h1 + (size_t)i * HID + u0 + j) =
                 make_float4(acc[j], acc[j + 1], acc[j + 2], acc[j + 3]);
     }
     __syncthreads();  // both halves of h1 are in the column
     // layer 2 and the output layer
 #pragma unroll
-    for (int j = 0; j < HALF; ++j) acc[j] = N.b2[u0 + j];
+    for (int j = 0; j < UNITS; ++j) acc[j] = N.b2[u0 + j];
 #pragma unroll 1
     for (int k = 0; k < HID; ++k) {
         const float hv = col[k][sl];
         const float4* w = reinterpret_cast<const float4*>(wt + OBS * HID + k * HID + u0);
 #pragma unroll
-        for (int j4 = 0; j4 < HALF / 4; ++j4) {
+        for (int j4 = 0; j4 < UNITS / 4; ++j4) {
             const float4 wv = w[j4];
             acc[4 * j4] += wv.x * hv;
             acc[4 * j4 + 1] += wv.y * hv;
@@ -175,16 +178,19 @@ __global__ __launch_bounds__(MLP_BLOCK) void mlp_forward_kernel(MlpPair P, int m
     }
     float o0 = 0.0f, o1 = 0.0f;
 #pragma unroll
-    for (int j = 0; j < HALF; ++j) {
+    for (int j = 0; j < UNITS; ++j) {
         acc[j] = tanhf(acc[j]);
         o0 += N.w3[u0 + j] * acc[j];
         if (N.od == 2) o1 += N.w3[HID + u0 + j] * acc[j];
     }
-    o0 += __shfl_xor(o0, 1, 64);  // the sample's other half (adjacent lane)
-    o1 += __shfl_xor(o1, 1, 64);
+#pragma unroll
+    for (int o = 1; o < TPS; o <<= 1) {  // the sample's other threads (adjacent lanes)
+        o0 += __shfl_xor(o0, o, 64);
+        o1 += __shfl_xor(o1, o, 64);
+    }
     if (i >= m) return;
 #pragma unroll
-    for (int j = 0; j < HALF; j += 4)
+    for (int j = 0; j < UNITS; j += 4)
         *reinterpret_cast<float4*>(N.h2 + (size_t)i * HID + u0 + j) =
             make_float4(acc[j], acc[j + 1], acc[j + 2], acc[j + 3]);
     if (u0 == 0) {
@@ -218,7 +224,7 @@ __global__ __launch_bounds__(MLP_BLOCK) void mlp_backward_kernel(MlpPair P, int 
     __shared__ float gcol[HID][MLP_SPB];
     const MlpNet& N = P.net[blockIdx.y];
     for (int e = threadIdx.x; e < HID * HID; e += MLP_BLOCK) w2s[e] = N.w2[e];
-    const int sl = threadIdx.x >> 1, u0 = (threadIdx.x & 1) * HALF;
+    const int sl = threadIdx.x / TPS, u0 = (threadIdx.x % TPS) * UNITS;
     const int i = blockIdx.x * MLP_SPB + sl;
     const bool live = i < m;
     double q[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
@@ -278,7 +284,7 @@ __global__ __launch_bounds__(MLP_BLOCK) void mlp_backward_kernel(MlpPair P, int 
     if (live) {
         const float* h2 = N.h2 + (size_t)i * HID + u0;
 #pragma unroll
-        for (int j = 0; j < HALF; j += 4) {
+        for (int j = 0; j < UNITS; j += 4) {
             const float4 hv = *reinterpret_cast<const float4*>(h2 + j);
             const float hh[4] = {hv.x, hv.y, hv.z, hv.w};
             float g[4];
@@ -295,15 +301,15 @@ __global__ __launch_bounds__(MLP_BLOCK) void mlp_backward_kernel(MlpPair P, int 
     __syncthreads();  // W2 staged, both halves of g2 in the column
     if (!live) return;
     // g1[k] = (sum_j g2[j] W2[j][k]) (1 - h1[k]^2) for this thread's 32 units k
-    float g1[HALF];
+    float g1[UNITS];
 #pragma unroll
-    for (int k = 0; k < HALF; ++k) g1[k] = 0.0f;
+    for (int k = 0; k < UNITS; ++k) g1[k] = 0.0f;
 #pragma unroll 1
     for (int j = 0; j < HID; ++j) {
         const float gv = gcol[j][sl];
         const float4* w = reinterpret_cast<const float4*>(w2s + j * HID + u0);
 #pragma unroll
-        for (int k4 = 0; k4 < HALF / 4; ++k4) {
+        for (int k4 = 0; k4 < UNITS / 4; ++k4) {
             const float4 wv = w[k4];
             g1[4 * k4] += gv * wv.x;
             g1[4 * k4 + 1] += gv * wv.y;
@@ -313,7 +319,7 @@ __global__ __launch_bounds__(MLP_BLOCK) void mlp_backward_kernel(MlpPair P, int 
     }
     const float* h1 = N.h1 + (size_t)i * HID + u0;
 #pragma unroll
-    for (int k = 0; k < HALF; k += 4) {
+    for (int k = 0; k < UNITS; k += 4) {
         const float4 hv = *reinterpret_cast<const float4*>(h1 + k);
         *reinterpret_cast<float4*>(N.g1 + (size_t)i * HID + u0 + k) =
             make_float4(g1[k] * (1.0f - hv.x * hv.x), g1[k + 1] * (1.0f - hv.y * hv.y),

@@ -178,7 +178,7 @@ class ManualStep:
     backward pass of the two 27-64-64 tanh MLPs written out instead of recorded by autograd, over
     flat parameter / gradient / Adam-moment buffers (the module's parameters become views of them),
     and nothing that waits for the host -- the whole step captures into one HIP graph.  On a GPU
-    it is seven libd2d_ppo.so launches (advantage statistics, both MLPs forward with two threads per
+    it is seven libd2d_ppo.so launches (advantage statistics, both MLPs forward with four threads per
     sample and net, loss head + backward to the hidden-layer gradients, all weight / bias gradients
     + their reduce, log_std's gradient and the statistics, clip + Adam) instead of ~190 autograd /
     optimiser kernels; on the CPU the same math in torch ops (split-K weight gradients).
@@ -249,7 +249,7 @@ class ManualStep:
             torch.sum(a, 0, out=lin.bias.grad)
 
     def _grad_hip(self, idx, rollout, acc):
-        """libd2d_ppo.so: advantage statistics, both MLPs forward (two threads per sample and net),
+        """libd2d_ppo.so: advantage statistics, both MLPs forward (four threads per sample and net),
         loss head + backward to the hidden-layer gradients, all weight / bias gradients, log_std's."""
         import ctypes as C
 

@@ -52,8 +52,8 @@ int32_t d2d_ppo_wgrad(int32_t m, int32_t n_problems, const float* const* a, cons
                       const int32_t* b_off, int32_t row_len, float* partial, float* g, void* stream);
 int32_t d2d_ppo_wgrad_chunks(int32_t m);
 
-/* The two MLPs (policy 27-64-64-2, value 27-64-64-1, tanh) per minibatch sample, two threads per
- * (sample, net) each owning half of every layer's units.  weights: 12 device pointers, per net (policy, then value): W1 [64][27], b1 [64],
+/* The two MLPs (policy 27-64-64-2, value 27-64-64-1, tanh) per minibatch sample, four threads per
+ * (sample, net) each owning a quarter of every layer's units.  weights: 12 device pointers, per net (policy, then value): W1 [64][27], b1 [64],
  * W2 [64][64], b2 [64], W3 [od][64], b3 [od].  bufs: 10 device pointers, per net: h1 [m][64],
  * h2 [m][64], out [m][od] (the action mean / the value), g1 [m][64], g2 [m][64].
  * mlp_forward: the rollout rows idx[0..m) of obs [.][27] through both nets (h1, h2, out) and the
