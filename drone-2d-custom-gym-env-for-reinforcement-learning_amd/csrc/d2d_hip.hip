@@ -52,6 +52,7 @@ struct d2d_handle {
     // pool_base (host copy; the kernels read *pool_dev), d2d_refresh_pool fills and switches halves
     int pool_base = 0, pool_n = 0;
     int32_t* pool_dev = nullptr;
+    int32_t* fill_ctl = nullptr;  // [2] K4's tick and finished-workgroup count
     uint64_t seed = 0;
     bool reset_done = false;
     uint64_t* stamps = nullptr;  // diagnostic builds (D2D_STAMPS) only
@@ -83,6 +84,9 @@ StepArgs make_args(const d2d_t* h) {
     a.env_scn = h->env_scn;
     a.pool_base = h->pool_dev;
     a.pool_n = h->pool_n;
+    a.fill_ctl = h->fill_ctl;
+    a.fill_every = D2D_FILL_EVERY;
+    a.fill_force = 0;
     a.cfg = h->cfg;
     a.damping_dt = std::pow(h->cfg.damping, 1.0 / 60.0);
     a.seed = h->seed;
@@ -96,8 +100,9 @@ StepArgs make_args(const d2d_t* h) {
 }
 
 // K4: fill every cache entry that does not belong to its env's current episode, ordered on `stream`
-hipError_t rc_fill(d2d_t* h, hipStream_t stream) {
+hipError_t rc_fill(d2d_t* h, hipStream_t stream, bool force = false) {
     StepArgs a = make_args(h);
+    a.fill_force = force ? 1 : 0;
     const int spb = (D2D_FILL_SPLIT && D2D_FILL_COMPACT) ? FILL_SPB : BLOCK;
     const dim3 grid((h->ns + spb - 1) / spb);
     if (sizeof(d2d::Scn) * (size_t)h->n_scn <= K2_LDS_BUDGET)
@@ -108,8 +113,8 @@ hipError_t rc_fill(d2d_t* h, hipStream_t stream) {
 }
 // drop every entry (new seed, counters or scenarios) and refill, ordered on `stream`
 hipError_t rc_rebuild(d2d_t* h, hipStream_t stream) {
-    hipError_t e = hipMemsetAsync(h->rc_tag, 0xFF, sizeof(int32_t) * (size_t)h->ns, stream);
-    if (e == hipSuccess && D2D_FILL_PERIOD > 0) e = rc_fill(h, stream);
+    hipError_t e = hipMemsetAsync(h->rc_tag, 0xFF, sizeof(int32_t) * D2D_RC_SLOTS * (size_t)h->ns, stream);
+    if (e == hipSuccess && D2D_FILL_PERIOD > 0) e = rc_fill(h, stream, true);
     if (e == hipSuccess) h->rc_dirty = false;
     return e;
 }
@@ -176,13 +181,13 @@ hipError_t alloc_layout(Layout& L, int n, const std::vector<int32_t>& lanes, con
     if ((e = hipMalloc(&L.st, sizeof(double) * D2D_NSTATE * ns)) != hipSuccess ||
         (e = hipMalloc(&L.ist, sizeof(int32_t) * D2D_NISTATE * ns)) != hipSuccess ||
         (e = hipMalloc(&L.acc, sizeof(double) * D2D_NSTATS * ns)) != hipSuccess ||
-        (e = hipMalloc(&L.rc_obs, sizeof(float) * D2D_OBS_DIM * ns)) != hipSuccess ||
-        (e = hipMalloc(&L.rc_rfl, sizeof(int32_t) * ns)) != hipSuccess ||
-        (e = hipMalloc(&L.rc_tag, sizeof(int32_t) * ns)) != hipSuccess ||
+        (e = hipMalloc(&L.rc_obs, sizeof(float) * D2D_OBS_DIM * D2D_RC_SLOTS * ns)) != hipSuccess ||
+        (e = hipMalloc(&L.rc_rfl, sizeof(int32_t) * D2D_RC_SLOTS * ns)) != hipSuccess ||
+        (e = hipMalloc(&L.rc_tag, sizeof(int32_t) * D2D_RC_SLOTS * ns)) != hipSuccess ||
         (e = hipMemset(L.st, 0, sizeof(double) * D2D_NSTATE * ns)) != hipSuccess ||
         (e = hipMemset(L.ist, 0, sizeof(int32_t) * D2D_NISTATE * ns)) != hipSuccess ||
         (e = hipMemset(L.acc, 0, sizeof(double) * D2D_NSTATS * ns)) != hipSuccess ||
-        (e = hipMemset(L.rc_tag, 0xFF, sizeof(int32_t) * ns)) != hipSuccess) {
+        (e = hipMemset(L.rc_tag, 0xFF, sizeof(int32_t) * D2D_RC_SLOTS * ns)) != hipSuccess) {
         free_layout(L);
         return e;
     }
@@ -282,6 +287,8 @@ int32_t d2d_create(const d2d_cfg* cfg, int32_t n_envs, int32_t device, d2d_t** o
     if ((e = hipMalloc(&h->env_scn, sizeof(int32_t) * n)) != hipSuccess ||
         (e = hipMalloc(&h->pool_dev, sizeof(int32_t))) != hipSuccess ||
         (e = hipMemset(h->pool_dev, 0, sizeof(int32_t))) != hipSuccess ||
+        (e = hipMalloc(&h->fill_ctl, 2 * sizeof(int32_t))) != hipSuccess ||
+        (e = hipMemset(h->fill_ctl, 0, 2 * sizeof(int32_t))) != hipSuccess ||
         (e = alloc_layout(L, n_envs, {}, {})) != hipSuccess) {
         d2d_destroy(h);
         return hip_fail(e, "d2d_create: hipMalloc");
@@ -305,6 +312,7 @@ void d2d_destroy(d2d_t* h) {
     if (h->brt) (void)hipFree(h->brt);
     if (h->env_scn) (void)hipFree(h->env_scn);
     if (h->pool_dev) (void)hipFree(h->pool_dev);
+    if (h->fill_ctl) (void)hipFree(h->fill_ctl);
     delete h;
 }
 

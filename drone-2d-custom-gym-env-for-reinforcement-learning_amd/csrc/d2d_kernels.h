@@ -71,6 +71,9 @@ struct StepArgs {
     const Scn* scn;          // [n_scn]
     const BrTab* brt;        // [n_scn] golden-march tables (d2d_brtab_kernel), or null
     int32_t* env_scn;        // [n] or null (all scenario 0); rewritten at resets in pool mode
+    int32_t* fill_ctl;         // K4's device tick [0] and finished-workgroup count [1]
+    int fill_every;            // K4 fills on every fill_every-th launch (the tick), others exit
+    int fill_force;            // K4 fills regardless of the tick (rebuilds)
     const int32_t* pool_base;  // pool mode: resets draw from scenarios [*pool_base, *pool_base + pool_n);
     int pool_n;                // d2d_refresh_pool switches *pool_base between the two table halves
                                // (device memory, so captured graphs follow a refresh)
@@ -87,9 +90,9 @@ struct StepArgs {
     const uint8_t* mask;     // reset kernel only
     uint64_t* stamps;        // diagnostic builds only (D2D_STAMPS): [waves][8] s_memtime stamps
     // auto-reset observation cache (handle-internal; see "Auto-reset observation cache" below)
-    float* rc_obs;           // [n][27] next reset observation
-    int32_t* rc_rfl;         // [n] flags of the next reset observation (LA lock)
-    int32_t* rc_tag;         // [n] episode counter the entry belongs to (-1: none)
+    float* rc_obs;           // [D2D_RC_SLOTS][n][27] reset observations (rc_entry: the slot of a key)
+    int32_t* rc_rfl;         // [D2D_RC_SLOTS][n] their flags (LA lock)
+    int32_t* rc_tag;         // [D2D_RC_SLOTS][n] episode counter an entry belongs to (-1: none)
     // Scenario-grouped slot layout (null unless the env -> scenario map is static and mixed).
     // Internal state lives in slots: slot s holds env lane_env[s] (-1: padding), and slots
     // [64 g, 64 g + 64) all hold envs of scenario wg_scn[g], so K1 workgroup g (after the XCD-aware
@@ -134,16 +137,26 @@ struct StepArgs {
 #ifndef D2D_FILL_COMPACT
 #define D2D_FILL_COMPACT 1  // K4 compacts the envs that need a fill into the leading lanes
 #endif
-constexpr int FILL_SPB = 128;  // K4 split path: slots per block (~26 fills per 16 steps at 65 536 envs)
+#ifndef D2D_RC_SLOTS
+#define D2D_RC_SLOTS 2  // reset-cache entries per env: the next reset's observation and the one after
+#endif
+#ifndef D2D_FILL_PERIOD
+#define D2D_FILL_PERIOD 16  // K4 launched after every this many steps (0: never; graphs of 16 steps)
+#endif
+#ifndef D2D_FILL_EVERY
+#define D2D_FILL_EVERY (D2D_RC_SLOTS == 2 ? 3 : 1)  // of those launches every this many fill (a device tick)
+#endif
+static_assert(D2D_RC_SLOTS == 1 || D2D_RC_SLOTS == 2, "one or two reset-cache slots");
+// K4 split path: slots per block -- about one 64-item round per block between fills (one slot:
+// ~26 fills per 16 steps of 128 slots; two slots: ~35 per 48 steps of 64 slots)
+constexpr int FILL_SPB = (D2D_RC_SLOTS == 2) ? 64 : 128;
 #ifndef D2D_FILL_SPLIT
 #define D2D_FILL_SPLIT 1  // K4: the block's four waves share each round of 64 envs (fill_split)
 #endif
 #ifndef D2D_FILL_SENSE_LATE
 #define D2D_FILL_SENSE_LATE 1  // K4 split: wave 0's sensor part after the first barrier
 #endif
-#ifndef D2D_FILL_PERIOD
-#define D2D_FILL_PERIOD 16  // K4 after every this many steps (0: never; every reset synchronous)
-#endif
+
 
 // Diagnostic phase stamps (separate timing-only build, never in the product): lane 0 of each wave
 // records s_memtime at the phase boundaries of K1 (slots 4, 5: role-specific hand-off points).
@@ -176,6 +189,11 @@ constexpr int FILL_SPB = 128;  // K4 split path: slots per block (~26 fills per 
 #endif
 
 __device__ __forceinline__ const BrTab* brtab(const StepArgs& a, int si) { return a.brt ? a.brt + si : nullptr; }
+// the reset-cache entry of slot i for key ep (the observation of the reset that ends episode ep):
+// slot ep % D2D_RC_SLOTS, so the entries of two consecutive episodes coexist
+__device__ __forceinline__ size_t rc_entry(const StepArgs& a, int i, uint32_t ep) {
+    return (size_t)(D2D_RC_SLOTS == 2 ? (ep & 1u) : 0u) * (size_t)a.ns + (size_t)i;
+}
 
 // Scenarios [first, first + count) into LDS; the returned table is indexed by the global scenario
 // index (a grouped K1 workgroup stages only its own scenario: the base is offset by -first, LDS
@@ -329,6 +347,9 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, Scn* s_scn, K1Shared&
     const int n = a.ns;
     const bool auto_reset = a.cfg.auto_reset != 0;
     STAMP(0);
+    if (D2D_FILL_EVERY > 1 && wg == 0 && threadIdx.x == 0 && a.fill_ctl)  // K4's tick: publish its next value
+        __hip_atomic_store(&a.fill_ctl[0], __hip_atomic_load(&a.fill_ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int ws = (GRP && LDS) ? a.wg_scn[wg] : 0;
     const int s0 = ws >= 0 ? ws : -ws - 2;          // a straddling group: its two scenarios s0, s0 + 1
     const int ncopy = (GRP && LDS) ? (ws >= 0 ? 1 : 2) : a.n_scn;
@@ -437,7 +458,7 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, Scn* s_scn, K1Shared&
             done = cause != 0;
             // which envs end (for W1, W2, W3) and whether their reset observation is cached
             const int32_t ep = fld(a.ist, D2D_I_EPISODE, n, i);
-            const bool cv = done && auto_reset && ((D2D_ABL & 16) != 0 || a.rc_tag[i] == ep);
+            const bool cv = done && auto_reset && ((D2D_ABL & 16) != 0 || a.rc_tag[rc_entry(a, i, (uint32_t)ep)] == ep);
             sh.ep[lane] = (uint32_t)ep;
             sh.cause[lane] = (uint32_t)cause;
             sh.sina[lane] = sn[0];
@@ -566,7 +587,7 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, Scn* s_scn, K1Shared&
         if (__ballot(need) != 0ull) {
             if (need) {
                 if (sh.cvalid[lane] != 0u) {
-                    const float* c = a.rc_obs + (size_t)i * D2D_OBS_DIM;
+                    const float* c = a.rc_obs + rc_entry(a, i, sh.ep[lane]) * D2D_OBS_DIM;
 #pragma unroll
                     for (int k = 0; k < 19; ++k) row[k] = c[k];
                 } else {
@@ -708,10 +729,11 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, Scn* s_scn, K1Shared&
             spawn_state(a, SN, ie, ep, sp);
             uint32_t rfl = 0;
             if (cv) {
-                const float* c = a.rc_obs + (size_t)i * D2D_OBS_DIM + 19;
+                const size_t ce = rc_entry(a, i, ep);
+                const float* c = a.rc_obs + ce * D2D_OBS_DIM + 19;
 #pragma unroll
                 for (int k = 0; k < 8; ++k) po[k] = (double)c[k];
-                rfl = (uint32_t)a.rc_rfl[i];
+                rfl = (uint32_t)a.rc_rfl[ce];
             } else {
                 path_obs(a.cfg, SN, brtab(a, nscn), sp[0], sp[1], sp[2], rfl, po);
             }
@@ -908,8 +930,10 @@ __device__ __forceinline__ void fill_split(const StepArgs& a, const Scn* scns, c
     const int n = a.ns;
     for (int r0 = 0; r0 < total; r0 += 64) {
         const bool act = r0 + lane < total;
-        const int i = list[act ? r0 + lane : r0];  // inactive lanes repeat the round's first env
-        const int32_t ep = fld(a.ist, D2D_I_EPISODE, n, i);
+        const int item = list[act ? r0 + lane : r0];  // inactive lanes repeat the round's first item
+        const int i = item >> 1;                      // slot; key = the env's episode counter + (item & 1)
+        const int32_t ep = fld(a.ist, D2D_I_EPISODE, n, i) + (item & 1);
+        const size_t ce = rc_entry(a, i, (uint32_t)ep);
         const int ie = a.lane_env ? a.lane_env[i] : i;
         const int si = next_scenario(a, ie, (uint32_t)ep);
         const Scn& S = scns[si];
@@ -917,7 +941,7 @@ __device__ __forceinline__ void fill_split(const StepArgs& a, const Scn* scns, c
         double sp[7];
         spawn_state(a, S, ie, (uint32_t)ep, sp);
         if (r0 == 0) FSTAMP(2);
-        float* c = a.rc_obs + (size_t)i * D2D_OBS_DIM;
+        float* c = a.rc_obs + ce * D2D_OBS_DIM;
         if (wave == 0 && !D2D_FILL_SENSE_LATE) {
             double so[19];
             sensor_obs(a.cfg, S, Body{sp[0], sp[1], sp[2], 0.0, 0.0, 0.0}, so);
@@ -975,11 +999,11 @@ __device__ __forceinline__ void fill_split(const StepArgs& a, const Scn* scns, c
             if (act) {
 #pragma unroll
                 for (int k = 0; k < 8; ++k) c[19 + k] = (float)o[k];
-                a.rc_rfl[i] = (int32_t)f;
+                a.rc_rfl[ce] = (int32_t)f;
             }
         }
         __syncthreads();  // the sensor part is stored before the tag; devp is reused next round
-        if (wave == 1 && act) a.rc_tag[i] = ep;
+        if (wave == 1 && act) a.rc_tag[ce] = ep;
     }
 }
 
@@ -989,7 +1013,7 @@ __device__ __forceinline__ void fill_split(const StepArgs& a, const Scn* scns, c
 // envs that do into the leading lanes (ballot + popcount), so the long search runs in as few
 // waves as possible instead of one wave per 64 envs with a few active lanes.
 template <bool LDS>
-__global__ __launch_bounds__(BLOCK) void d2d_fill_kernel(StepArgs a) {
+__device__ __forceinline__ void fill_work(const StepArgs& a) {
     extern __shared__ __attribute__((aligned(16))) Scn s_scn[];
     __shared__ int list[BLOCK];
     __shared__ int cnt[BLOCK / 64];
@@ -998,9 +1022,17 @@ __global__ __launch_bounds__(BLOCK) void d2d_fill_kernel(StepArgs a) {
     const int n = a.ns;
     // slots per block: BLOCK, or FILL_SPB with the split path (about one 64-env round per block)
     const int spb = (D2D_FILL_SPLIT && D2D_FILL_COMPACT) ? FILL_SPB : BLOCK;
-    const int i0 = blockIdx.x * spb + threadIdx.x;  // slot
-    const bool need = ((int)threadIdx.x < spb) && (i0 < n) && (!a.lane_env || a.lane_env[i0] >= 0) &&
-                      (a.rc_tag[i0] != fld(a.ist, D2D_I_EPISODE, n, i0));
+    // work items: (slot, which) -- the entry for the env's current episode counter (which = 0) and,
+    // with two slots, for the next one (which = 1); thread t takes slot t % spb, which t / spb
+    static_assert(D2D_RC_SLOTS == 1 || (D2D_FILL_SPLIT && D2D_FILL_COMPACT && 2 * FILL_SPB <= BLOCK),
+                  "two reset-cache slots need the split, compacting fill with 2 items per slot");
+    const int which = (D2D_RC_SLOTS == 2) ? (int)threadIdx.x / spb : 0;
+    const int i0 = blockIdx.x * spb + ((D2D_RC_SLOTS == 2) ? (int)threadIdx.x % spb : (int)threadIdx.x);  // slot
+    const bool need = ((int)threadIdx.x < D2D_RC_SLOTS * spb) && (i0 < n) &&
+                      (!a.lane_env || a.lane_env[i0] >= 0) && [&] {
+                          const int32_t key = fld(a.ist, D2D_I_EPISODE, n, i0) + which;
+                          return a.rc_tag[rc_entry(a, i0, (uint32_t)key)] != key;
+                      }();
     int i = i0, total = 0;
     if (!D2D_FILL_COMPACT) {
         __syncthreads();
@@ -1016,13 +1048,13 @@ __global__ __launch_bounds__(BLOCK) void d2d_fill_kernel(StepArgs a) {
         off += (w < wave) ? cnt[w] : 0;
         total += cnt[w];
     }
-    if (need) list[off + __popcll(m & ((1ull << lane) - 1ull))] = i0;
+    if (need) list[off + __popcll(m & ((1ull << lane) - 1ull))] = 2 * i0 + which;
     __syncthreads();
     if (D2D_FILL_SPLIT) {
         if (total == 0) return;  // block-uniform
     } else {
         if ((int)threadIdx.x >= total) return;
-        i = list[threadIdx.x];
+        i = list[threadIdx.x] >> 1;
     }
     }
     if (D2D_FILL_SPLIT && D2D_FILL_COMPACT) {
@@ -1044,13 +1076,33 @@ __global__ __launch_bounds__(BLOCK) void d2d_fill_kernel(StepArgs a) {
     uint32_t f = 0;
     sensor_obs(a.cfg, S, Body{sp[0], sp[1], sp[2], 0.0, 0.0, 0.0}, so);
     path_obs(a.cfg, S, brtab(a, si), sp[0], sp[1], sp[2], f, o);
-    float* c = a.rc_obs + (size_t)i * D2D_OBS_DIM;
+    const size_t ce = rc_entry(a, i, (uint32_t)ep);  // (one slot: this path is not built with two)
+    float* c = a.rc_obs + ce * D2D_OBS_DIM;
 #pragma unroll
     for (int k = 0; k < 19; ++k) c[k] = (float)so[k];
 #pragma unroll
     for (int k = 0; k < 8; ++k) c[19 + k] = (float)o[k];
-    a.rc_rfl[i] = (int32_t)f;
-    a.rc_tag[i] = ep;
+    a.rc_rfl[ce] = (int32_t)f;
+    a.rc_tag[ce] = ep;
+}
+
+// The launch cadence is fixed on the host (every D2D_FILL_PERIOD steps, so a captured graph of 16
+// steps holds one launch); with two cache slots only every D2D_FILL_EVERY-th launch fills, decided
+// by a device tick (so a replayed graph alternates too): every workgroup reads ctl[0], workgroup 0
+// writes the next value to ctl[1], and the next K1 launch copies it to ctl[0] -- no workgroup
+// writes what another may still read, and no atomics contend on one address.
+template <bool LDS>
+__global__ __launch_bounds__(BLOCK) void d2d_fill_kernel(StepArgs a) {
+    const bool ticked = !a.fill_force && a.fill_every > 1;
+    bool run = true;
+    if (ticked) {
+        const int tick = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(&a.fill_ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        run = tick % a.fill_every == a.fill_every - 1;
+        if (blockIdx.x == 0 && threadIdx.x == 0)
+            __hip_atomic_store(&a.fill_ctl[1], tick + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (run) fill_work<LDS>(a);
 }
 
 // ------------------------------------------------------------------------- golden-march tables
