@@ -446,6 +446,49 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradProblems P, int m, int 
     }
 }
 
+// The same problems on the matrix cores: v_mfma_f32_32x32x2_f32 (exact f32 in / f32 accumulate),
+// D[i][j] = sum_k A[i][k] B[k][j] with i = a's column (output unit), j = b's column (input unit),
+// k = the minibatch row.  Wave w of workgroup (c, k) owns one 32 x 32 tile of problem k's output
+// (p, q <= 64: up to 2 x 2 tiles) and steps through the chunk's rows two at a time; lane l loads
+// a[row + l / 32][p0 + l % 32] and b[row + l / 32][q0 + l % 32] (coalesced 128-byte halves).  The
+// q0 == 0 waves also sum their a values for the bias.  Same partial-row layout as wgrad_kernel.
+#ifndef D2D_PPO_WGRAD_MFMA
+#define D2D_PPO_WGRAD_MFMA 0  // 1: the matrix-core kernel (measured slower: 55 vs 36 us, load-latency bound)
+#endif
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+__global__ __launch_bounds__(256) void wgrad_mfma_kernel(WgradProblems P, int m, int row_len,
+                                                         float* __restrict__ partial) {
+    const WgradProblem& pr = P.k[blockIdx.y];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int nqt = (pr.q + 31) / 32, npt = (pr.p + 31) / 32;
+    if (wave >= npt * nqt) return;  // an idle wave (no workgroup barriers below)
+    const int p0 = (wave / nqt) * 32, q0 = (wave % nqt) * 32;
+    const int ci = lane & 31, h = lane >> 5;
+    const bool pa = p0 + ci < pr.p, qb = q0 + ci < pr.q;
+    const int r0 = blockIdx.x * WG_ROWS, r1 = min(m, r0 + WG_ROWS);
+    const float* __restrict__ A = pr.a + p0 + ci;
+    const float* __restrict__ B = pr.b + q0 + ci;
+    f32x16 acc = {};
+    float bs = 0.0f;
+#pragma unroll 8
+    for (int t = 0; t < WG_ROWS / 2; ++t) {  // rows past r1 contribute zeros (the last chunk)
+        const int row = r0 + 2 * t + h;
+        const bool ok = row < r1;
+        const float av = (ok && pa) ? A[(size_t)row * pr.lda] : 0.0f;
+        const float bv = (ok && qb) ? B[(size_t)row * pr.ldb] : 0.0f;
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+        bs += av;
+    }
+    float* out = partial + (size_t)blockIdx.x * row_len;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+        const int i = (v & 3) + 8 * (v >> 2) + 4 * h;  // the C/D map of the 32 x 32 MFMA
+        if (p0 + i < pr.p && qb) out[pr.w_off + (p0 + i) * pr.q + q0 + ci] = acc[v];
+    }
+    bs += __shfl_xor(bs, 32, 64);  // both row parities
+    if (q0 == 0 && h == 0 && pa) out[pr.b_off + p0 + ci] = bs;
+}
+
 // g[e] = sum over the n_chunks rows of partial[.][e], e < row_len: 64 elements per workgroup, the
 // chunks split over the workgroup's four waves
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(int n_chunks, int row_len, const float* __restrict__ partial,
@@ -506,7 +549,12 @@ int32_t d2d_ppo_wgrad(int32_t m, int32_t n_problems, const float* const* a, cons
         P.k[k] = WgradProblem{a[k], b[k], lda[k], ldb[k], p[k], q[k], w_off[k], b_off[k]};
     }
     const int nc = (m + WG_ROWS - 1) / WG_ROWS;
-    hipLaunchKernelGGL(wgrad_kernel, dim3(nc, n_problems), dim3(256), 0, (hipStream_t)stream, P, m, row_len, partial);
+    if (D2D_PPO_WGRAD_MFMA)
+        hipLaunchKernelGGL(wgrad_mfma_kernel, dim3(nc, n_problems), dim3(256), 0, (hipStream_t)stream, P, m, row_len,
+                           partial);
+    else
+        hipLaunchKernelGGL(wgrad_kernel, dim3(nc, n_problems), dim3(256), 0, (hipStream_t)stream, P, m, row_len,
+                           partial);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return (int32_t)e;
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((row_len + 63) / 64), dim3(256), 0, (hipStream_t)stream, nc,
