@@ -382,6 +382,12 @@ struct WgradProblems {
 };
 constexpr int WG_TILE = 64, WG_ROWS = 256;
 
+#ifndef D2D_PPO_WGRAD_MFMA
+// 0: VALU 4 x 4 blocks from LDS tiles; 1: matrix cores straight from memory (wgrad_mfma_kernel,
+// 55 vs 36 us: load-latency bound); 2: matrix cores fed from this kernel's LDS tiles
+#define D2D_PPO_WGRAD_MFMA 2
+#endif
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 __global__ __launch_bounds__(256) void wgrad_kernel(WgradProblems P, int m, int row_len, float* __restrict__ partial) {
     __shared__ float ta[WG_TILE][64 + 4];
     __shared__ float tb[WG_TILE][64 + 4];
@@ -390,6 +396,12 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradProblems P, int m, int 
     const int pi = (threadIdx.x >> 4) * 4, qi = (threadIdx.x & 15) * 4;  // this thread's 4 x 4 block
     float acc[4][4] = {};
     float bsum[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    // the matrix-core path's tile of this wave (D2D_PPO_WGRAD_MFMA == 2)
+    const int mw = threadIdx.x >> 6, mci = threadIdx.x & 31, mh = (threadIdx.x >> 5) & 1;
+    const int nqt = (q + 31) / 32, npt = (p + 31) / 32;
+    const int mp0 = (mw / max(nqt, 1)) * 32, mq0 = (mw % max(nqt, 1)) * 32;
+    f32x16 macc = {};
+    float mbs = 0.0f;
     const int r0 = blockIdx.x * WG_ROWS, r1 = min(m, r0 + WG_ROWS);
     // element v of this thread's share of a tile: row (tid + 256 v) / 64, column (tid + 256 v) % 64;
     // the next tile is loaded into registers while the current one is multiplied
@@ -414,7 +426,18 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradProblems P, int m, int 
         }
         __syncthreads();
         if (rt + WG_TILE < r1) fetch(rt + WG_TILE);
-        if (pi < p && qi < q) {
+        if (D2D_PPO_WGRAD_MFMA == 2) {
+            // wave w: the 32 x 32 output tile (p0, q0); lane l: A[k = l / 32][i = l % 32] = a[row][p0 + i],
+            // B[k][j = l % 32] = b[row][q0 + j], row = 2 t + l / 32
+            if (mw < npt * nqt) {
+#pragma unroll 8
+                for (int t = 0; t < WG_TILE / 2; ++t) {
+                    const float av = ta[2 * t + mh][mp0 + mci];
+                    macc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, tb[2 * t + mh][mq0 + mci], macc, 0, 0, 0);
+                    mbs += av;
+                }
+            }
+        } else if (pi < p && qi < q) {
 #pragma unroll 8
             for (int r = 0; r < WG_TILE; ++r) {
                 const float4 av = *reinterpret_cast<const float4*>(&ta[r][pi]);
@@ -435,6 +458,18 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradProblems P, int m, int 
         }
     }
     float* out = partial + (size_t)blockIdx.x * row_len;
+    if (D2D_PPO_WGRAD_MFMA == 2) {
+        if (mw < npt * nqt) {
+#pragma unroll
+            for (int v = 0; v < 16; ++v) {
+                const int i = (v & 3) + 8 * (v >> 2) + 4 * mh;  // the C/D map of the 32 x 32 MFMA
+                if (mp0 + i < p && mq0 + mci < q) out[pr.w_off + (mp0 + i) * q + mq0 + mci] = macc[v];
+            }
+            mbs += __shfl_xor(mbs, 32, 64);
+            if (mq0 == 0 && mh == 0 && mp0 + mci < p) out[pr.b_off + mp0 + mci] = mbs;
+        }
+        return;
+    }
 #pragma unroll
     for (int x = 0; x < 4; ++x) {
         if (pi + x >= p) continue;
@@ -452,10 +487,6 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradProblems P, int m, int 
 // (p, q <= 64: up to 2 x 2 tiles) and steps through the chunk's rows two at a time; lane l loads
 // a[row + l / 32][p0 + l % 32] and b[row + l / 32][q0 + l % 32] (coalesced 128-byte halves).  The
 // q0 == 0 waves also sum their a values for the bias.  Same partial-row layout as wgrad_kernel.
-#ifndef D2D_PPO_WGRAD_MFMA
-#define D2D_PPO_WGRAD_MFMA 0  // 1: the matrix-core kernel (measured slower: 55 vs 36 us, load-latency bound)
-#endif
-typedef float f32x16 __attribute__((ext_vector_type(16)));
 __global__ __launch_bounds__(256) void wgrad_mfma_kernel(WgradProblems P, int m, int row_len,
                                                          float* __restrict__ partial) {
     const WgradProblem& pr = P.k[blockIdx.y];
@@ -549,7 +580,7 @@ int32_t d2d_ppo_wgrad(int32_t m, int32_t n_problems, const float* const* a, cons
         P.k[k] = WgradProblem{a[k], b[k], lda[k], ldb[k], p[k], q[k], w_off[k], b_off[k]};
     }
     const int nc = (m + WG_ROWS - 1) / WG_ROWS;
-    if (D2D_PPO_WGRAD_MFMA)
+    if (D2D_PPO_WGRAD_MFMA == 1)
         hipLaunchKernelGGL(wgrad_mfma_kernel, dim3(nc, n_problems), dim3(256), 0, (hipStream_t)stream, P, m, row_len,
                            partial);
     else

@@ -130,7 +130,8 @@ def ppo_native():
 
         from . import _native  # noqa: F401  (torch owns the HIP runtime first)
 
-        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libd2d_ppo.so")
+        path = os.environ.get("D2D_PPO_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib",
+                                                             "libd2d_ppo.so")  # (env: A/B builds, tools/)
         if not os.path.exists(path):
             raise RuntimeError(f"{path} not found: the HIP extension is not built "
                                "(run `python -c 'import __graft_entry__ as g; g.build()'`)")
