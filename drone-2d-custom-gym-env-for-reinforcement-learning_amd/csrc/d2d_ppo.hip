@@ -10,6 +10,7 @@
 namespace {
 
 constexpr float HALF_LOG_2PI = 0.91893853320467274f;  // 0.5 * log(2 pi)
+typedef float f32x16 __attribute__((ext_vector_type(16)));  // a 32 x 32 f32 MFMA accumulator
 
 // sum over the 64 lanes of a wave (every lane gets the total)
 __device__ __forceinline__ double wave_sum(double x) {
@@ -206,6 +207,111 @@ __global__ __launch_bounds__(MLP_BLOCK) void mlp_forward_kernel(MlpPair P, int m
     (void)w3;
 }
 
+// The forward pass on the matrix cores (v_mfma_f32_32x32x2_f32): a workgroup takes FM_SPB = 32
+// samples and both nets; wave w computes the 32 (samples) x 32 (units) tile [net w / 2, units
+// 32 (w % 2) ..] of each hidden layer, D[i = sample][j = unit] = sum_k A[i][k] B[k][j] with
+// A = the layer input (LDS, one sample per lane) and B = W^T, whose 46 operand values per lane
+// (W's row j = a lane) are loaded once into registers.  The tile's lane holds unit j and 16
+// samples, so h1 goes through LDS (as the next layer's A operand) and so does h2 (the output
+// layers are 64-term dot products per (output row, sample), one thread each, weights in LDS).
+// ~20 KB of LDS per workgroup: 1024 workgroups at m = 32768 keep 4 per CU resident.
+#ifndef D2D_PPO_FWD_MFMA
+#define D2D_PPO_FWD_MFMA 1
+#endif
+constexpr int FM_SPB = 32, FM_TILES = 1, XS = OBS + 2, HS = HID + 1;  // LDS row strides: bank spread
+__global__ __launch_bounds__(256) void mlp_forward_mfma_kernel(MlpPair P, int m, const int64_t* __restrict__ idx,
+                                                               const float* __restrict__ obs,
+                                                               float* __restrict__ xg) {
+    __shared__ float xs[FM_TILES * FM_SPB][XS];
+    __shared__ float hs[2][FM_SPB][HS];  // h1, then h2, of the current 32-sample tile
+    __shared__ int64_t rows[FM_TILES * FM_SPB];
+    __shared__ float w3s[4][HID + 1];  // output rows of both nets (od0 + od1 <= 4), bias in column HID
+    const int sb = blockIdx.x * FM_TILES * FM_SPB, tid = threadIdx.x, od0 = P.net[0].od;
+    const int w = tid >> 6, lane = tid & 63, ci = lane & 31, h = lane >> 5;
+    const int net = w >> 1, j0 = (w & 1) * 32;
+    const MlpNet& N = P.net[net];
+    // the B operands stay in registers for the whole kernel: lane (ci, h) of wave w holds
+    // W[j0 + ci][2 t + h] for every k step t of both layers (14 + 32 VGPRs)
+    float w1r[(OBS + 1) / 2], w2r[HID / 2];
+#pragma unroll
+    for (int t = 0; t < (OBS + 1) / 2; ++t) w1r[t] = 2 * t + h < OBS ? N.w1[(j0 + ci) * OBS + 2 * t + h] : 0.0f;
+#pragma unroll
+    for (int t = 0; t < HID / 2; ++t) w2r[t] = N.w2[(j0 + ci) * HID + 2 * t + h];
+    const float b1 = N.b1[j0 + ci], b2 = N.b2[j0 + ci];
+    {
+        const int orow = tid >> 6, j = tid & 63, on = orow >= od0, r = orow - on * od0;
+        if (orow < od0 + P.net[1].od) {
+            w3s[orow][j] = P.net[on].w3[r * HID + j];
+            if (j == 0) w3s[orow][HID] = P.net[on].b3[r];
+        }
+    }
+    constexpr int NX = FM_TILES * FM_SPB * OBS, NI = (NX + 255) / 256;
+    if (tid < FM_TILES * FM_SPB) {
+        rows[tid] = sb + tid < m ? idx[sb + tid] : -1;
+        xs[tid][OBS] = 0.0f;  // the k padding of the 28-deep layer-1 product
+    }
+    __syncthreads();  // rows
+    {
+        float xv[NI];
+#pragma unroll
+        for (int c = 0; c < NI; ++c) {
+            const int e = c * 256 + tid, sl = e / OBS, k = e % OBS;
+            const int64_t r = e < NX ? rows[sl] : -1;
+            xv[c] = r >= 0 ? obs[r * OBS + k] : 0.0f;
+        }
+#pragma unroll
+        for (int c = 0; c < NI; ++c) {
+            const int e = c * 256 + tid, sl = e / OBS, k = e % OBS;
+            if (e < NX) {
+                xs[sl][k] = xv[c];
+                // the gathered minibatch observations, for the weight gradients
+                if (sb + sl < m) xg[(size_t)sb * OBS + e] = xv[c];
+            }
+        }
+    }
+    for (int tile = 0; tile < FM_TILES; ++tile) {
+        const int s0 = sb + tile * FM_SPB;
+        __syncthreads();  // staging done / the previous tile's outputs have read hs
+        // layer 1 (k = 27 inputs, padded to 28)
+        f32x16 acc = {};
+#pragma unroll
+        for (int t = 0; t < (OBS + 1) / 2; ++t)
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xs[tile * FM_SPB + ci][2 * t + h], w1r[t], acc, 0, 0, 0);
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+            const int i = (v & 3) + 8 * (v >> 2) + 4 * h;  // sample of register v (C/D map)
+            const float y = tanhf(acc[v] + b1);
+            hs[net][i][j0 + ci] = y;
+            if (s0 + i < m) N.h1[(size_t)(s0 + i) * HID + j0 + ci] = y;
+        }
+        __syncthreads();
+        // layer 2
+        acc = f32x16{};
+#pragma unroll
+        for (int t = 0; t < HID / 2; ++t)
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(hs[net][ci][2 * t + h], w2r[t], acc, 0, 0, 0);
+        __syncthreads();  // every wave has read h1 before h2 overwrites it
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+            const int i = (v & 3) + 8 * (v >> 2) + 4 * h;
+            const float y = tanhf(acc[v] + b2);
+            hs[net][i][j0 + ci] = y;
+            if (s0 + i < m) N.h2[(size_t)(s0 + i) * HID + j0 + ci] = y;
+        }
+        __syncthreads();
+        // output layers: thread t -> (output row t / 32 of both nets' od0 + od1 rows, sample t % 32),
+        // weights and biases from LDS
+        if (tid < (od0 + P.net[1].od) * FM_SPB) {
+            const int orow = tid / FM_SPB, sl = tid % FM_SPB, i = s0 + sl, on = orow >= od0;
+            const int r = orow - on * od0;
+            float o = w3s[orow][HID];
+#pragma unroll 16
+            for (int j = 0; j < HID; ++j) o += w3s[orow][j] * hs[on][sl][j];
+            if (i < m) P.net[on].out[(size_t)i * P.net[on].od + r] = o;
+        }
+    }
+}
+
 // the loss head (policy: the clipped surrogate's d/d mean; value: the squared error's d/d V) and the
 // backward pass to the two hidden layers' output gradients; per-workgroup partial sums
 // (sum min(s1, s2), sum (R - V)^2, #clipped, sum dL/dlogp (z0^2 - 1), sum dL/dlogp (z1^2 - 1)):
@@ -223,7 +329,14 @@ __global__ __launch_bounds__(MLP_BLOCK) void mlp_backward_kernel(MlpPair P, int 
     __shared__ __attribute__((aligned(16))) float w2s[HID * HID];
     __shared__ float gcol[HID][MLP_SPB];
     const MlpNet& N = P.net[blockIdx.y];
-    for (int e = threadIdx.x; e < HID * HID; e += MLP_BLOCK) w2s[e] = N.w2[e];
+    {  // W2 into LDS, all four loads per thread in flight before the stores
+        static_assert(HID * HID == 4 * 4 * MLP_BLOCK, "W2 staging");
+        float4 wv[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) wv[c] = reinterpret_cast<const float4*>(N.w2)[c * MLP_BLOCK + threadIdx.x];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) reinterpret_cast<float4*>(w2s)[c * MLP_BLOCK + threadIdx.x] = wv[c];
+    }
     const int sl = threadIdx.x / TPS, u0 = (threadIdx.x % TPS) * UNITS;
     const int i = blockIdx.x * MLP_SPB + sl;
     const bool live = i < m;
@@ -387,7 +500,6 @@ constexpr int WG_TILE = 64, WG_ROWS = 256;
 // 55 vs 36 us: load-latency bound); 2: matrix cores fed from this kernel's LDS tiles
 #define D2D_PPO_WGRAD_MFMA 2
 #endif
-typedef float f32x16 __attribute__((ext_vector_type(16)));
 __global__ __launch_bounds__(256) void wgrad_kernel(WgradProblems P, int m, int row_len, float* __restrict__ partial) {
     __shared__ float ta[WG_TILE][64 + 4];
     __shared__ float tb[WG_TILE][64 + 4];
@@ -609,8 +721,12 @@ int32_t d2d_ppo_mlp_forward(int32_t m, const int64_t* idx, const float* obs, con
                             float* const* bufs, float* xg, void* stream) {
     if (m <= 0) return 0;
     MlpPair P = make_pair(weights, bufs);
-    hipLaunchKernelGGL(mlp_forward_kernel, dim3((m + MLP_SPB - 1) / MLP_SPB, 2), dim3(MLP_BLOCK), 0,
-                       (hipStream_t)stream, P, m, idx, obs, xg);
+    if (D2D_PPO_FWD_MFMA)
+        hipLaunchKernelGGL(mlp_forward_mfma_kernel, dim3((m + FM_TILES * FM_SPB - 1) / (FM_TILES * FM_SPB)), dim3(256), 0,
+                           (hipStream_t)stream, P, m, idx, obs, xg);
+    else
+        hipLaunchKernelGGL(mlp_forward_kernel, dim3((m + MLP_SPB - 1) / MLP_SPB, 2), dim3(MLP_BLOCK), 0,
+                           (hipStream_t)stream, P, m, idx, obs, xg);
     return rc(hipGetLastError());
 }
 
