@@ -207,37 +207,77 @@ __global__ __launch_bounds__(MLP_BLOCK) void mlp_forward_kernel(MlpPair P, int m
     (void)w3;
 }
 
-// The forward pass on the matrix cores (v_mfma_f32_32x32x2_f32): a workgroup takes FM_SPB = 32
-// samples and both nets; wave w computes the 32 (samples) x 32 (units) tile [net w / 2, units
-// 32 (w % 2) ..] of each hidden layer, D[i = sample][j = unit] = sum_k A[i][k] B[k][j] with
-// A = the layer input (LDS, one sample per lane) and B = W^T, whose 46 operand values per lane
-// (W's row j = a lane) are loaded once into registers.  The tile's lane holds unit j and 16
-// samples, so h1 goes through LDS (as the next layer's A operand) and so does h2 (the output
-// layers are 64-term dot products per (output row, sample), one thread each, weights in LDS).
-// ~20 KB of LDS per workgroup: 1024 workgroups at m = 32768 keep 4 per CU resident.
+// The forward pass on the matrix cores (v_mfma_f32_32x32x2_f32): a workgroup takes FM_TILES = 2
+// tiles of FM_SPB = 32 samples and both nets; wave w computes the 32 (samples) x 32 (units) tile
+// [net w / 2, units 32 (w % 2) ..] of each hidden layer, D[i = sample][j = unit] = sum_k A[i][k] B[k][j]
+// with A = the layer input (LDS, one sample per lane) and B = W^T, whose 46 operand values per lane
+// (W's row j = a lane) are staged once through LDS into registers.  The tile's lane holds unit j and
+// 16 samples, so h1 goes through LDS (as the next layer's A operand, and to global memory as row
+// stores) and so does h2 (the output layers are 64-term dot products per (output row, sample), one
+// thread each, weights in LDS).  Measured per 32768-sample minibatch (rocprofv3): 1 tile per
+// workgroup 29.8 us, 2 tiles 25.4 us, 4 tiles 35.0 us (one workgroup per CU); the VALU kernel 42.5 us.
 #ifndef D2D_PPO_FWD_MFMA
 #define D2D_PPO_FWD_MFMA 1
 #endif
-constexpr int FM_SPB = 32, FM_TILES = 1, XS = OBS + 2, HS = HID + 1;  // LDS row strides: bank spread
+constexpr int FM_SPB = 32, FM_TILES = 2, XS = OBS + 2, HS = HID + 1;  // LDS row strides: bank spread
+// h1 or h2 of a 32-sample tile (both nets), LDS -> global as 16-byte row-contiguous stores: 4 per
+// thread instead of 16 dword column stores per lane (the MFMA's C/D layout holds a unit's column),
+// which made the forward store-issue-bound.
+__device__ __forceinline__ void store_tile(const MlpPair& P, int s0, int m, const float (*hs)[FM_SPB][HS], int tid,
+                                           bool second) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int c = q * 256 + tid, n = c >> 9, r = (c >> 4) & 31, k = (c & 15) * 4;
+        if (s0 + r < m) {
+            const float* src = &hs[n][r][k];
+            float* dst = (second ? P.net[n].h2 : P.net[n].h1) + (size_t)(s0 + r) * HID + k;
+            *reinterpret_cast<float4*>(dst) = make_float4(src[0], src[1], src[2], src[3]);
+        }
+    }
+}
 __global__ __launch_bounds__(256) void mlp_forward_mfma_kernel(MlpPair P, int m, const int64_t* __restrict__ idx,
                                                                const float* __restrict__ obs,
                                                                float* __restrict__ xg) {
-    __shared__ float xs[FM_TILES * FM_SPB][XS];
-    __shared__ float hs[2][FM_SPB][HS];  // h1, then h2, of the current 32-sample tile
+    // One LDS region, used first to stage both nets' W1 and W2 (read with coalesced loads: the
+    // register operands below gathered straight from global memory touch 32 cache lines per
+    // instruction, which made the kernel address-bound), then for the inputs and hidden tiles.
+    constexpr int WST1 = HID * OBS, WSTN = WST1 + HID * HS;  // staged floats per net (W2 rows padded)
+    static_assert(FM_TILES * FM_SPB * XS + 2 * FM_SPB * HS <= 2 * WSTN, "LDS union");
+    __shared__ float ubuf[2 * WSTN];
+    float(*xs)[XS] = reinterpret_cast<float(*)[XS]>(ubuf);
+    float(*hs)[FM_SPB][HS] = reinterpret_cast<float(*)[FM_SPB][HS]>(ubuf + FM_TILES * FM_SPB * XS);
     __shared__ int64_t rows[FM_TILES * FM_SPB];
     __shared__ float w3s[4][HID + 1];  // output rows of both nets (od0 + od1 <= 4), bias in column HID
     const int sb = blockIdx.x * FM_TILES * FM_SPB, tid = threadIdx.x, od0 = P.net[0].od;
     const int w = tid >> 6, lane = tid & 63, ci = lane & 31, h = lane >> 5;
     const int net = w >> 1, j0 = (w & 1) * 32;
     const MlpNet& N = P.net[net];
-    // the B operands stay in registers for the whole kernel: lane (ci, h) of wave w holds
-    // W[j0 + ci][2 t + h] for every k step t of both layers (14 + 32 VGPRs)
-    float w1r[(OBS + 1) / 2], w2r[HID / 2];
+    {
+        constexpr int NWE = 2 * WST1 + 2 * HID * HID, NWI = (NWE + 255) / 256;
+        float wv[NWI];
 #pragma unroll
-    for (int t = 0; t < (OBS + 1) / 2; ++t) w1r[t] = 2 * t + h < OBS ? N.w1[(j0 + ci) * OBS + 2 * t + h] : 0.0f;
+        for (int c = 0; c < NWI; ++c) {
+            const int e = c * 256 + tid;
+            if (e < 2 * WST1) {
+                const int n = e >= WST1;
+                wv[c] = P.net[n].w1[e - n * WST1];
+            } else if (e < NWE) {
+                const int f = e - 2 * WST1, n = f >> 12;
+                wv[c] = P.net[n].w2[f & 4095];
+            }
+        }
 #pragma unroll
-    for (int t = 0; t < HID / 2; ++t) w2r[t] = N.w2[(j0 + ci) * HID + 2 * t + h];
-    const float b1 = N.b1[j0 + ci], b2 = N.b2[j0 + ci];
+        for (int c = 0; c < NWI; ++c) {
+            const int e = c * 256 + tid;
+            if (e < 2 * WST1) {
+                const int n = e >= WST1;
+                ubuf[n * WSTN + e - n * WST1] = wv[c];
+            } else if (e < NWE) {
+                const int f = e - 2 * WST1, n = f >> 12, g = f & 4095;
+                ubuf[n * WSTN + WST1 + (g >> 6) * HS + (g & 63)] = wv[c];
+            }
+        }
+    }
     {
         const int orow = tid >> 6, j = tid & 63, on = orow >= od0, r = orow - on * od0;
         if (orow < od0 + P.net[1].od) {
@@ -245,20 +285,28 @@ __global__ __launch_bounds__(256) void mlp_forward_mfma_kernel(MlpPair P, int m,
             if (j == 0) w3s[orow][HID] = P.net[on].b3[r];
         }
     }
+    if (tid < FM_TILES * FM_SPB) rows[tid] = sb + tid < m ? idx[sb + tid] : -1;
+    const float b1 = N.b1[j0 + ci], b2 = N.b2[j0 + ci];
+    __syncthreads();  // weights staged, rows
     constexpr int NX = FM_TILES * FM_SPB * OBS, NI = (NX + 255) / 256;
-    if (tid < FM_TILES * FM_SPB) {
-        rows[tid] = sb + tid < m ? idx[sb + tid] : -1;
-        xs[tid][OBS] = 0.0f;  // the k padding of the 28-deep layer-1 product
-    }
-    __syncthreads();  // rows
-    {
-        float xv[NI];
+    float xv[NI];  // this thread's share of the minibatch's observation rows (gathered early)
 #pragma unroll
-        for (int c = 0; c < NI; ++c) {
-            const int e = c * 256 + tid, sl = e / OBS, k = e % OBS;
-            const int64_t r = e < NX ? rows[sl] : -1;
-            xv[c] = r >= 0 ? obs[r * OBS + k] : 0.0f;
-        }
+    for (int c = 0; c < NI; ++c) {
+        const int e = c * 256 + tid, sl = e / OBS, k = e % OBS;
+        const int64_t r = e < NX ? rows[sl] : -1;
+        xv[c] = r >= 0 ? obs[r * OBS + k] : 0.0f;
+    }
+    // the B operands stay in registers for the whole kernel: lane (ci, h) of wave w holds
+    // W[j0 + ci][2 t + h] for every k step t of both layers (14 + 32 VGPRs)
+    float w1r[(OBS + 1) / 2], w2r[HID / 2];
+#pragma unroll
+    for (int t = 0; t < (OBS + 1) / 2; ++t)
+        w1r[t] = 2 * t + h < OBS ? ubuf[net * WSTN + (j0 + ci) * OBS + 2 * t + h] : 0.0f;
+#pragma unroll
+    for (int t = 0; t < HID / 2; ++t) w2r[t] = ubuf[net * WSTN + WST1 + (j0 + ci) * HS + 2 * t + h];
+    __syncthreads();  // every wave holds its operands: the region becomes xs / hs
+    if (tid < FM_TILES * FM_SPB) xs[tid][OBS] = 0.0f;  // the k padding of the 28-deep layer-1 product
+    {
 #pragma unroll
         for (int c = 0; c < NI; ++c) {
             const int e = c * 256 + tid, sl = e / OBS, k = e % OBS;
@@ -282,9 +330,9 @@ __global__ __launch_bounds__(256) void mlp_forward_mfma_kernel(MlpPair P, int m,
             const int i = (v & 3) + 8 * (v >> 2) + 4 * h;  // sample of register v (C/D map)
             const float y = tanhf(acc[v] + b1);
             hs[net][i][j0 + ci] = y;
-            if (s0 + i < m) N.h1[(size_t)(s0 + i) * HID + j0 + ci] = y;
         }
         __syncthreads();
+        store_tile(P, s0, m, hs, tid, false);
         // layer 2
         acc = f32x16{};
 #pragma unroll
@@ -296,9 +344,9 @@ __global__ __launch_bounds__(256) void mlp_forward_mfma_kernel(MlpPair P, int m,
             const int i = (v & 3) + 8 * (v >> 2) + 4 * h;
             const float y = tanhf(acc[v] + b2);
             hs[net][i][j0 + ci] = y;
-            if (s0 + i < m) N.h2[(size_t)(s0 + i) * HID + j0 + ci] = y;
         }
         __syncthreads();
+        store_tile(P, s0, m, hs, tid, true);
         // output layers: thread t -> (output row t / 32 of both nets' od0 + od1 rows, sample t % 32),
         // weights and biases from LDS
         if (tid < (od0 + P.net[1].od) * FM_SPB) {
