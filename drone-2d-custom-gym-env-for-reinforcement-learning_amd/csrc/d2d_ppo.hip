@@ -31,6 +31,26 @@ __device__ __forceinline__ double block_sum(double x, double* red) {
     return t;
 }
 
+// block_sum of N values at once (one barrier pair); red holds N x (threads / 64) doubles
+template <int N>
+__device__ __forceinline__ void block_sum_n(double (&x)[N], double* red) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+    for (int k = 0; k < N; ++k) x[k] = wave_sum(x[k]);
+    __syncthreads();
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < N; ++k) red[k * nw + w] = x[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        double t = 0.0;
+        for (int j = 0; j < nw; ++j) t += red[k * nw + j];
+        x[k] = t;
+    }
+}
+
 // per-workgroup (sum, sum of squares) of adv[idx[i]] in double: ws[2 b], ws[2 b + 1]
 __global__ __launch_bounds__(D2D_PPO_HEAD_BLOCK) void adv_stats_kernel(int m, const int64_t* __restrict__ idx,
                                                                        const float* __restrict__ adv,
@@ -48,15 +68,13 @@ __global__ __launch_bounds__(D2D_PPO_HEAD_BLOCK) void adv_stats_kernel(int m, co
 __global__ __launch_bounds__(256) void head_finish_kernel(int m, int nb, const float* partial, const float* log_std,
                                                           float ent_coef, float* ls_grad, float* acc_pl,
                                                           float* acc_vl, float* acc_ent, float* acc_clip) {
-    __shared__ double red[4];
-    double s[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+    __shared__ double red[5 * 4];
+    double t[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
     for (int b = threadIdx.x; b < nb; b += blockDim.x) {
 #pragma unroll
-        for (int k = 0; k < 5; ++k) s[k] += partial[(size_t)b * 5 + k];
+        for (int k = 0; k < 5; ++k) t[k] += partial[(size_t)b * 5 + k];
     }
-    double t[5];
-#pragma unroll
-    for (int k = 0; k < 5; ++k) t[k] = block_sum(s[k], red);
+    block_sum_n(t, red);
     if (threadIdx.x == 0) {
         ls_grad[0] = (float)t[3] - ent_coef;
         ls_grad[1] = (float)t[4] - ent_coef;
@@ -373,7 +391,7 @@ __global__ __launch_bounds__(MLP_BLOCK) void mlp_backward_kernel(MlpPair P, int 
                                                                  const double* __restrict__ ws, int nbs,
                                                                  int normalize, float clip, float vf_coef,
                                                                  float* __restrict__ partial) {
-    __shared__ double red[MLP_BLOCK / 64];
+    __shared__ double red[5 * (MLP_BLOCK / 64)];
     __shared__ __attribute__((aligned(16))) float w2s[HID * HID];
     __shared__ float gcol[HID][MLP_SPB];
     const MlpNet& N = P.net[blockIdx.y];
@@ -398,8 +416,10 @@ __global__ __launch_bounds__(MLP_BLOCK) void mlp_backward_kernel(MlpPair P, int 
                 s += ws[2 * b];
                 sq += ws[2 * b + 1];
             }
-            s = block_sum(s, red);
-            sq = block_sum(sq, red);
+            double sv[2] = {s, sq};
+            block_sum_n(sv, red);
+            s = sv[0];
+            sq = sv[1];
             const double mu = s / m, var = (sq - s * mu) / (m > 1 ? m - 1 : 1);
             adv_mean = (float)mu;
             adv_inv = 1.0f / ((float)sqrt(var > 0.0 ? var : 0.0) + 1e-8f);
@@ -433,10 +453,9 @@ __global__ __launch_bounds__(MLP_BLOCK) void mlp_backward_kernel(MlpPair P, int 
             q[1] = (double)err * err;
         }
     }
-    double t[5];
-#pragma unroll
-    for (int k = 0; k < 5; ++k) t[k] = block_sum(q[k], red);
+    block_sum_n(q, red);
     if (threadIdx.x == 0) {
+        const double* t = q;
         float* o = partial + ((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 5;
 #pragma unroll
         for (int k = 0; k < 5; ++k) o[k] = (float)t[k];
