@@ -55,13 +55,14 @@ __device__ __forceinline__ void block_sum_n(double (&x)[N], double* red) {
 __global__ __launch_bounds__(D2D_PPO_HEAD_BLOCK) void adv_stats_kernel(int m, const int64_t* __restrict__ idx,
                                                                        const float* __restrict__ adv,
                                                                        double* __restrict__ ws) {
-    __shared__ double red[D2D_PPO_HEAD_BLOCK / 64];
+    __shared__ double red[2 * (D2D_PPO_HEAD_BLOCK / 64)];
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const double x = i < m ? (double)adv[idx[i]] : 0.0;
-    const double s = block_sum(x, red), q = block_sum(x * x, red);
+    double sq[2] = {x, x * x};
+    block_sum_n(sq, red);
     if (threadIdx.x == 0) {
-        ws[2 * blockIdx.x] = s;
-        ws[2 * blockIdx.x + 1] = q;
+        ws[2 * blockIdx.x] = sq[0];
+        ws[2 * blockIdx.x + 1] = sq[1];
     }
 }
 
@@ -70,7 +71,19 @@ __global__ __launch_bounds__(256) void head_finish_kernel(int m, int nb, const f
                                                           float* acc_vl, float* acc_ent, float* acc_clip) {
     __shared__ double red[5 * 4];
     double t[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
-    for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+    int b = threadIdx.x;
+    for (; b + 3 * 256 < nb; b += 4 * 256) {  // four rows' loads in flight
+        float v[4][5];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int k = 0; k < 5; ++k) v[u][k] = partial[(size_t)(b + u * 256) * 5 + k];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int k = 0; k < 5; ++k) t[k] += v[u][k];
+    }
+    for (; b < nb; b += 256) {
 #pragma unroll
         for (int k = 0; k < 5; ++k) t[k] += partial[(size_t)b * 5 + k];
     }
@@ -403,7 +416,10 @@ __global__ __launch_bounds__(MLP_BLOCK) void mlp_backward_kernel(MlpPair P, int 
 #pragma unroll
         for (int c = 0; c < 4; ++c) reinterpret_cast<float4*>(w2s)[c * MLP_BLOCK + threadIdx.x] = wv[c];
     }
-    const int sl = threadIdx.x / TPS, u0 = (threadIdx.x % TPS) * UNITS;
+    // the sample's TPS threads own interleaved 4-unit groups (thread r: units 4 r + 4 TPS c ..), so a
+    // wave's 16-byte row loads and stores cover 4 TPS contiguous floats per sample, not 4
+    const int sl = threadIdx.x / TPS, r4 = (threadIdx.x % TPS) * 4;
+    auto ub = [r4](int j) { return (j / 4) * 4 * TPS + r4; };  // first unit of this thread's group j / 4
     const int i = blockIdx.x * MLP_SPB + sl;
     const bool live = i < m;
     double q[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
@@ -436,7 +452,7 @@ __global__ __launch_bounds__(MLP_BLOCK) void mlp_backward_kernel(MlpPair P, int 
             const float g_lp = (s1 <= s2) ? a * ratio * (-1.0f / m) : 0.0f;
             go0 = g_lp * z0 * is0;
             go1 = g_lp * z1 * is1;
-            if (u0 == 0) {
+            if (r4 == 0) {
                 N.gout[2 * i] = go0;
                 N.gout[2 * i + 1] = go1;
                 q[0] = fminf(s1, s2);
@@ -448,7 +464,7 @@ __global__ __launch_bounds__(MLP_BLOCK) void mlp_backward_kernel(MlpPair P, int 
     } else if (live) {
         const float err = ret[idx[i]] - N.out[i];
         go0 = err * (-2.0f * vf_coef / m);
-        if (u0 == 0) {
+        if (r4 == 0) {
             N.gout[i] = go0;
             q[1] = (double)err * err;
         }
@@ -462,20 +478,20 @@ __global__ __launch_bounds__(MLP_BLOCK) void mlp_backward_kernel(MlpPair P, int 
     }
     // g2 = (gout W3) * (1 - h2^2): this thread's 32 units, into the sample's LDS column
     if (live) {
-        const float* h2 = N.h2 + (size_t)i * HID + u0;
+        const float* h2 = N.h2 + (size_t)i * HID;
 #pragma unroll
         for (int j = 0; j < UNITS; j += 4) {
-            const float4 hv = *reinterpret_cast<const float4*>(h2 + j);
+            const float4 hv = *reinterpret_cast<const float4*>(h2 + ub(j));
             const float hh[4] = {hv.x, hv.y, hv.z, hv.w};
             float g[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                float d = go0 * N.w3[u0 + j + u];
-                if (N.od == 2) d += go1 * N.w3[HID + u0 + j + u];
+                float d = go0 * N.w3[ub(j) + u];
+                if (N.od == 2) d += go1 * N.w3[HID + ub(j) + u];
                 g[u] = d * (1.0f - hh[u] * hh[u]);
-                gcol[u0 + j + u][sl] = g[u];
+                gcol[ub(j) + u][sl] = g[u];
             }
-            *reinterpret_cast<float4*>(N.g2 + (size_t)i * HID + u0 + j) = make_float4(g[0], g[1], g[2], g[3]);
+            *reinterpret_cast<float4*>(N.g2 + (size_t)i * HID + ub(j)) = make_float4(g[0], g[1], g[2], g[3]);
         }
     }
     __syncthreads();  // W2 staged, both halves of g2 in the column
@@ -487,21 +503,20 @@ __global__ __launch_bounds__(MLP_BLOCK) void mlp_backward_kernel(MlpPair P, int 
 #pragma unroll 1
     for (int j = 0; j < HID; ++j) {
         const float gv = gcol[j][sl];
-        const float4* w = reinterpret_cast<const float4*>(w2s + j * HID + u0);
 #pragma unroll
         for (int k4 = 0; k4 < UNITS / 4; ++k4) {
-            const float4 wv = w[k4];
+            const float4 wv = *reinterpret_cast<const float4*>(w2s + j * HID + ub(4 * k4));
             g1[4 * k4] += gv * wv.x;
             g1[4 * k4 + 1] += gv * wv.y;
             g1[4 * k4 + 2] += gv * wv.z;
             g1[4 * k4 + 3] += gv * wv.w;
         }
     }
-    const float* h1 = N.h1 + (size_t)i * HID + u0;
+    const float* h1 = N.h1 + (size_t)i * HID;
 #pragma unroll
     for (int k = 0; k < UNITS; k += 4) {
-        const float4 hv = *reinterpret_cast<const float4*>(h1 + k);
-        *reinterpret_cast<float4*>(N.g1 + (size_t)i * HID + u0 + k) =
+        const float4 hv = *reinterpret_cast<const float4*>(h1 + ub(k));
+        *reinterpret_cast<float4*>(N.g1 + (size_t)i * HID + ub(k)) =
             make_float4(g1[k] * (1.0f - hv.x * hv.x), g1[k + 1] * (1.0f - hv.y * hv.y),
                         g1[k + 2] * (1.0f - hv.z * hv.z), g1[k + 3] * (1.0f - hv.w * hv.w));
     }
@@ -543,6 +558,65 @@ __global__ __launch_bounds__(ADAM_THREADS) void adam_kernel(int n, float* __rest
     }
     __syncthreads();
     if (threadIdx.x == 0) t[0] = step;
+}
+
+// The same step spread over ceil(n / 1024) workgroups (4 parameters per thread): every workgroup
+// computes the full gradient norm itself (n floats from L2, eight loads in flight per thread, one
+// summation order, so every workgroup gets the same clip coefficient) and updates its slice.  The
+// step counter is read by all of them, so adam_tick_kernel increments it afterwards, and the
+// clipped gradient is not written back (another workgroup may still be reading g for its norm).
+// Off by default: measured 8.1 us + 3.9 us for the one-thread tick launch (a launch costs ~4 us
+// whatever it does) against 10.8 us for the one-workgroup kernel.
+#ifndef D2D_PPO_ADAM_SPREAD
+#define D2D_PPO_ADAM_SPREAD 0
+#endif
+constexpr int ADAM_WG = 256, ADAM_SLICE = 4 * ADAM_WG;
+__global__ __launch_bounds__(ADAM_WG) void adam_spread_kernel(int n, float* __restrict__ p,
+                                                              const float* __restrict__ g, float* __restrict__ m1,
+                                                              float* __restrict__ m2, const float* __restrict__ t,
+                                                              float lr, float b1, float b2, float eps,
+                                                              float max_norm) {
+    __shared__ double red[ADAM_WG / 64];
+    const int base = blockIdx.x * ADAM_SLICE + threadIdx.x;
+    float gs[4], a0[4], v0[4], p0[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {  // this workgroup's slice, loaded before the norm pass
+        const int i = base + k * ADAM_WG;
+        gs[k] = i < n ? g[i] : 0.0f;
+        a0[k] = i < n ? m1[i] : 0.0f;
+        v0[k] = i < n ? m2[i] : 0.0f;
+        p0[k] = i < n ? p[i] : 0.0f;
+    }
+    double q = 0.0;
+    int i = threadIdx.x;
+    for (; i + 7 * ADAM_WG < n; i += 8 * ADAM_WG) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = g[i + u * ADAM_WG];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) q += (double)v[u] * v[u];
+    }
+    for (; i < n; i += ADAM_WG) q += (double)g[i] * g[i];
+    const double norm = sqrt(block_sum(q, red));
+    const float coef = fminf((float)(max_norm / (norm + 1e-6)), 1.0f);
+    const float step = t[0] + 1.0f;
+    const float bc1 = 1.0f - powf(b1, step), bc2s = sqrtf(1.0f - powf(b2, step));
+    const float lr_t = lr / bc1;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int e = base + k * ADAM_WG;
+        if (e < n) {
+            const float gi = gs[k] * coef;
+            const float a = a0[k] + (1.0f - b1) * (gi - a0[k]);  // exp_avg.lerp_(grad, 1 - beta1)
+            const float v = v0[k] * b2 + (1.0f - b2) * gi * gi;
+            m1[e] = a;
+            m2[e] = v;
+            p[e] = p0[k] - a * lr_t / (sqrtf(v) / bc2s + eps);
+        }
+    }
+}
+__global__ void adam_tick_kernel(float* t) {
+    if (threadIdx.x == 0) t[0] += 1.0f;
 }
 
 // ---------------------------------------------------------------------------- weight gradients
@@ -707,8 +781,16 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(int n_chunks, int row
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int e = blockIdx.x * 64 + lane;
     float s = 0.0f;
-    if (e < row_len) {
-        for (int c = w; c < n_chunks; c += 4) s += partial[(size_t)c * row_len + e];
+    if (e < row_len) {  // chunks w, w + 4, ... in order, eight loads in flight at a time
+        int c = w;
+        for (; c + 28 < n_chunks; c += 32) {
+            float v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) v[u] = partial[(size_t)(c + 4 * u) * row_len + e];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) s += v[u];
+        }
+        for (; c < n_chunks; c += 4) s += partial[(size_t)c * row_len + e];
     }
     red[w][lane] = s;
     __syncthreads();
@@ -742,6 +824,12 @@ int32_t d2d_ppo_head_finish(int32_t m, int32_t n_blocks, const float* partial, c
 int32_t d2d_ppo_adam(int32_t n, float* p, float* g, float* m1, float* m2, float* t, float lr, float b1, float b2,
                      float eps, float max_norm, void* stream) {
     if (n <= 0) return 0;
+    if (D2D_PPO_ADAM_SPREAD) {
+        hipLaunchKernelGGL(adam_spread_kernel, dim3((n + ADAM_SLICE - 1) / ADAM_SLICE), dim3(ADAM_WG), 0,
+                           (hipStream_t)stream, n, p, g, m1, m2, t, lr, b1, b2, eps, max_norm);
+        hipLaunchKernelGGL(adam_tick_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, t);
+        return rc(hipGetLastError());
+    }
     if (n > ADAM_THREADS * ADAM_PER_THREAD) return (int32_t)hipErrorInvalidValue;
     hipLaunchKernelGGL(adam_kernel, dim3(1), dim3(ADAM_THREADS), 0, (hipStream_t)stream, n, p, g, m1, m2, t, lr, b1,
                        b2, eps, max_norm);

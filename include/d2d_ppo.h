@@ -36,7 +36,9 @@ int32_t d2d_ppo_head_finish(int32_t m, int32_t n_blocks, const float* partial, c
 
 /* clip_grad_norm_(max_norm) then one torch.optim.Adam step (betas b1, b2, eps; bias corrections
  * from the step counter *t, which is incremented) over n parameters p with gradients g and
- * moments m1, m2.  One workgroup (n is the policy's ~10 k parameters). */
+ * moments m1, m2; g is clipped in place, as torch clips .grad.  One workgroup, n <= 16 384 (the
+ * policy has ~10 k parameters).  Built with D2D_PPO_ADAM_SPREAD=1: ceil(n / 1024) workgroups, each
+ * computing the full norm, then a one-thread launch increments *t, any n, g left unclipped. */
 int32_t d2d_ppo_adam(int32_t n, float* p, float* g, float* m1, float* m2, float* t, float lr, float b1, float b2,
                      float eps, float max_norm, void* stream);
 
