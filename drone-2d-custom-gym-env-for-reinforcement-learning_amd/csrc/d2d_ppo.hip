@@ -268,7 +268,9 @@ __device__ __forceinline__ void store_tile(const MlpPair& P, int s0, int m, cons
 }
 __global__ __launch_bounds__(256) void mlp_forward_mfma_kernel(MlpPair P, int m, const int64_t* __restrict__ idx,
                                                                const float* __restrict__ obs,
-                                                               float* __restrict__ xg) {
+                                                               float* __restrict__ xg,
+                                                               const float* __restrict__ adv,
+                                                               double* __restrict__ ws) {
     // One LDS region, used first to stage both nets' W1 and W2 (read with coalesced loads: the
     // register operands below gathered straight from global memory touch 32 cache lines per
     // instruction, which made the kernel address-bound), then for the inputs and hidden tiles.
@@ -319,6 +321,16 @@ __global__ __launch_bounds__(256) void mlp_forward_mfma_kernel(MlpPair P, int m,
     if (tid < FM_TILES * FM_SPB) rows[tid] = sb + tid < m ? idx[sb + tid] : -1;
     const float b1 = N.b1[j0 + ci], b2 = N.b2[j0 + ci];
     __syncthreads();  // weights staged, rows
+    static_assert(FM_TILES * FM_SPB == D2D_PPO_HEAD_BLOCK, "one advantage partial per workgroup");
+    if (adv != nullptr && tid < 64) {  // d2d_ppo_adv_stats' partials of this workgroup's 64 rows
+        const int64_t r = rows[tid];
+        const double x = r >= 0 ? (double)adv[r] : 0.0;
+        const double s1 = wave_sum(x), s2 = wave_sum(x * x);
+        if (tid == 0) {
+            ws[2 * blockIdx.x] = s1;
+            ws[2 * blockIdx.x + 1] = s2;
+        }
+    }
     constexpr int NX = FM_TILES * FM_SPB * OBS, NI = (NX + 255) / 256;
     float xv[NI];  // this thread's share of the minibatch's observation rows (gathered early)
 #pragma unroll
@@ -872,17 +884,28 @@ static MlpPair make_pair(const float* const* w, float* const* buf) {
     return P;
 }
 
-int32_t d2d_ppo_mlp_forward(int32_t m, const int64_t* idx, const float* obs, const float* const* weights,
-                            float* const* bufs, float* xg, void* stream) {
+int32_t d2d_ppo_mlp_forward_adv(int32_t m, const int64_t* idx, const float* obs, const float* adv,
+                                const float* const* weights, float* const* bufs, float* xg, double* ws, void* stream) {
     if (m <= 0) return 0;
+    if (adv != nullptr && ws == nullptr) return (int32_t)hipErrorInvalidValue;
     MlpPair P = make_pair(weights, bufs);
-    if (D2D_PPO_FWD_MFMA)
+    if (D2D_PPO_FWD_MFMA) {
         hipLaunchKernelGGL(mlp_forward_mfma_kernel, dim3((m + FM_TILES * FM_SPB - 1) / (FM_TILES * FM_SPB)), dim3(256), 0,
-                           (hipStream_t)stream, P, m, idx, obs, xg);
-    else
+                           (hipStream_t)stream, P, m, idx, obs, xg, adv, ws);
+    } else {
+        if (adv != nullptr) {
+            const int32_t e = d2d_ppo_adv_stats(m, idx, adv, ws, stream);
+            if (e != 0) return e;
+        }
         hipLaunchKernelGGL(mlp_forward_kernel, dim3((m + MLP_SPB - 1) / MLP_SPB, 2), dim3(MLP_BLOCK), 0,
                            (hipStream_t)stream, P, m, idx, obs, xg);
+    }
     return rc(hipGetLastError());
+}
+
+int32_t d2d_ppo_mlp_forward(int32_t m, const int64_t* idx, const float* obs, const float* const* weights,
+                            float* const* bufs, float* xg, void* stream) {
+    return d2d_ppo_mlp_forward_adv(m, idx, obs, nullptr, weights, bufs, xg, nullptr, stream);
 }
 
 int32_t d2d_ppo_mlp_partial_rows(int32_t m) { return 2 * ((m + MLP_SPB - 1) / MLP_SPB); }

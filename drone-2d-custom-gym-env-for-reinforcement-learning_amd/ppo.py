@@ -145,13 +145,14 @@ def ppo_native():
             "d2d_ppo_wgrad": [i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp, vp, vp],
             "d2d_ppo_wgrad_chunks": [i32],
             "d2d_ppo_mlp_forward": [i32, vp, vp, vp, vp, vp, vp],
+            "d2d_ppo_mlp_forward_adv": [i32, vp, vp, vp, vp, vp, vp, vp, vp],
             "d2d_ppo_mlp_backward": [i32, vp, vp, vp, vp, vp, vp, vp, i32, f32, f32, vp, vp, vp, vp, vp],
             "d2d_ppo_mlp_partial_rows": [i32],
         }
         for name, args in sig.items():
             fn = getattr(lib, name)
             fn.restype, fn.argtypes = C.c_int32, args
-        if lib.d2d_ppo_abi_version() != 1:
+        if lib.d2d_ppo_abi_version() != 2:
             raise RuntimeError("libd2d_ppo.so ABI mismatch")
         _PPO_LIB = lib
     return _PPO_LIB
@@ -257,7 +258,7 @@ class ManualStep:
         cfg, pol, lib, st = self.cfg, self.pol, self.lib, self._stream()
         obs_all, act_all, ol_all, adv_all, ret_all = rollout
         M, dev = idx.numel(), self.P.device
-        nb = (M + 255) // 256
+        nb = (M + 63) // 64  # D2D_PPO_HEAD_BLOCK rows per advantage partial
         if M not in self._bufs:
             # one set of work buffers per minibatch size, kept for the handle's life: a captured graph
             # holds the full-size set's addresses while a ragged last minibatch runs eagerly on its own
@@ -279,10 +280,10 @@ class ManualStep:
                                                               "h1v", "h2v", "val", "g1v", "g2v")])
         gptr = (C.c_void_p * 2)(hb["gm"].data_ptr(), hb["gv"].data_ptr())
         norm = int(cfg.normalize_advantage and M > 1)
-        if norm:
-            _ok(lib.d2d_ppo_adv_stats(M, idx.data_ptr(), adv_all.data_ptr(), hb["ws"].data_ptr(), st), "adv_stats")
-        _ok(lib.d2d_ppo_mlp_forward(M, idx.data_ptr(), obs_all.data_ptr(), wptr, bptr, hb["xg"].data_ptr(), st),
-            "d2d_ppo_mlp_forward")
+        # the forward launch also writes the advantage statistics' partials when they are needed
+        _ok(lib.d2d_ppo_mlp_forward_adv(M, idx.data_ptr(), obs_all.data_ptr(), adv_all.data_ptr() if norm else None,
+                                        wptr, bptr, hb["xg"].data_ptr(), hb["ws"].data_ptr(), st),
+            "d2d_ppo_mlp_forward_adv")
         _ok(lib.d2d_ppo_mlp_backward(M, idx.data_ptr(), act_all.data_ptr(), ol_all.data_ptr(), adv_all.data_ptr(),
                                      ret_all.data_ptr(), pol.log_std.data_ptr(), hb["ws"].data_ptr(), norm,
                                      cfg.clip_range, cfg.vf_coef, wptr, bptr, gptr, hb["partial"].data_ptr(), st),

@@ -17,8 +17,8 @@
 extern "C" {
 #endif
 
-#define D2D_PPO_ABI_VERSION 1
-#define D2D_PPO_HEAD_BLOCK 256
+#define D2D_PPO_ABI_VERSION 2
+#define D2D_PPO_HEAD_BLOCK 64  /* v1: 256 */
 
 int32_t d2d_ppo_abi_version(void);
 
@@ -67,6 +67,10 @@ int32_t d2d_ppo_wgrad_chunks(int32_t m);
  * squared value error scaled by vf_coef. */
 int32_t d2d_ppo_mlp_forward(int32_t m, const int64_t* idx, const float* obs, const float* const* weights,
                             float* const* bufs, float* xg, void* stream);
+/* mlp_forward plus d2d_ppo_adv_stats' partials into ws from the same launch (adv != NULL; the
+ * matrix-core forward's workgroups each take D2D_PPO_HEAD_BLOCK rows).  Added in ABI v2. */
+int32_t d2d_ppo_mlp_forward_adv(int32_t m, const int64_t* idx, const float* obs, const float* adv,
+                                const float* const* weights, float* const* bufs, float* xg, double* ws, void* stream);
 int32_t d2d_ppo_mlp_partial_rows(int32_t m);
 int32_t d2d_ppo_mlp_backward(int32_t m, const int64_t* idx, const float* act, const float* old_logp, const float* adv,
                              const float* ret, const float* log_std, const double* ws, int32_t normalize, float clip,
