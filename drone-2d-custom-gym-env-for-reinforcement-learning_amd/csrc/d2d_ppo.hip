@@ -66,10 +66,20 @@ __global__ __launch_bounds__(D2D_PPO_HEAD_BLOCK) void adv_stats_kernel(int m, co
     }
 }
 
-__global__ __launch_bounds__(256) void head_finish_kernel(int m, int nb, const float* partial, const float* log_std,
-                                                          float ent_coef, float* ls_grad, float* acc_pl,
-                                                          float* acc_vl, float* acc_ent, float* acc_clip) {
+// the head's partial rows finished by one 256-thread workgroup (head_finish_kernel, or the last
+// workgroup of wgrad_reduce_kernel)
+struct HeadArgs {
+    int m, nb;
+    const float* partial;  // nullptr: no head work
+    const float* log_std;
+    float ent_coef;
+    float* ls_grad;
+    float *acc_pl, *acc_vl, *acc_ent, *acc_clip;
+};
+__device__ __forceinline__ void head_finish_body(const HeadArgs& H) {
     __shared__ double red[5 * 4];
+    const int m = H.m, nb = H.nb;
+    const float* partial = H.partial;
     double t[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
     int b = threadIdx.x;
     for (; b + 3 * 256 < nb; b += 4 * 256) {  // four rows' loads in flight
@@ -89,14 +99,15 @@ __global__ __launch_bounds__(256) void head_finish_kernel(int m, int nb, const f
     }
     block_sum_n(t, red);
     if (threadIdx.x == 0) {
-        ls_grad[0] = (float)t[3] - ent_coef;
-        ls_grad[1] = (float)t[4] - ent_coef;
-        *acc_pl += (float)(-t[0] / m);
-        *acc_vl += (float)(t[1] / m);
-        *acc_clip += (float)(t[2] / m);
-        *acc_ent += (0.5f + HALF_LOG_2PI + log_std[0]) + (0.5f + HALF_LOG_2PI + log_std[1]);
+        H.ls_grad[0] = (float)t[3] - H.ent_coef;
+        H.ls_grad[1] = (float)t[4] - H.ent_coef;
+        *H.acc_pl += (float)(-t[0] / m);
+        *H.acc_vl += (float)(t[1] / m);
+        *H.acc_clip += (float)(t[2] / m);
+        *H.acc_ent += (0.5f + HALF_LOG_2PI + H.log_std[0]) + (0.5f + HALF_LOG_2PI + H.log_std[1]);
     }
 }
+__global__ __launch_bounds__(256) void head_finish_kernel(HeadArgs H) { head_finish_body(H); }
 
 // ------------------------------------------------------------------ per-sample MLP passes
 // blockIdx.y = 0: the policy net (27-64-64 tanh -> 2), 1: the value net (-> 1); the activations are
@@ -788,7 +799,14 @@ __global__ __launch_bounds__(256) void wgrad_mfma_kernel(WgradProblems P, int m,
 // g[e] = sum over the n_chunks rows of partial[.][e], e < row_len: 64 elements per workgroup, the
 // chunks split over the workgroup's four waves
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(int n_chunks, int row_len, const float* __restrict__ partial,
-                                                           float* __restrict__ g) {
+                                                           float* __restrict__ g, HeadArgs H) {
+    // with H.partial set, the last workgroup finishes the loss head (head_finish_kernel's work) and
+    // writes log_std's two gradient slots, which the reduce then leaves alone
+    if (H.partial != nullptr && blockIdx.x == gridDim.x - 1) {
+        head_finish_body(H);
+        return;
+    }
+    const long ls_off = H.partial != nullptr ? (long)(H.ls_grad - g) : -8;
     __shared__ float red[4][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int e = blockIdx.x * 64 + lane;
@@ -806,7 +824,8 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(int n_chunks, int row
     }
     red[w][lane] = s;
     __syncthreads();
-    if (w == 0 && e < row_len) g[e] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    if (w == 0 && e < row_len && (e < ls_off || e >= ls_off + 2))
+        g[e] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
 }
 
 inline int32_t rc(hipError_t e) { return e == hipSuccess ? 0 : (int32_t)e; }
@@ -828,8 +847,8 @@ int32_t d2d_ppo_head_finish(int32_t m, int32_t n_blocks, const float* partial, c
                             float* log_std_grad, float* acc_pl, float* acc_vl, float* acc_ent, float* acc_clip,
                             void* stream) {
     if (m <= 0) return 0;
-    hipLaunchKernelGGL(head_finish_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, m, n_blocks, partial, log_std,
-                       ent_coef, log_std_grad, acc_pl, acc_vl, acc_ent, acc_clip);
+    const HeadArgs H{m, n_blocks, partial, log_std, ent_coef, log_std_grad, acc_pl, acc_vl, acc_ent, acc_clip};
+    hipLaunchKernelGGL(head_finish_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, H);
     return rc(hipGetLastError());
 }
 
@@ -848,9 +867,10 @@ int32_t d2d_ppo_adam(int32_t n, float* p, float* g, float* m1, float* m2, float*
     return rc(hipGetLastError());
 }
 
-int32_t d2d_ppo_wgrad(int32_t m, int32_t n_problems, const float* const* a, const int32_t* lda, const float* const* b,
-                      const int32_t* ldb, const int32_t* p, const int32_t* q, const int32_t* w_off,
-                      const int32_t* b_off, int32_t row_len, float* partial, float* g, void* stream) {
+static int32_t wgrad_launch(int32_t m, int32_t n_problems, const float* const* a, const int32_t* lda,
+                            const float* const* b, const int32_t* ldb, const int32_t* p, const int32_t* q,
+                            const int32_t* w_off, const int32_t* b_off, int32_t row_len, float* partial, float* g,
+                            const HeadArgs& H, void* stream) {
     if (m <= 0 || n_problems <= 0) return 0;
     if (n_problems > D2D_PPO_WGRAD_MAX) return (int32_t)hipErrorInvalidValue;
     WgradProblems P{};
@@ -867,9 +887,27 @@ int32_t d2d_ppo_wgrad(int32_t m, int32_t n_problems, const float* const* a, cons
                            partial);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return (int32_t)e;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((row_len + 63) / 64), dim3(256), 0, (hipStream_t)stream, nc,
-                       row_len, partial, g);
+    if (H.partial != nullptr && (H.ls_grad < g || H.ls_grad + 2 > g + row_len)) return (int32_t)hipErrorInvalidValue;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((row_len + 63) / 64 + (H.partial != nullptr)), dim3(256), 0,
+                       (hipStream_t)stream, nc, row_len, partial, g, H);
     return rc(hipGetLastError());
+}
+
+int32_t d2d_ppo_wgrad(int32_t m, int32_t n_problems, const float* const* a, const int32_t* lda, const float* const* b,
+                      const int32_t* ldb, const int32_t* p, const int32_t* q, const int32_t* w_off,
+                      const int32_t* b_off, int32_t row_len, float* partial, float* g, void* stream) {
+    return wgrad_launch(m, n_problems, a, lda, b, ldb, p, q, w_off, b_off, row_len, partial, g, HeadArgs{}, stream);
+}
+
+int32_t d2d_ppo_wgrad_head(int32_t m, int32_t n_problems, const float* const* a, const int32_t* lda,
+                           const float* const* b, const int32_t* ldb, const int32_t* p, const int32_t* q,
+                           const int32_t* w_off, const int32_t* b_off, int32_t row_len, float* partial, float* g,
+                           int32_t n_blocks, const float* head_partial, const float* log_std, float ent_coef,
+                           float* log_std_grad, float* acc_pl, float* acc_vl, float* acc_ent, float* acc_clip,
+                           void* stream) {
+    if (head_partial == nullptr) return (int32_t)hipErrorInvalidValue;
+    const HeadArgs H{m, n_blocks, head_partial, log_std, ent_coef, log_std_grad, acc_pl, acc_vl, acc_ent, acc_clip};
+    return wgrad_launch(m, n_problems, a, lda, b, ldb, p, q, w_off, b_off, row_len, partial, g, H, stream);
 }
 
 int32_t d2d_ppo_wgrad_chunks(int32_t m) { return (m + WG_ROWS - 1) / WG_ROWS; }

@@ -143,6 +143,8 @@ def ppo_native():
             "d2d_ppo_head_finish": [i32, i32, vp, vp, f32, vp, vp, vp, vp, vp, vp],
             "d2d_ppo_adam": [i32, vp, vp, vp, vp, vp, f32, f32, f32, f32, f32, vp],
             "d2d_ppo_wgrad": [i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp, vp, vp],
+            "d2d_ppo_wgrad_head": [i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp, vp,
+                                   i32, vp, vp, f32, vp, vp, vp, vp, vp, vp],
             "d2d_ppo_wgrad_chunks": [i32],
             "d2d_ppo_mlp_forward": [i32, vp, vp, vp, vp, vp, vp],
             "d2d_ppo_mlp_forward_adv": [i32, vp, vp, vp, vp, vp, vp, vp, vp],
@@ -291,19 +293,20 @@ class ManualStep:
         layers = ((hb["gm"], hb["h2p"], pol.action_net), (hb["gv"], hb["h2v"], pol.value_net),
                   (hb["g2p"], hb["h1p"], pn[2]), (hb["g2v"], hb["h1v"], vn[2]), (hb["g1p"], hb["xg"], pn[0]),
                   (hb["g1v"], hb["xg"], vn[0]))
-        self._wgrad_hip(M, layers, hb["wpart"])
         ls = pol.log_std
-        _ok(lib.d2d_ppo_head_finish(M, prow, hb["partial"].data_ptr(), ls.data_ptr(), cfg.ent_coef,
-                                    ls.grad.data_ptr(), acc["policy_loss"].data_ptr(), acc["value_loss"].data_ptr(),
-                                    acc["entropy"].data_ptr(), acc["clip_fraction"].data_ptr(), st),
-            "d2d_ppo_head_finish")
+        # the head's finish (log-std gradient, loss statistics) rides on the gradient reduce's launch
+        head = (prow, hb["partial"].data_ptr(), ls.data_ptr(), cfg.ent_coef, ls.grad.data_ptr(),
+                acc["policy_loss"].data_ptr(), acc["value_loss"].data_ptr(), acc["entropy"].data_ptr(),
+                acc["clip_fraction"].data_ptr())
+        self._wgrad_hip(M, layers, hb["wpart"], head)
 
     @staticmethod
     def _tanh_grad_torch(h, g):
         return g.mul_(1.0 - h * h)
 
-    def _wgrad_hip(self, M, layers, wpart):
-        """All six weight / bias gradients in one libd2d_ppo.so launch (+ its reduce) into G."""
+    def _wgrad_hip(self, M, layers, wpart, head=None):
+        """All six weight / bias gradients in one libd2d_ppo.so launch (+ its reduce) into G; with
+        `head` (d2d_ppo_head_finish's arguments after m) the reduce launch also finishes the head."""
         import ctypes as C
 
         row_len = self.G.numel()  # all of G: log_std's slots (no problem covers them) are rewritten after
@@ -321,8 +324,12 @@ class ManualStep:
         bo = arr(C.c_int32, [(lin.bias.grad.data_ptr() - base) // 4 for _, _, lin in layers])
         for a, b, _ in layers:
             assert a.stride(1) == 1 and b.stride(1) == 1 and a.shape[0] == b.shape[0] == M
-        _ok(self.lib.d2d_ppo_wgrad(M, n, a_p, lda, b_p, ldb, pp, qq, wo, bo, row_len, wpart.data_ptr(), base,
-                                   self._stream()), "d2d_ppo_wgrad")
+        if head is None:
+            _ok(self.lib.d2d_ppo_wgrad(M, n, a_p, lda, b_p, ldb, pp, qq, wo, bo, row_len, wpart.data_ptr(), base,
+                                       self._stream()), "d2d_ppo_wgrad")
+        else:
+            _ok(self.lib.d2d_ppo_wgrad_head(M, n, a_p, lda, b_p, ldb, pp, qq, wo, bo, row_len, wpart.data_ptr(), base,
+                                            *head, self._stream()), "d2d_ppo_wgrad_head")
 
     def _stream(self):
         return torch.cuda.current_stream(self.P.device).cuda_stream

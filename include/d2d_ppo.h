@@ -52,6 +52,15 @@ int32_t d2d_ppo_adam(int32_t n, float* p, float* g, float* m1, float* m2, float*
 int32_t d2d_ppo_wgrad(int32_t m, int32_t n_problems, const float* const* a, const int32_t* lda, const float* const* b,
                       const int32_t* ldb, const int32_t* p, const int32_t* q, const int32_t* w_off,
                       const int32_t* b_off, int32_t row_len, float* partial, float* g, void* stream);
+/* d2d_ppo_wgrad and d2d_ppo_head_finish in two launches instead of three (the reduce's last
+ * workgroup finishes the head; log_std_grad must point at two slots inside g[0 .. row_len), which
+ * the reduce leaves to the head).  Added in ABI v2. */
+int32_t d2d_ppo_wgrad_head(int32_t m, int32_t n_problems, const float* const* a, const int32_t* lda,
+                           const float* const* b, const int32_t* ldb, const int32_t* p, const int32_t* q,
+                           const int32_t* w_off, const int32_t* b_off, int32_t row_len, float* partial, float* g,
+                           int32_t n_blocks, const float* head_partial, const float* log_std, float ent_coef,
+                           float* log_std_grad, float* acc_pl, float* acc_vl, float* acc_ent, float* acc_clip,
+                           void* stream);
 int32_t d2d_ppo_wgrad_chunks(int32_t m);
 
 /* The two MLPs (policy 27-64-64-2, value 27-64-64-1, tanh) per minibatch sample, four threads per
