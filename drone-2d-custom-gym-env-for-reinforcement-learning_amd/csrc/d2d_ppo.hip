@@ -583,6 +583,68 @@ __global__ __launch_bounds__(ADAM_THREADS) void adam_kernel(int n, float* __rest
     if (threadIdx.x == 0) t[0] = step;
 }
 
+// adam_kernel's step run by one 256-thread workgroup (the gradient reduce's last one to finish):
+// thread t stands in for adam_kernel's threads t + 256 j (j < 4), with the same per-thread and
+// per-wave summation order of the norm, so the result is bit-identical to adam_kernel's.
+struct AdamArgs {
+    int n;
+    float *p, *m1, *m2, *t;  // p == nullptr: no Adam step in the reduce launch
+    float lr, b1, b2, eps, max_norm;
+    int* ticket;  // workgroups done; the last one resets it to 0
+};
+constexpr int ADAM_VT = ADAM_THREADS / 256;  // virtual adam_kernel threads per thread
+__device__ __forceinline__ void adam_body_256(const AdamArgs& A, float* __restrict__ g) {
+    __shared__ double red[ADAM_THREADS / 64];
+    const int n = A.n, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    float gv[ADAM_VT][ADAM_PER_THREAD];
+    double q[ADAM_VT];
+#pragma unroll
+    for (int j = 0; j < ADAM_VT; ++j) {
+        q[j] = 0.0;
+#pragma unroll
+        for (int k = 0; k < ADAM_PER_THREAD; ++k) {
+            const int i = threadIdx.x + 256 * j + k * ADAM_THREADS;
+            gv[j][k] = i < n ? g[i] : 0.0f;
+        }
+#pragma unroll
+        for (int k = 0; k < ADAM_PER_THREAD; ++k) q[j] += (double)gv[j][k] * gv[j][k];
+    }
+#pragma unroll
+    for (int j = 0; j < ADAM_VT; ++j) q[j] = wave_sum(q[j]);
+    if (lane == 0) {
+#pragma unroll
+        for (int j = 0; j < ADAM_VT; ++j) red[w + 4 * j] = q[j];  // adam_kernel's wave w + 4 j
+    }
+    __syncthreads();
+    double tot = 0.0;
+    for (int k = 0; k < ADAM_THREADS / 64; ++k) tot += red[k];
+    const double norm = sqrt(tot);
+    const float coef = fminf((float)(A.max_norm / (norm + 1e-6)), 1.0f);
+    const float step = A.t[0] + 1.0f;
+    const float b1 = A.b1, b2 = A.b2;
+    const float bc1 = 1.0f - powf(b1, step), bc2s = sqrtf(1.0f - powf(b2, step));
+    const float lr_t = A.lr / bc1;
+#pragma unroll
+    for (int j = 0; j < ADAM_VT; ++j) {
+#pragma unroll
+        for (int k = 0; k < ADAM_PER_THREAD; ++k) {
+            const int i = threadIdx.x + 256 * j + k * ADAM_THREADS;
+            if (i < n) {
+                const float gi = gv[j][k] * coef;
+                g[i] = gi;
+                const float a0 = A.m1[i], v0 = A.m2[i];
+                const float a = a0 + (1.0f - b1) * (gi - a0);
+                const float v = v0 * b2 + (1.0f - b2) * gi * gi;
+                A.m1[i] = a;
+                A.m2[i] = v;
+                A.p[i] -= a * lr_t / (sqrtf(v) / bc2s + A.eps);
+            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) A.t[0] = step;
+}
+
 // The same step spread over ceil(n / 1024) workgroups (4 parameters per thread): every workgroup
 // computes the full gradient norm itself (n floats from L2, eight loads in flight per thread, one
 // summation order, so every workgroup gets the same clip coefficient) and updates its slice.  The
@@ -798,14 +860,8 @@ __global__ __launch_bounds__(256) void wgrad_mfma_kernel(WgradProblems P, int m,
 
 // g[e] = sum over the n_chunks rows of partial[.][e], e < row_len: 64 elements per workgroup, the
 // chunks split over the workgroup's four waves
-__global__ __launch_bounds__(256) void wgrad_reduce_kernel(int n_chunks, int row_len, const float* __restrict__ partial,
-                                                           float* __restrict__ g, HeadArgs H) {
-    // with H.partial set, the last workgroup finishes the loss head (head_finish_kernel's work) and
-    // writes log_std's two gradient slots, which the reduce then leaves alone
-    if (H.partial != nullptr && blockIdx.x == gridDim.x - 1) {
-        head_finish_body(H);
-        return;
-    }
+__device__ __forceinline__ void wgrad_reduce_body(int n_chunks, int row_len, const float* __restrict__ partial,
+                                                  float* __restrict__ g, const HeadArgs& H) {
     const long ls_off = H.partial != nullptr ? (long)(H.ls_grad - g) : -8;
     __shared__ float red[4][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -826,6 +882,29 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(int n_chunks, int row
     __syncthreads();
     if (w == 0 && e < row_len && (e < ls_off || e >= ls_off + 2))
         g[e] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+}
+
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(int n_chunks, int row_len, const float* __restrict__ partial,
+                                                           float* __restrict__ g, HeadArgs H, AdamArgs A) {
+    // with H.partial set, the last workgroup finishes the loss head (head_finish_kernel's work) and
+    // writes log_std's two gradient slots, which the reduce then leaves alone
+    if (H.partial != nullptr && blockIdx.x == gridDim.x - 1) {
+        head_finish_body(H);
+    } else {
+        wgrad_reduce_body(n_chunks, row_len, partial, g, H);
+    }
+    if (A.p == nullptr) return;
+    // with A.p set, the workgroup that finishes last runs the clip + Adam step on the whole of g
+    __shared__ int last;
+    __syncthreads();
+    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // the workgroup's g writes
+    if (threadIdx.x == 0)
+        last = __hip_atomic_fetch_add(A.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
+    __syncthreads();
+    if (!last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every other workgroup's g writes
+    adam_body_256(A, g);
+    if (threadIdx.x == 0) __hip_atomic_store(A.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 inline int32_t rc(hipError_t e) { return e == hipSuccess ? 0 : (int32_t)e; }
@@ -870,7 +949,7 @@ int32_t d2d_ppo_adam(int32_t n, float* p, float* g, float* m1, float* m2, float*
 static int32_t wgrad_launch(int32_t m, int32_t n_problems, const float* const* a, const int32_t* lda,
                             const float* const* b, const int32_t* ldb, const int32_t* p, const int32_t* q,
                             const int32_t* w_off, const int32_t* b_off, int32_t row_len, float* partial, float* g,
-                            const HeadArgs& H, void* stream) {
+                            const HeadArgs& H, const AdamArgs& A, void* stream) {
     if (m <= 0 || n_problems <= 0) return 0;
     if (n_problems > D2D_PPO_WGRAD_MAX) return (int32_t)hipErrorInvalidValue;
     WgradProblems P{};
@@ -888,15 +967,18 @@ static int32_t wgrad_launch(int32_t m, int32_t n_problems, const float* const* a
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return (int32_t)e;
     if (H.partial != nullptr && (H.ls_grad < g || H.ls_grad + 2 > g + row_len)) return (int32_t)hipErrorInvalidValue;
+    if (A.p != nullptr && (A.n != row_len || A.ticket == nullptr || A.n > ADAM_THREADS * ADAM_PER_THREAD))
+        return (int32_t)hipErrorInvalidValue;
     hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((row_len + 63) / 64 + (H.partial != nullptr)), dim3(256), 0,
-                       (hipStream_t)stream, nc, row_len, partial, g, H);
+                       (hipStream_t)stream, nc, row_len, partial, g, H, A);
     return rc(hipGetLastError());
 }
 
 int32_t d2d_ppo_wgrad(int32_t m, int32_t n_problems, const float* const* a, const int32_t* lda, const float* const* b,
                       const int32_t* ldb, const int32_t* p, const int32_t* q, const int32_t* w_off,
                       const int32_t* b_off, int32_t row_len, float* partial, float* g, void* stream) {
-    return wgrad_launch(m, n_problems, a, lda, b, ldb, p, q, w_off, b_off, row_len, partial, g, HeadArgs{}, stream);
+    return wgrad_launch(m, n_problems, a, lda, b, ldb, p, q, w_off, b_off, row_len, partial, g, HeadArgs{}, AdamArgs{},
+                        stream);
 }
 
 int32_t d2d_ppo_wgrad_head(int32_t m, int32_t n_problems, const float* const* a, const int32_t* lda,
@@ -907,7 +989,22 @@ int32_t d2d_ppo_wgrad_head(int32_t m, int32_t n_problems, const float* const* a,
                            void* stream) {
     if (head_partial == nullptr) return (int32_t)hipErrorInvalidValue;
     const HeadArgs H{m, n_blocks, head_partial, log_std, ent_coef, log_std_grad, acc_pl, acc_vl, acc_ent, acc_clip};
-    return wgrad_launch(m, n_problems, a, lda, b, ldb, p, q, w_off, b_off, row_len, partial, g, H, stream);
+    return wgrad_launch(m, n_problems, a, lda, b, ldb, p, q, w_off, b_off, row_len, partial, g, H, AdamArgs{}, stream);
+}
+
+int32_t d2d_ppo_wgrad_head_adam(int32_t m, int32_t n_problems, const float* const* a, const int32_t* lda,
+                                const float* const* b, const int32_t* ldb, const int32_t* p, const int32_t* q,
+                                const int32_t* w_off, const int32_t* b_off, int32_t row_len, float* partial, float* g,
+                                int32_t n_blocks, const float* head_partial, const float* log_std, float ent_coef,
+                                float* log_std_grad, float* acc_pl, float* acc_vl, float* acc_ent, float* acc_clip,
+                                float* params, float* m1, float* m2, float* t, float lr, float b1, float b2, float eps,
+                                float max_norm, int32_t* ticket, void* stream) {
+    if (head_partial == nullptr || params == nullptr || m1 == nullptr || m2 == nullptr || t == nullptr ||
+        ticket == nullptr)
+        return (int32_t)hipErrorInvalidValue;
+    const HeadArgs H{m, n_blocks, head_partial, log_std, ent_coef, log_std_grad, acc_pl, acc_vl, acc_ent, acc_clip};
+    const AdamArgs A{row_len, params, m1, m2, t, lr, b1, b2, eps, max_norm, ticket};
+    return wgrad_launch(m, n_problems, a, lda, b, ldb, p, q, w_off, b_off, row_len, partial, g, H, A, stream);
 }
 
 int32_t d2d_ppo_wgrad_chunks(int32_t m) { return (m + WG_ROWS - 1) / WG_ROWS; }

@@ -145,6 +145,9 @@ def ppo_native():
             "d2d_ppo_wgrad": [i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp, vp, vp],
             "d2d_ppo_wgrad_head": [i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp, vp,
                                    i32, vp, vp, f32, vp, vp, vp, vp, vp, vp],
+            "d2d_ppo_wgrad_head_adam": [i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp, vp,
+                                        i32, vp, vp, f32, vp, vp, vp, vp, vp,
+                                        vp, vp, vp, vp, f32, f32, f32, f32, f32, vp, vp],
             "d2d_ppo_wgrad_chunks": [i32],
             "d2d_ppo_mlp_forward": [i32, vp, vp, vp, vp, vp, vp],
             "d2d_ppo_mlp_forward_adv": [i32, vp, vp, vp, vp, vp, vp, vp, vp],
@@ -154,7 +157,7 @@ def ppo_native():
         for name, args in sig.items():
             fn = getattr(lib, name)
             fn.restype, fn.argtypes = C.c_int32, args
-        if lib.d2d_ppo_abi_version() != 2:
+        if lib.d2d_ppo_abi_version() != 3:
             raise RuntimeError("libd2d_ppo.so ABI mismatch")
         _PPO_LIB = lib
     return _PPO_LIB
@@ -207,6 +210,13 @@ class ManualStep:
         # the fused element-wise kernels on a GPU (libd2d_ppo.so, loud if missing); torch ops on CPU
         self.lib = ppo_native() if torch.device(device).type == "cuda" else None
         self._bufs = {}  # minibatch size -> (work buffers, partial rows) of the HIP path
+        # D2D_PPO_FUSE_ADAM=1 (single rank): Adam runs as the gradient reduce's last workgroup
+        # (d2d_ppo_wgrad_head_adam) instead of its own d2d_ppo_adam launch; bit-identical results, off
+        # by default (slower as measured, see DESIGN.md "PPO update")
+        import os
+
+        self.fuse_adam = self.lib is not None and os.environ.get("D2D_PPO_FUSE_ADAM", "0") == "1"
+        self._ticket = torch.zeros(1, dtype=torch.int32, device=device) if self.lib is not None else None
         o = 0
         for p in params:
             k = p.numel()
@@ -216,6 +226,9 @@ class ManualStep:
             o += k
 
     def step(self, idx, rollout, acc: dict, world: int = 1):
+        if self.fuse_adam and world == 1:
+            self._grad_hip(idx, rollout, acc, adam=True)  # gradient + clip + Adam, no exchange between
+            return
         self.grad(idx, rollout, acc)
         self.apply(world)
 
@@ -252,7 +265,7 @@ class ManualStep:
             _wgrad(a, b, lin.weight.grad)
             torch.sum(a, 0, out=lin.bias.grad)
 
-    def _grad_hip(self, idx, rollout, acc):
+    def _grad_hip(self, idx, rollout, acc, adam: bool = False):
         """libd2d_ppo.so: advantage statistics, both MLPs forward (four threads per sample and net),
         loss head + backward to the hidden-layer gradients, all weight / bias gradients, log_std's."""
         import ctypes as C
@@ -298,15 +311,16 @@ class ManualStep:
         head = (prow, hb["partial"].data_ptr(), ls.data_ptr(), cfg.ent_coef, ls.grad.data_ptr(),
                 acc["policy_loss"].data_ptr(), acc["value_loss"].data_ptr(), acc["entropy"].data_ptr(),
                 acc["clip_fraction"].data_ptr())
-        self._wgrad_hip(M, layers, hb["wpart"], head)
+        self._wgrad_hip(M, layers, hb["wpart"], head, adam)
 
     @staticmethod
     def _tanh_grad_torch(h, g):
         return g.mul_(1.0 - h * h)
 
-    def _wgrad_hip(self, M, layers, wpart, head=None):
+    def _wgrad_hip(self, M, layers, wpart, head=None, adam: bool = False):
         """All six weight / bias gradients in one libd2d_ppo.so launch (+ its reduce) into G; with
-        `head` (d2d_ppo_head_finish's arguments after m) the reduce launch also finishes the head."""
+        `head` (d2d_ppo_head_finish's arguments after m) the reduce launch also finishes the head, and
+        with `adam` its last workgroup also runs apply()'s clip + Adam step (single rank)."""
         import ctypes as C
 
         row_len = self.G.numel()  # all of G: log_std's slots (no problem covers them) are rewritten after
@@ -327,6 +341,13 @@ class ManualStep:
         if head is None:
             _ok(self.lib.d2d_ppo_wgrad(M, n, a_p, lda, b_p, ldb, pp, qq, wo, bo, row_len, wpart.data_ptr(), base,
                                        self._stream()), "d2d_ppo_wgrad")
+        elif adam:
+            cfg = self.cfg
+            _ok(self.lib.d2d_ppo_wgrad_head_adam(M, n, a_p, lda, b_p, ldb, pp, qq, wo, bo, row_len, wpart.data_ptr(),
+                                                 base, *head, self.P.data_ptr(), self.m.data_ptr(),
+                                                 self.v.data_ptr(), self.t.data_ptr(), cfg.learning_rate, 0.9, 0.999,
+                                                 1e-5, cfg.max_grad_norm, self._ticket.data_ptr(), self._stream()),
+                "d2d_ppo_wgrad_head_adam")
         else:
             _ok(self.lib.d2d_ppo_wgrad_head(M, n, a_p, lda, b_p, ldb, pp, qq, wo, bo, row_len, wpart.data_ptr(), base,
                                             *head, self._stream()), "d2d_ppo_wgrad_head")

@@ -1,4 +1,4 @@
-/* d2d_ppo.h -- C ABI of libd2d_ppo.so: one PPO minibatch update in seven launches
+/* d2d_ppo.h -- C ABI of libd2d_ppo.so: one PPO minibatch update in five launches
  * (drone2d_amd.ppo.ManualStep).  The reference trains with
  * Stable-Baselines3 2.1's PPO.train (main.py:181-210); these kernels restate its loss head, the
  * backward pass through the two MLPs and clip_grad_norm_ + torch.optim.Adam over one flat
@@ -17,7 +17,7 @@
 extern "C" {
 #endif
 
-#define D2D_PPO_ABI_VERSION 2
+#define D2D_PPO_ABI_VERSION 3
 #define D2D_PPO_HEAD_BLOCK 64  /* v1: 256 */
 
 int32_t d2d_ppo_abi_version(void);
@@ -61,6 +61,21 @@ int32_t d2d_ppo_wgrad_head(int32_t m, int32_t n_problems, const float* const* a,
                            int32_t n_blocks, const float* head_partial, const float* log_std, float ent_coef,
                            float* log_std_grad, float* acc_pl, float* acc_vl, float* acc_ent, float* acc_clip,
                            void* stream);
+/* d2d_ppo_wgrad_head and d2d_ppo_adam in one launch (single-rank training: no gradient exchange
+ * between the two).  Whichever reduce workgroup finishes last (a device counter `ticket`, one
+ * int32 initialised to 0, which that workgroup resets to 0) runs the clip + Adam step over
+ * params[0 .. row_len) with g = the reduced gradient; same arithmetic and summation order as
+ * d2d_ppo_adam, so results are bit-identical to the two-call sequence.  row_len <= 16 384.  Added in
+ * ABI v3.  Measured slower than the two calls on MI355X (0.0403 vs 0.0337 s per 65 536-env update):
+ * the cross-workgroup hand-off needs an L2 write-back / invalidate (agent-scope fences) and the
+ * 256-thread Adam is load-latency bound, so drone2d_amd.ppo uses it only with D2D_PPO_FUSE_ADAM=1. */
+int32_t d2d_ppo_wgrad_head_adam(int32_t m, int32_t n_problems, const float* const* a, const int32_t* lda,
+                                const float* const* b, const int32_t* ldb, const int32_t* p, const int32_t* q,
+                                const int32_t* w_off, const int32_t* b_off, int32_t row_len, float* partial, float* g,
+                                int32_t n_blocks, const float* head_partial, const float* log_std, float ent_coef,
+                                float* log_std_grad, float* acc_pl, float* acc_vl, float* acc_ent, float* acc_clip,
+                                float* params, float* m1, float* m2, float* t, float lr, float b1, float b2, float eps,
+                                float max_norm, int32_t* ticket, void* stream);
 int32_t d2d_ppo_wgrad_chunks(int32_t m);
 
 /* The two MLPs (policy 27-64-64-2, value 27-64-64-1, tanh) per minibatch sample, four threads per
