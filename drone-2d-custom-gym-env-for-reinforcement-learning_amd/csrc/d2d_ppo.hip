@@ -551,14 +551,21 @@ __global__ __launch_bounds__(ADAM_THREADS) void adam_kernel(int n, float* __rest
                                                             float* __restrict__ t, float lr, float b1, float b2,
                                                             float eps, float max_norm) {
     __shared__ double red[ADAM_THREADS / 64];
-    float gv[ADAM_PER_THREAD];
-    double q = 0.0;
+    // the moments and parameters are loaded with the gradient, ahead of the norm's reduction, so
+    // the update below waits on no memory
+    float gv[ADAM_PER_THREAD], a0v[ADAM_PER_THREAD], v0v[ADAM_PER_THREAD], p0v[ADAM_PER_THREAD];
 #pragma unroll
     for (int k = 0; k < ADAM_PER_THREAD; ++k) {
         const int i = threadIdx.x + k * ADAM_THREADS;
-        gv[k] = i < n ? g[i] : 0.0f;
-        q += (double)gv[k] * gv[k];
+        const bool in = i < n;
+        gv[k] = in ? g[i] : 0.0f;
+        a0v[k] = in ? m1[i] : 0.0f;
+        v0v[k] = in ? m2[i] : 0.0f;
+        p0v[k] = in ? p[i] : 0.0f;
     }
+    double q = 0.0;
+#pragma unroll
+    for (int k = 0; k < ADAM_PER_THREAD; ++k) q += (double)gv[k] * gv[k];
     const double norm = sqrt(block_sum(q, red));
     // torch.nn.utils.clip_grad_norm_: clip_coef = max_norm / (norm + 1e-6), clamped to 1
     const float coef = fminf((float)(max_norm / (norm + 1e-6)), 1.0f);
@@ -571,12 +578,12 @@ __global__ __launch_bounds__(ADAM_THREADS) void adam_kernel(int n, float* __rest
         if (i < n) {
             const float gi = gv[k] * coef;
             g[i] = gi;
-            const float a0 = m1[i], v0 = m2[i];
+            const float a0 = a0v[k], v0 = v0v[k];
             const float a = a0 + (1.0f - b1) * (gi - a0);  // exp_avg.lerp_(grad, 1 - beta1)
             const float v = v0 * b2 + (1.0f - b2) * gi * gi;
             m1[i] = a;
             m2[i] = v;
-            p[i] -= a * lr_t / (sqrtf(v) / bc2s + eps);
+            p[i] = p0v[k] - a * lr_t / (sqrtf(v) / bc2s + eps);
         }
     }
     __syncthreads();
