@@ -891,6 +891,8 @@ __device__ __forceinline__ void wgrad_reduce_body(int n_chunks, int row_len, con
         g[e] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
 }
 
+// ADAM: the fused-Adam instantiation (its registers stay out of the plain reduce's)
+template <bool ADAM>
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(int n_chunks, int row_len, const float* __restrict__ partial,
                                                            float* __restrict__ g, HeadArgs H, AdamArgs A) {
     // with H.partial set, the last workgroup finishes the loss head (head_finish_kernel's work) and
@@ -900,8 +902,8 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(int n_chunks, int row
     } else {
         wgrad_reduce_body(n_chunks, row_len, partial, g, H);
     }
-    if (A.p == nullptr) return;
-    // with A.p set, the workgroup that finishes last runs the clip + Adam step on the whole of g
+    if (!ADAM) return;
+    // ADAM: the workgroup that finishes last runs the clip + Adam step on the whole of g
     __shared__ int last;
     __syncthreads();
     if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // the workgroup's g writes
@@ -976,8 +978,13 @@ static int32_t wgrad_launch(int32_t m, int32_t n_problems, const float* const* a
     if (H.partial != nullptr && (H.ls_grad < g || H.ls_grad + 2 > g + row_len)) return (int32_t)hipErrorInvalidValue;
     if (A.p != nullptr && (A.n != row_len || A.ticket == nullptr || A.n > ADAM_THREADS * ADAM_PER_THREAD))
         return (int32_t)hipErrorInvalidValue;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((row_len + 63) / 64 + (H.partial != nullptr)), dim3(256), 0,
-                       (hipStream_t)stream, nc, row_len, partial, g, H, A);
+    const dim3 rgrid((row_len + 63) / 64 + (H.partial != nullptr));
+    if (A.p != nullptr)
+        hipLaunchKernelGGL(wgrad_reduce_kernel<true>, rgrid, dim3(256), 0, (hipStream_t)stream, nc, row_len, partial, g,
+                           H, A);
+    else
+        hipLaunchKernelGGL(wgrad_reduce_kernel<false>, rgrid, dim3(256), 0, (hipStream_t)stream, nc, row_len, partial,
+                           g, H, A);
     return rc(hipGetLastError());
 }
 
