@@ -665,9 +665,9 @@ __device__ __forceinline__ void adam_body_256(const AdamArgs& A, float* __restri
 constexpr int ADAM_WG = 256, ADAM_SLICE = 4 * ADAM_WG;
 __global__ __launch_bounds__(ADAM_WG) void adam_spread_kernel(int n, float* __restrict__ p,
                                                               const float* __restrict__ g, float* __restrict__ m1,
-                                                              float* __restrict__ m2, const float* __restrict__ t,
+                                                              float* __restrict__ m2, float* __restrict__ t,
                                                               float lr, float b1, float b2, float eps,
-                                                              float max_norm) {
+                                                              float max_norm, int* __restrict__ ticket) {
     __shared__ double red[ADAM_WG / 64];
     const int base = blockIdx.x * ADAM_SLICE + threadIdx.x;
     float gs[4], a0[4], v0[4], p0[4];
@@ -705,6 +705,16 @@ __global__ __launch_bounds__(ADAM_WG) void adam_spread_kernel(int n, float* __re
             m2[e] = v;
             p[e] = p0[k] - a * lr_t / (sqrtf(v) / bc2s + eps);
         }
+    }
+    if (ticket == nullptr) return;  // adam_tick_kernel advances the step counter
+    // with a ticket: the workgroup that finishes last advances it.  Every workgroup has consumed its
+    // read of t[0] (its updates above depend on it) before its thread 0 takes a ticket, and no
+    // workgroup reads anything another one writes, so no fence is needed.
+    __syncthreads();
+    if (threadIdx.x == 0 &&
+        __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1) {
+        t[0] = step;
+        __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 __global__ void adam_tick_kernel(float* t) {
@@ -945,13 +955,22 @@ int32_t d2d_ppo_adam(int32_t n, float* p, float* g, float* m1, float* m2, float*
     if (n <= 0) return 0;
     if (D2D_PPO_ADAM_SPREAD) {
         hipLaunchKernelGGL(adam_spread_kernel, dim3((n + ADAM_SLICE - 1) / ADAM_SLICE), dim3(ADAM_WG), 0,
-                           (hipStream_t)stream, n, p, g, m1, m2, t, lr, b1, b2, eps, max_norm);
+                           (hipStream_t)stream, n, p, g, m1, m2, t, lr, b1, b2, eps, max_norm, nullptr);
         hipLaunchKernelGGL(adam_tick_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, t);
         return rc(hipGetLastError());
     }
     if (n > ADAM_THREADS * ADAM_PER_THREAD) return (int32_t)hipErrorInvalidValue;
     hipLaunchKernelGGL(adam_kernel, dim3(1), dim3(ADAM_THREADS), 0, (hipStream_t)stream, n, p, g, m1, m2, t, lr, b1,
                        b2, eps, max_norm);
+    return rc(hipGetLastError());
+}
+
+int32_t d2d_ppo_adam_spread(int32_t n, float* p, const float* g, float* m1, float* m2, float* t, float lr, float b1,
+                            float b2, float eps, float max_norm, int32_t* ticket, void* stream) {
+    if (n <= 0) return 0;
+    if (ticket == nullptr) return (int32_t)hipErrorInvalidValue;
+    hipLaunchKernelGGL(adam_spread_kernel, dim3((n + ADAM_SLICE - 1) / ADAM_SLICE), dim3(ADAM_WG), 0,
+                       (hipStream_t)stream, n, p, g, m1, m2, t, lr, b1, b2, eps, max_norm, ticket);
     return rc(hipGetLastError());
 }
 

@@ -142,6 +142,7 @@ def ppo_native():
             "d2d_ppo_adv_stats": [i32, vp, vp, vp, vp],
             "d2d_ppo_head_finish": [i32, i32, vp, vp, f32, vp, vp, vp, vp, vp, vp],
             "d2d_ppo_adam": [i32, vp, vp, vp, vp, vp, f32, f32, f32, f32, f32, vp],
+            "d2d_ppo_adam_spread": [i32, vp, vp, vp, vp, vp, f32, f32, f32, f32, f32, vp, vp],
             "d2d_ppo_wgrad": [i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp, vp, vp],
             "d2d_ppo_wgrad_head": [i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp, vp,
                                    i32, vp, vp, f32, vp, vp, vp, vp, vp, vp],
@@ -217,6 +218,8 @@ class ManualStep:
 
         self.fuse_adam = self.lib is not None and os.environ.get("D2D_PPO_FUSE_ADAM", "0") == "1"
         self._ticket = torch.zeros(1, dtype=torch.int32, device=device) if self.lib is not None else None
+        # D2D_PPO_ADAM_SPREAD=1: the Adam step over ~11 workgroups (d2d_ppo_adam_spread) instead of one
+        self.adam_spread = self.lib is not None and os.environ.get("D2D_PPO_ADAM_SPREAD", "0") == "1"
         o = 0
         for p in params:
             k = p.numel()
@@ -388,6 +391,12 @@ class ManualStep:
         if world > 1:
             dist.all_reduce(G)  # data-parallel PPO: mean gradient over the ranks (RCCL)
             G.div_(world)
+        if self.lib is not None and self.adam_spread:
+            _ok(self.lib.d2d_ppo_adam_spread(G.numel(), self.P.data_ptr(), G.data_ptr(), self.m.data_ptr(),
+                                             self.v.data_ptr(), self.t.data_ptr(), cfg.learning_rate, 0.9, 0.999,
+                                             1e-5, cfg.max_grad_norm, self._ticket.data_ptr(), self._stream()),
+                "d2d_ppo_adam_spread")
+            return
         if self.lib is not None:
             _ok(self.lib.d2d_ppo_adam(G.numel(), self.P.data_ptr(), G.data_ptr(), self.m.data_ptr(),
                                       self.v.data_ptr(), self.t.data_ptr(), cfg.learning_rate, 0.9, 0.999, 1e-5,

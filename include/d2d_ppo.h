@@ -42,6 +42,13 @@ int32_t d2d_ppo_head_finish(int32_t m, int32_t n_blocks, const float* partial, c
 int32_t d2d_ppo_adam(int32_t n, float* p, float* g, float* m1, float* m2, float* t, float lr, float b1, float b2,
                      float eps, float max_norm, void* stream);
 
+/* d2d_ppo_adam's step over ceil(n / 1024) workgroups in one launch, any n: every workgroup computes
+ * the full gradient norm itself and updates its slice; the last one to finish (device counter
+ * `ticket`, one int32 initialised to 0, reset to 0 by that workgroup) advances *t.  g is left
+ * unclipped.  Same arithmetic as d2d_ppo_adam except the norm's summation order.  Added in ABI v3. */
+int32_t d2d_ppo_adam_spread(int32_t n, float* p, const float* g, float* m1, float* m2, float* t, float lr, float b1,
+                            float b2, float eps, float max_norm, int32_t* ticket, void* stream);
+
 /* Weight and bias gradients of up to D2D_PPO_WGRAD_MAX linear layers in one launch (+ one reduce):
  * for problem k, g[w_off[k] + i q + j] = sum_r a_k[r][i] b_k[r][j] (i < p[k], j < q[k]; rows r < m;
  * a_k row stride lda[k], b_k ldb[k]; p, q <= 64) and g[b_off[k] + i] = sum_r a_k[r][i].  `a` and `b`
