@@ -84,8 +84,33 @@ def barrier_sync(world):
     torch.cuda.synchronize()
 
 
+def cpu_info() -> dict:
+    """The host's CPU budget: the affinity set, the cgroup CPU quota (if any), the CPU model."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(round(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"affinity_cores": aff, "cgroup_quota_cores": quota, "cpu_model": model}
+
+
 def cpu_baseline(args, kwargs):
-    """Time the C oracle on a bounded sample of the same workload (test infrastructure)."""
+    """Time the C oracle on a bounded sample of the same workload (test infrastructure).
+
+    Threads: one per core of the affinity set (1 core and all cores), capped only
+    by a cgroup CPU quota when one is set (more threads than the quota would time-slice) and by
+    D2D_CPU_THREADS if given; ``cores`` is the thread count actually used."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle
 
@@ -94,7 +119,12 @@ def cpu_baseline(args, kwargs):
     from drone2d_amd.env import build_scenarios
 
     oracle.build()
-    threads = min(len(os.sched_getaffinity(0)), 16)
+    info = cpu_info()
+    threads = info["affinity_cores"]
+    if info["cgroup_quota_cores"]:
+        threads = min(threads, info["cgroup_quota_cores"])
+    if os.environ.get("D2D_CPU_THREADS"):
+        threads = min(threads, int(os.environ["D2D_CPU_THREADS"]))
     n = args.envs
     scn = [s.to_c() for s in build_scenarios(kwargs)]
     b = oracle.OracleBatch(make_cfg(dict(kwargs)), scn, n)
@@ -118,9 +148,10 @@ def cpu_baseline(args, kwargs):
     dt1 = time.perf_counter() - t1
     b.close()
     return {"value": n * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "single_core_value": n * steps1 / dt1,
+            "single_core_value": n * steps1 / dt1, **info,
             "sample": f"C oracle (oracle/d2d_oracle.c, scalar fp64 port of the reference step), "
-                      f"{n} envs x {steps} steps of {args.scenario} with auto-reset, {threads} threads, "
+                      f"{n} envs x {steps} steps of {args.scenario} with auto-reset, {threads} threads "
+                      f"({info['affinity_cores']} cores in the affinity set, {info['cpu_model']}), "
                       f"{dt:.1f} s; single core: {steps1} steps, {dt1:.1f} s"}
 
 
@@ -137,8 +168,11 @@ def main():
     n = args.envs
     # this rank's block of a global batch of world x n envs (global env ids, no step collective)
     venv = shard.make_shard_venv(n * world, rank, world, device=dev, seed=12345, with_info=args.info, **kwargs)
-    g = torch.Generator(device=dev).manual_seed(1000 + rank)
-    bank = [(torch.rand(n, 2, device=dev, generator=g) * 2 - 1).contiguous() for _ in range(ACTION_BANK)]
+    # one global action bank (seed 1000) sliced by rank: a run of world x n envs in one process
+    # steps exactly the same envs with exactly the same actions (global env ids below)
+    g = torch.Generator(device=dev).manual_seed(1000)
+    bank = [(torch.rand(n * world, 2, device=dev, generator=g) * 2 - 1)[rank * n:(rank + 1) * n].contiguous()
+            for _ in range(ACTION_BANK)]
     venv.reset()
     stream = torch.cuda.current_stream(dev)
 
@@ -200,12 +234,14 @@ def main():
     kern_ms = float(np.sum([s.elapsed_time(e) for s, e in zip(starts, ends)])) / n_timed
 
     wall_t = torch.tensor([wall], dtype=torch.float64, device=dev)
-    kern_t = torch.tensor([kern_ms], dtype=torch.float64, device=dev)
+    kern_ranks = [kern_ms]
     if world > 1:
         dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
-        dist.all_reduce(kern_t, op=dist.ReduceOp.MAX)
+        kern_ranks = [None] * world
+        dist.all_gather_object(kern_ranks, kern_ms)
+        kern_ranks = [float(k) for k in kern_ranks]
     wall = float(wall_t.item())
-    kern_ms = float(kern_t.item())
+    kern_ms = max(kern_ranks)
 
     if rank == 0:
         total_steps = n * world * n_timed
@@ -241,8 +277,13 @@ def main():
                          "kernel": "d2d_step_kernel + d2d_fill_kernel/16 (per step)", "kernel_ms": kern_ms,
                          "bytes_per_env_step": bytes_env},
             "episodes": {"finished": float(st[1]), "mean_return": float(st[0] / max(st[1], 1)),
-                         "success": float(st[2]), "collisions": float(st[4]),
+                         "success": float(st[2]), "fails": float(st[3]), "collisions": float(st[4]),
+                         "sum_ape": float(st[5]), "sum_len": float(st[6]),
                          "allreduce_ms": t_ar * 1e3},
+            # the multi-rank evidence: ranks that stepped, the collective's backend, each rank's
+            # device time per step (the line's kernel_ms is their max)
+            "ranks": world, "backend": (dist.get_backend() if world > 1 else None),
+            "kernel_ms_per_rank": kern_ranks,
         }
         vf = os.path.join(REPO, "profiles", f"valu_{tag}.json")
         if os.path.exists(vf):

@@ -53,16 +53,21 @@ def test_golden_teacher_forced(d2, which):
     venv.close()
 
 
-@pytest.mark.parametrize("scn", ["corridor", "S_corridor", "large", "mixed"])
-def test_vs_oracle_teacher_forced(d2, scn):
+@pytest.mark.parametrize("scn,n", [("corridor", 2048), ("S_corridor", 2048), ("large", 2048), ("mixed", 2048),
+                                   ("corridor_free", 4096)])
+def test_vs_oracle_teacher_forced(d2, scn, n):
+    """HIP vs oracle with auto-reset, teacher-forced every step.  corridor_free at 4 096 envs is
+    BASELINE configs[1] (no obstacles: obs 8..16 = (1, 0, 0) x 3, CA = 0)."""
     scenarios = SCENARIOS if scn == "mixed" else [scn]
-    venv, orc = make_pair(d2, 2048, scenarios, seed=99, kwargs=_cfgkw())
+    venv, orc = make_pair(d2, n, scenarios, seed=99, kwargs=_cfgkw())
     rng = np.random.default_rng(1)
     dones = 0
-    for t in range(150):
+    for t in range(160):
         act = np.clip(rng.normal(0.0, 0.6, (venv.num_envs, 2)), -1, 1).astype(np.float32)
         compare_step(venv, orc, act)
         dones += int(orc.term.sum())
+        if scn.endswith("_free"):
+            np.testing.assert_array_equal(orc.obs[:, 8:17], np.tile([1.0, 0.0, 0.0], 3)[None].repeat(n, 0))
     assert dones > 50  # auto-resets were exercised
     venv.close()
 
@@ -247,13 +252,18 @@ def test_full_size_determinism_and_shard_invariance(d2):
     assert torch.equal(torch.cat([s0[2], s1[2]], 1), a[2])
 
 
-@pytest.mark.parametrize("scn", ["corridor", "large", "S_corridor"])
-def test_full_size_properties(d2, scn):
-    obs0, outs, st, ist, stats = _rollout(d2, FULL, 3, 60, scn=scn)
+@pytest.mark.parametrize("scn,n", [("corridor", FULL), ("large", FULL), ("S_corridor", FULL),
+                                   ("corridor_free", 4096)])
+def test_full_size_properties(d2, scn, n):
+    """BASELINE sizes: 65 536 envs (configs[2], [3]) and configs[1]'s 4 096 obstacle-free envs."""
+    obs0, outs, st, ist, stats = _rollout(d2, n, 3, 60, scn=scn)
     assert torch.isfinite(obs0).all()
     n_done = 0
+    free = torch.tensor([1.0, 0.0, 0.0] * 3, device=obs0.device)
     for obs, rew, term in outs:
         assert torch.isfinite(obs).all() and torch.isfinite(rew).all()
+        if scn.endswith("_free"):  # no obstacles: the unfilled sensor slots (drone_2d_env.py:660-720)
+            assert torch.equal(obs[:, 8:17], free.expand(n, 9))
         # sin/cos slots are in [-1, 1]; distance slots are 2d/diag - 1 >= -1 - r/diag
         sc = obs[:, [9, 10, 12, 13, 15, 16, 17, 18, 23, 24, 25, 26]]
         assert (sc.abs() <= 1.0 + 1e-6).all()

@@ -142,3 +142,111 @@ def test_flight_paths(d2, tmp_path):
     back = json.load(open(tmp_path / "flight_paths"))
     assert [len(p) for p in back] == list(m["time_spent"]) and back[0][0] == fps[0][0]
     assert s["Successes"] + s["Fails"] == n
+
+
+# ---------------------------------------------------------------- sharded test loop (§8(f)-3 at scale)
+N_SHARD = 37  # odd: uneven shards
+
+
+def _harness_worker(rank, world, port, out_dir, hip=False):
+    import sys
+
+    for p in (HERE, os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "oracle")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+
+    import drone2d_amd  # noqa: F401
+    from drone2d_amd import harness, shard
+    from drone2d_amd.config import ENV_TEST_CONFIG
+    from oracle_backend import OracleVecBackend
+
+    shard.init_process_group_from_env("gloo")
+    kw = dict(ENV_TEST_CONFIG, scenario="corridor")
+    n = N_SHARD if not hip else 4 * N_SHARD
+    if hip:
+        be = shard.make_shard_venv(n, rank, world, device=torch.device("cuda", 0), seed=3, **kw)
+    else:
+        off, cnt = shard.shard_range(n, world, rank)
+        be = OracleVecBackend(cnt, seed=3, env_id_offset=off, **kw)
+    pol = harness.MlpActor.from_npz(os.path.join(GOLD, "agent_17_90.npz"), batch_invariant=True)
+    m = harness.run_first_episodes(be, pol, seed=3, flight_paths=True)
+    s = harness.write_results_rank0(m, os.path.join(out_dir, "sharded"), "corridor", "17", "agent")
+    assert (s is None) == (rank != 0)
+    if rank == 0:
+        assert m["successes"] + m["fails"] + m["unfinished"] == n
+    dist.barrier()
+    dist.destroy_process_group()
+    be.close()
+
+
+def _single(out_dir, hip=False):
+    from drone2d_amd import harness
+    from drone2d_amd.config import ENV_TEST_CONFIG
+
+    kw = dict(ENV_TEST_CONFIG, scenario="corridor")
+    if hip:
+        import drone2d_amd as d2
+
+        be = d2.Drone2dVecEnv(4 * N_SHARD, device=torch.device("cuda", 0), seed=3, **kw)
+    else:
+        be = OracleVecBackend(N_SHARD, seed=3, **kw)
+    pol = harness.MlpActor.from_npz(os.path.join(GOLD, "agent_17_90.npz"), batch_invariant=True)
+    m = harness.run_first_episodes(be, pol, seed=3, flight_paths=True)
+    be.close()
+    harness.write_results(m, os.path.join(out_dir, "single"), "corridor", "17", "agent")
+    return m
+
+
+def _sharded_files_match(tmp_path, hip):
+    import socket
+
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_harness_worker, args=(r, 2, port, str(tmp_path), hip)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=600)
+        assert p.exitcode == 0
+    m = _single(str(tmp_path), hip)
+    assert m["unfinished"] == 0 and m["successes"] + m["fails"] > 0
+    files = ["corridor_17_results.txt", "flight_paths", "collisions.npy", "rewards.npy", "apes.npy",
+             "time_spent.npy"]
+    for f in files:
+        a = open(tmp_path / "sharded" / f, "rb").read()
+        b = open(tmp_path / "single" / f, "rb").read()
+        assert a == b, f
+
+
+def test_sharded_test_loop_matches_single_batch(d2, tmp_path):
+    """main.py:258-327 over two gloo ranks (the C oracle standing in for each rank's GPU shard:
+    test infrastructure): rank 0 gathers the per-episode records in global env order and writes
+    results.txt, the four .npy files and flight_paths byte-identical to one unsharded batch."""
+    _sharded_files_match(tmp_path, hip=False)
+
+
+@pytest.mark.gpu
+def test_sharded_test_loop_hip_matches_single_batch(d2, tmp_path):
+    """The same with each rank's HIP shard (two processes on the one GPU, gloo for the gather)."""
+    _sharded_files_match(tmp_path, hip=True)
+
+
+def test_batch_invariant_actor(d2):
+    """The fixed-order actor gives each row the same action whatever batch it is evaluated in."""
+    from drone2d_amd import harness
+
+    pol = harness.MlpActor.from_npz(os.path.join(GOLD, "agent_17_90.npz"), batch_invariant=True)
+    ref = harness.MlpActor.from_npz(os.path.join(GOLD, "agent_17_90.npz"))
+    x = torch.from_numpy(np.random.default_rng(1).uniform(-1, 1, (301, 27)).astype(np.float32))
+    full = pol.act(x, deterministic=True)
+    for a, b in ((0, 1), (5, 77), (100, 301)):
+        assert torch.equal(pol.act(x[a:b], deterministic=True), full[a:b])
+    np.testing.assert_allclose(full.numpy(), ref.act(x, deterministic=True).numpy(), atol=1e-5)
