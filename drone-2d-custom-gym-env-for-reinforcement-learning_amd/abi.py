@@ -7,7 +7,7 @@ from __future__ import annotations
 
 import ctypes as C
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 MAX_WPS = 16
 MAX_SEGS = MAX_WPS - 2
@@ -71,4 +71,15 @@ class D2DScn(C.Structure):
         ("spawn_xmin", C.c_double), ("spawn_xmax", C.c_double),
         ("spawn_ymin", C.c_double), ("spawn_ymax", C.c_double),
         ("spawn_amin", C.c_double), ("spawn_amax", C.c_double),
+    ]
+
+
+class D2DCurriculum(C.Structure):
+    """d2d_curriculum: the fresh curriculum generator's parameters (cfg.scn_pool = 2)."""
+    _fields_ = [
+        ("stage", C.c_int32), ("n_wps", C.c_int32),
+        ("segment_length", C.c_double),
+        ("random_path_spawn", C.c_int32), ("corner_lo", C.c_int32), ("corner_hi", C.c_int32),
+        ("pad", C.c_int32),
+        ("sim_num0", C.c_double), ("envs_total", C.c_double),
     ]

@@ -1,0 +1,285 @@
+// d2d_curriculum.h -- the curriculum reset generator on the device (cfg.scn_pool = 2, "fresh").
+//
+// The reference's curriculum env draws a new scenario at every reset (drone_2d_env.py:199-215,
+// 318-372): a corner (random.randint over spawn_corners), a random waypoint path
+// (generate_random_waypoints_2d, predef_path.py:307-363) and its QPMI2D fit (:20-50), then by stage
+// a spawn box (stage 2) or obstacles around / on the path (generate_obstacles_around_path,
+// obstacles.py:58-89), the stage following the step count sim_num (:326-372).  Here the episode
+// that env i starts with episode counter k gets G(seed, gid i, k, stage): the same draws in the
+// same order from a Philox stream keyed by (seed, gid, k) instead of NumPy's / Python's global
+// generators, so every episode's scenario is independent of the batch size and of the sharding.
+// The stream, the fit and the arithmetic are restated by the CPU oracle (oracle/d2d_oracle.c,
+// o_gen_curriculum); sin / cos / log come from d2d_pmath.h on both sides so the two draw
+// bit-identical scenarios.  The host generator drone2d_amd/curriculum.py (bit-exact against the
+// reference's own draws) is the distributional reference (tests/test_curriculum.py, GPU KS tests).
+//
+// Deviations from the reference, all distribution-preserving: the normal draws use the polar method
+// (NumPy's legacy gauss) on Philox uniforms; np.random.binomial(1, p) is u < p; the direction angle
+// of an obstacle offset is taken as the path gradient's unit normal, cos / sin(atan2(dy, dx) - pi/2)
+// = (dy, -dx) / |(dx, dy)|; sim_num values that fall in the reference's schedule gaps (exactly
+// 700 000, 1e6, 1.6e6, 2e6, where the reference creates no drone and fails) take the stage below.
+#pragma once
+#include "d2d_device.h"
+#include "d2d_pmath.h"
+
+namespace d2d {
+
+constexpr uint32_t GEN_TAG = 0x43550000u;  // Philox counter word 2 of the generator's blocks
+
+// sequential uniforms of one (seed, gid, key) stream: block b = Philox(gid, key, GEN_TAG + b, 0)
+struct GenRng {
+    uint32_t gid, key, k0, k1, blk, pos;
+    uint32_t buf[4];
+    __device__ void init(uint64_t seed, uint32_t g, uint32_t k) {
+        gid = g;
+        key = k;
+        k0 = (uint32_t)seed;
+        k1 = (uint32_t)(seed >> 32);
+        blk = 0;
+        pos = 4;
+    }
+    __device__ uint32_t next32() {
+        if (pos == 4) {
+            philox(gid, key, GEN_TAG + blk, 0u, k0, k1, buf);
+            ++blk;
+            pos = 0;
+        }
+        return buf[pos++];
+    }
+    __device__ double u01() {  // [0, 1), 53 bits
+        const uint32_t a = next32(), b = next32();
+        return u53(a, b);
+    }
+    // numpy / Python uniform(low, high) = low + (high - low) * random()
+    __device__ double uniform(double lo, double hi) { return lo + (hi - lo) * u01(); }
+    // random.randint(a, b): uniform over {a, ..., b}
+    __device__ int randint(int a, int b) {
+        const int k = (int)(u01() * (double)(b - a + 1));
+        return a + (k < b - a ? k : b - a);
+    }
+    // np.random.normal(mean, std): the polar method (NumPy's legacy gauss), one value per pair
+    __device__ double normal(double mean, double std) {
+        double x1, x2, r2;
+        int guard = 0;
+        do {
+            x1 = 2.0 * u01() - 1.0;
+            x2 = 2.0 * u01() - 1.0;
+            r2 = x1 * x1 + x2 * x2;
+        } while ((r2 >= 1.0 || r2 == 0.0) && ++guard < 64);
+        const double f = sqrt(-2.0 * d2d_pm_log(r2) / r2);
+        return mean + std * (f * x2);
+    }
+};
+
+// the reference's sim_num schedule (drone_2d_env.py:326-372); *chance: the obstacle spawn chance of
+// stages 3 / 4 (linear ramps), from `stage` when the curriculum fixes one (stage_3: 0.6, stage_4: 1)
+__host__ __device__ inline int gen_stage(const d2d_curriculum& c, double sim, double* chance) {
+    *chance = 0.0;
+    int st = c.stage;
+    if (st < 1 || st > 5) {
+        // (0 <= sim < 700 000: stage 1; the gaps 700 000 / 1e6 / 1.6e6 / 2e6 and negative counts,
+        // where the reference creates no drone, take the stage below)
+        if (sim <= 700000.0) st = 1;
+        else if (sim <= 1000000.0) st = 2;
+        else if (sim <= 1600000.0) st = 3;
+        else if (sim <= 2000000.0) st = 4;
+        else st = 5;
+        if (st == 3) *chance = (sim - 1000000.0) * (0.6 - 0.2) / (1600000.0 - 1000000.0) + 0.2;
+        if (st == 4) *chance = (sim - 1600000.0) * (1.0 - 0.6) / (2000000.0 - 1600000.0) + 0.6;
+        return st;
+    }
+    if (st == 3) *chance = 0.6;
+    if (st == 4) *chance = 1.0;
+    return st;
+}
+
+// QPMI2D fit (predef_path.py:20-50): knots = cumulative segment lengths; one quadratic per interior
+// waypoint n through (u_{n-1}, u_n, u_{n+1}), the 3x3 system solved by Gaussian elimination with
+// partial pivoting (NumPy: inv(U_n).dot(wp); same solution to rounding)
+__device__ inline void gen_solve3(double A[3][3], double b[3], double x[3]) {
+    for (int c = 0; c < 3; ++c) {
+        int p = c;
+        for (int r = c + 1; r < 3; ++r)
+            if (fabs(A[r][c]) > fabs(A[p][c])) p = r;
+        if (p != c) {
+            for (int k = 0; k < 3; ++k) {
+                const double t = A[c][k];
+                A[c][k] = A[p][k];
+                A[p][k] = t;
+            }
+            const double t = b[c];
+            b[c] = b[p];
+            b[p] = t;
+        }
+        for (int r = c + 1; r < 3; ++r) {
+            const double f = A[r][c] / A[c][c];
+            for (int k = c + 1; k < 3; ++k) A[r][k] = A[r][k] - f * A[c][k];
+            b[r] = b[r] - f * b[c];
+        }
+    }
+    for (int r = 2; r >= 0; --r) {
+        double s = b[r];
+        for (int k = r + 1; k < 3; ++k) s = s - A[r][k] * x[k];
+        x[r] = s / A[r][r];
+    }
+}
+__device__ inline void gen_fit(const double* wx, const double* wy, int nw, d2d_scn& s) {
+    s.n_wps = nw;
+    double acc = 0.0;
+    s.us[0] = 0.0;
+    for (int i = 0; i + 1 < nw; ++i) {
+        const double dx = wx[i + 1] - wx[i], dy = wy[i + 1] - wy[i];
+        acc = acc + sqrt(dx * dx + dy * dy);
+        s.us[i + 1] = acc;
+    }
+    for (int i = nw; i < D2D_MAX_WPS; ++i) s.us[i] = 0.0;
+    for (int k = nw - 2; k < D2D_MAX_SEGS; ++k) s.xa[k] = s.xb[k] = s.xc[k] = s.ya[k] = s.yb[k] = s.yc[k] = 0.0;
+    for (int n = 1; n + 1 < nw; ++n) {
+        const double u[3] = {s.us[n - 1], s.us[n], s.us[n + 1]};
+        double A[3][3], B[3][3], bx[3] = {wx[n - 1], wx[n], wx[n + 1]}, by[3] = {wy[n - 1], wy[n], wy[n + 1]}, px[3],
+                                   py[3];
+        for (int r = 0; r < 3; ++r) {
+            A[r][0] = B[r][0] = u[r] * u[r];
+            A[r][1] = B[r][1] = u[r];
+            A[r][2] = B[r][2] = 1.0;
+        }
+        gen_solve3(A, bx, px);
+        gen_solve3(B, by, py);
+        s.xa[n - 1] = px[0];
+        s.xb[n - 1] = px[1];
+        s.xc[n - 1] = px[2];
+        s.ya[n - 1] = py[0];
+        s.yb[n - 1] = py[1];
+        s.yc[n - 1] = py[2];
+    }
+}
+// QPMI2D.calculate_gradient (predef_path.py:145-188; drone2d_amd/scenarios.py QPMIPath.gradient)
+__device__ inline void gen_gradient(const d2d_scn& s, double u, double& gx, double& gy) {
+    const int nw = s.n_wps, last = nw - 3;
+    if (u >= s.us[0] && u <= s.us[1]) {
+        gx = s.xa[0] * u * 2.0 + s.xb[0];
+        gy = s.ya[0] * u * 2.0 + s.yb[0];
+        return;
+    }
+    if (u >= s.us[nw - 2]) {
+        gx = s.xa[last] * u * 2.0 + s.xb[last];
+        gy = s.ya[last] * u * 2.0 + s.yb[last];
+        return;
+    }
+    int n = 0;
+    while (n < nw - 1 && !(u <= s.us[n + 1])) ++n;
+    const double du = s.us[n + 1] - s.us[n];
+    const double mr = (u - s.us[n]) / du, mf = (s.us[n + 1] - u) / du;
+    const double dx1 = s.xa[n - 1] * u * 2.0 + s.xb[n - 1], dy1 = s.ya[n - 1] * u * 2.0 + s.yb[n - 1];
+    const double dx2 = s.xa[n] * u * 2.0 + s.xb[n], dy2 = s.ya[n] * u * 2.0 + s.yb[n];
+    gx = mr * dx2 + mf * dx1;
+    gy = mr * dy2 + mf * dy1;
+}
+
+// generate_obstacles_around_path (obstacles.py:58-89): appends up to n circles (the reference's
+// `while num_obstacles < n` with a real-valued n), rejection on |offset| <= size + 10 off the path
+__device__ inline void gen_obstacles(GenRng& R, const Scn& S, d2d_scn& s, double n, double mean, double std, bool on_path) {
+    const double L = s.us[s.n_wps - 1];
+    int num = 0, tries = 0;
+    while ((double)num < n && s.n_circles < D2D_MAX_CIRCLES && tries < 4096) {
+        ++tries;
+        const double u = R.uniform(0.20 * L, 0.90 * L);
+        double gx, gy;
+        gen_gradient(s, u, gx, gy);
+        const double dist = R.normal(mean, std);
+        double x, y;
+        path_eval(S, u, x, y);
+        // (cos, sin)(atan2(gy, gx) - pi/2) = (gy, -gx) / |g|
+        const double g = sqrt(gx * gx + gy * gy);
+        const double ox = x + dist * (gy / g), oy = y + dist * (-gx / g);
+        const double size = R.uniform(10.0, 50.0);
+        const double dx = ox - x, dy = oy - y;
+        const double off = sqrt(dx * dx + dy * dy);
+        if (!on_path && off > size + 10.0) {
+            s.cx[s.n_circles] = ox;
+            s.cy[s.n_circles] = oy;
+            s.cr[s.n_circles] = size;
+            s.n_circles += 1;
+            ++num;
+        } else if (on_path) {
+            s.cx[s.n_circles] = x;
+            s.cy[s.n_circles] = y;
+            s.cr[s.n_circles] = size;
+            s.n_circles += 1;
+            ++num;
+        }
+    }
+}
+
+// one curriculum reset: writes the ABI record `s` and its device form `S` (both in global memory)
+__device__ inline void gen_curriculum(const d2d_curriculum& c, double W, double H, uint64_t seed, uint32_t gid,
+                                      uint32_t key, double sim, d2d_scn& s, Scn& S) {
+    GenRng R;
+    R.init(seed, gid, key);
+    const int corner = c.random_path_spawn ? R.randint(c.corner_lo, c.corner_hi) : 2;  // 1 DL 2 DR 3 UL 4 UR
+    const int nw = c.n_wps < 3 ? 3 : (c.n_wps > D2D_MAX_WPS ? D2D_MAX_WPS : c.n_wps);
+    double wx[D2D_MAX_WPS], wy[D2D_MAX_WPS];
+    double lo, hi;
+    if (corner == 1) {
+        wx[0] = R.uniform(100.0, 180.0);
+        wy[0] = R.uniform(100.0, 180.0);
+        lo = 0.0;
+        hi = PI / 2.0;
+    } else if (corner == 3) {
+        wx[0] = R.uniform(100.0, 180.0);
+        wy[0] = R.uniform(H - 180.0, H - 100.0);
+        lo = 0.0;
+        hi = -PI / 2.0;
+    } else if (corner == 4) {
+        wx[0] = R.uniform(W - 180.0, W - 100.0);
+        wy[0] = R.uniform(H - 180.0, H - 100.0);
+        lo = -PI / 2.0;
+        hi = -PI;
+    } else {
+        wx[0] = R.uniform(W - 180.0, W - 100.0);
+        wy[0] = R.uniform(100.0, 180.0);
+        lo = PI / 2.0;
+        hi = PI;
+    }
+    for (int i = 0; i + 1 < nw; ++i) {
+        const double az = R.uniform(lo, hi);
+        double sa, ca;
+        d2d_pm_sincos(az, &sa, &ca);
+        wx[i + 1] = wx[i] + c.segment_length * ca;
+        wy[i + 1] = wy[i] + c.segment_length * sa;
+    }
+    gen_fit(wx, wy, nw, s);
+    s.n_circles = 0;
+    s.wp_last_x = wx[nw - 1];
+    s.wp_last_y = wy[nw - 1];
+    s.spawn_xmin = s.spawn_xmax = wx[0];
+    s.spawn_ymin = s.spawn_ymax = wy[0];
+    s.spawn_amin = -PI / 4.0;
+    s.spawn_amax = PI / 4.0;
+    double chance;
+    const int st = gen_stage(c, sim, &chance);
+    if (st == 2) {  // drone spawned uniformly on the screen, no obstacles (:333-337)
+        s.spawn_xmin = 100.0;
+        s.spawn_xmax = W - 100.0;
+        s.spawn_ymin = 100.0;
+        s.spawn_ymax = H - 100.0;
+    }
+    scn_build(s, S);  // the path, for the obstacle placement
+    if (st == 3) {
+        if (R.u01() < chance) gen_obstacles(R, S, s, 1.0, 0.0, 100.0, false);
+    } else if (st == 4) {
+        if (R.u01() < chance) gen_obstacles(R, S, s, 1.0, 0.0, 0.0, true);
+    } else if (st == 5) {
+        double n_obs = R.normal(1.0, 4.0);
+        if (n_obs < 0.0 && n_obs > -3.0) n_obs = 1.0;
+        if (n_obs < -3.0) n_obs = 0.0;
+        if (n_obs != 0.0) {
+            gen_obstacles(R, S, s, n_obs, 0.0, 100.0, false);
+            gen_obstacles(R, S, s, 1.0, 0.0, 0.0, true);
+        }
+    }
+    for (int k = s.n_circles; k < D2D_MAX_CIRCLES; ++k) s.cx[k] = s.cy[k] = s.cr[k] = 0.0;
+    scn_build(s, S);
+}
+
+}  // namespace d2d

@@ -67,7 +67,7 @@ struct Scn {
 static_assert(sizeof(Scn) % 16 == 0, "Scn size");
 // Returns false if the table is outside what the record form reproduces exactly: the last-segment
 // window us[nw-2] - 0.001 must not reach back past us[nw-3] (always true for real waypoints).
-inline bool scn_build(const d2d_scn& a, Scn& s) {
+__host__ __device__ inline bool scn_build(const d2d_scn& a, Scn& s) {
     const int nw = a.n_wps, nseg = nw - 2;
     if (nw >= 4 && !(a.us[nw - 2] - 0.001 > a.us[nw - 3])) return false;
     s.n_wps = nw;

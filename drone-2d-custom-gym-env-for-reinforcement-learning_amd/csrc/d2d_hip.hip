@@ -67,6 +67,16 @@ struct d2d_handle {
     int32_t* env_slot = nullptr;  // [n] env -> slot
     int n_groups = 0;
     uint64_t n_steps = 0;        // d2d_step calls (fill cadence)
+    // pool / fresh curriculum
+    d2d_scn* abi = nullptr;      // [n_scn] ABI records of the table (pool and fresh modes: readback)
+    int pool_valid = 0;          // pool mode: bit h = half h holds uploaded scenarios
+    d2d_curriculum cur{};        // fresh mode: generator parameters
+    int32_t* scn_tag = nullptr;  // fresh mode: [2 n] episode key of each slot
+    int64_t* gclk = nullptr;     // fresh mode: [2 n] clock at generation
+    int64_t* clock = nullptr;    // [1] the step clock (K1 advances it)
+    uint64_t fresh_seed = 0;
+    bool fresh_seeded = false;
+    int32_t generation = 0;      // bumped whenever captured graphs' pointers go stale
 };
 
 namespace {
@@ -96,8 +106,34 @@ StepArgs make_args(const d2d_t* h) {
     a.rc_tag = h->rc_tag;
     a.lane_env = h->lane_env;
     a.wg_scn = h->wg_scn;
+    a.scn_tag = h->scn_tag;
+    a.clock = h->clock;
     return a;
 }
+
+// K5: the fresh curriculum's scenario slots (restore: every slot from its recipe), on `stream`
+hipError_t fresh_regen(d2d_t* h, hipStream_t stream, bool restore = false) {
+    FreshArgs f{};
+    f.n = h->n;
+    f.ist = h->ist;
+    f.env_scn = h->env_scn;
+    f.cur = h->cur;
+    f.W = h->cfg.screen_w;
+    f.H = h->cfg.screen_h;
+    f.seed = h->seed;
+    f.env_id_base = (uint32_t)h->cfg.env_id_base;
+    f.abi = h->abi;
+    f.scn = h->scn;
+    f.brt = h->brt;
+    f.tag = h->scn_tag;
+    f.gclk = h->gclk;
+    f.clock = h->clock;
+    f.restore = restore ? 1 : 0;
+    const int items = restore ? 2 * h->n : h->n;
+    hipLaunchKernelGGL(d2d_fresh_kernel, dim3((items + 63) / 64), dim3(64), 0, stream, f);
+    return hipGetLastError();
+}
+bool fresh_mode(const d2d_t* h) { return h->cfg.scn_pool == 2; }
 
 // K4: fill every cache entry that does not belong to its env's current episode, ordered on `stream`
 hipError_t rc_fill(d2d_t* h, hipStream_t stream, bool force = false) {
@@ -289,6 +325,8 @@ int32_t d2d_create(const d2d_cfg* cfg, int32_t n_envs, int32_t device, d2d_t** o
         (e = hipMemset(h->pool_dev, 0, sizeof(int32_t))) != hipSuccess ||
         (e = hipMalloc(&h->fill_ctl, 2 * sizeof(int32_t))) != hipSuccess ||
         (e = hipMemset(h->fill_ctl, 0, 2 * sizeof(int32_t))) != hipSuccess ||
+        (e = hipMalloc(&h->clock, sizeof(int64_t))) != hipSuccess ||
+        (e = hipMemset(h->clock, 0, sizeof(int64_t))) != hipSuccess ||
         (e = alloc_layout(L, n_envs, {}, {})) != hipSuccess) {
         d2d_destroy(h);
         return hip_fail(e, "d2d_create: hipMalloc");
@@ -313,6 +351,10 @@ void d2d_destroy(d2d_t* h) {
     if (h->env_scn) (void)hipFree(h->env_scn);
     if (h->pool_dev) (void)hipFree(h->pool_dev);
     if (h->fill_ctl) (void)hipFree(h->fill_ctl);
+    if (h->clock) (void)hipFree(h->clock);
+    if (h->abi) (void)hipFree(h->abi);
+    if (h->scn_tag) (void)hipFree(h->scn_tag);
+    if (h->gclk) (void)hipFree(h->gclk);
     delete h;
 }
 
@@ -329,6 +371,7 @@ int32_t d2d_debug_stamps(d2d_t* h, uint64_t* buf) {
 
 int32_t d2d_set_scenarios(d2d_t* h, const d2d_scn* scns, int32_t n_scn, const int32_t* env_scn_host) {
     if (!h || !scns || n_scn <= 0) return fail(D2D_E_ARG, "d2d_set_scenarios: null handle/scenarios or n_scn <= 0");
+    if (fresh_mode(h)) return fail(D2D_E_ARG, "d2d_set_scenarios: fresh curriculum mode (cfg.scn_pool = 2) uses d2d_set_curriculum");
     for (int k = 0; k < n_scn; ++k) {
         const d2d_scn& s = scns[k];
         if (s.n_wps < 3 || s.n_wps > D2D_MAX_WPS)
@@ -351,9 +394,11 @@ int32_t d2d_set_scenarios(d2d_t* h, const d2d_scn* scns, int32_t n_scn, const in
     hipError_t e;
     d2d::Scn* scn = nullptr;
     d2d::BrTab* brt = nullptr;
+    d2d_scn* abi = nullptr;
     auto drop = [&](hipError_t err, const char* what) {
         if (scn) (void)hipFree(scn);
         if (brt) (void)hipFree(brt);
+        if (abi) (void)hipFree(abi);
         return hip_fail(err, what);
     };
     // pool mode: room for a second pool half (d2d_refresh_pool), zero until the first refresh
@@ -362,6 +407,12 @@ int32_t d2d_set_scenarios(d2d_t* h, const d2d_scn* scns, int32_t n_scn, const in
     if ((e = hipMalloc(&scn, sizeof(d2d::Scn) * T)) != hipSuccess) return drop(e, "hipMalloc scn");
     if ((e = hipMemset(scn, 0, sizeof(d2d::Scn) * T)) != hipSuccess) return drop(e, "hipMemset scn");
     if ((e = hipMemcpy(scn, tab.data(), bytes, hipMemcpyHostToDevice)) != hipSuccess) return drop(e, "hipMemcpy scn");
+    if (h->cfg.scn_pool) {  // pool mode keeps the ABI records for checkpoints / readback
+        if ((e = hipMalloc(&abi, sizeof(d2d_scn) * T)) != hipSuccess) return drop(e, "hipMalloc abi");
+        if ((e = hipMemset(abi, 0, sizeof(d2d_scn) * T)) != hipSuccess) return drop(e, "hipMemset abi");
+        if ((e = hipMemcpy(abi, scns, sizeof(d2d_scn) * (size_t)n_scn, hipMemcpyHostToDevice)) != hipSuccess)
+            return drop(e, "hipMemcpy abi");
+    }
     // golden-march tables: forced searches on the device (same arithmetic as the step kernels)
     if ((e = hipMalloc(&brt, sizeof(d2d::BrTab) * T)) != hipSuccess) return drop(e, "hipMalloc brt");
     if ((e = hipMemset(brt, 0, sizeof(d2d::BrTab) * T)) != hipSuccess) return drop(e, "hipMemset brt");
@@ -390,11 +441,15 @@ int32_t d2d_set_scenarios(d2d_t* h, const d2d_scn* scns, int32_t n_scn, const in
     }
     if (h->scn) (void)hipFree(h->scn);
     if (h->brt) (void)hipFree(h->brt);
+    if (h->abi) (void)hipFree(h->abi);
     h->scn = scn;
     h->brt = brt;
+    h->abi = abi;
     h->n_scn = (int)T;
     h->pool_base = 0;
     h->pool_n = n_scn;
+    h->pool_valid = 1;
+    h->generation += 1;  // the old tables are freed: captured graphs point at them
     h->rc_dirty = true;  // cached reset observations belong to the old scenarios
     e = env_scn_host ? hipMemcpy(h->env_scn, env_scn_host, sizeof(int32_t) * (size_t)h->n, hipMemcpyHostToDevice)
                      : hipMemset(h->env_scn, 0, sizeof(int32_t) * (size_t)h->n);
@@ -412,6 +467,19 @@ int32_t d2d_reset(d2d_t* h, const uint8_t* mask_dev, uint64_t seed, float* obs_d
     if (h->n_scn <= 0) return fail(D2D_E_STATE, "d2d_reset: call d2d_set_scenarios first");
     DeviceGuard g(h->device);
     h->seed = seed;
+    hipError_t e;
+    if (fresh_mode(h)) {
+        // scenarios are keyed by the seed: a new seed drops every slot; then the slots of the
+        // episodes this reset starts
+        if (!h->fresh_seeded || h->fresh_seed != seed) {
+            if ((e = hipMemsetAsync(h->scn_tag, 0xFF, sizeof(int32_t) * 2 * (size_t)h->n, (hipStream_t)stream)) !=
+                hipSuccess)
+                return hip_fail(e, "d2d_reset: fresh slots");
+            h->fresh_seed = seed;
+            h->fresh_seeded = true;
+        }
+        if ((e = fresh_regen(h, (hipStream_t)stream)) != hipSuccess) return hip_fail(e, "d2d_reset: fresh scenarios");
+    }
     StepArgs a = make_args(h);
     a.obs = obs_dev;
     a.mask = mask_dev;
@@ -420,8 +488,10 @@ int32_t d2d_reset(d2d_t* h, const uint8_t* mask_dev, uint64_t seed, float* obs_d
         hipLaunchKernelGGL(d2d_reset_kernel<true>, grid, dim3(BLOCK), sizeof(d2d::Scn) * h->n_scn, (hipStream_t)stream, a);
     else
         hipLaunchKernelGGL(d2d_reset_kernel<false>, grid, dim3(BLOCK), 0, (hipStream_t)stream, a);
-    hipError_t e = hipGetLastError();
+    e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "d2d_reset launch");
+    if (fresh_mode(h) && (e = fresh_regen(h, (hipStream_t)stream)) != hipSuccess)
+        return hip_fail(e, "d2d_reset: fresh scenarios");
     // cached next-reset observations depend on the seed and the episode counters: drop and refill
     if ((e = rc_rebuild(h, (hipStream_t)stream)) != hipSuccess) return hip_fail(e, "d2d_reset: cache rebuild");
     h->reset_done = true;
@@ -460,6 +530,8 @@ int32_t d2d_step(d2d_t* h, const float* act_dev, float* obs_dev, float* rew_dev,
         hipLaunchKernelGGL((d2d_step_kernel<false, false>), grid, dim3(K1_THREADS), 0, (hipStream_t)stream, a);
     e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "d2d_step launch");
+    if (fresh_mode(h) && (e = fresh_regen(h, (hipStream_t)stream)) != hipSuccess)
+        return hip_fail(e, "d2d_step: fresh scenarios");
     if (D2D_FILL_PERIOD > 0 && h->cfg.auto_reset && ++h->n_steps % D2D_FILL_PERIOD == 0 &&
         (e = rc_fill(h, (hipStream_t)stream)) != hipSuccess)
         return hip_fail(e, "d2d_step: cache fill");
@@ -516,6 +588,8 @@ int32_t d2d_set_state(d2d_t* h, const double* state_dev, const int32_t* istate_d
                 hipSuccess)
             return hip_fail(e, "d2d_set_state");
     }
+    if (fresh_mode(h) && (e = fresh_regen(h, (hipStream_t)stream)) != hipSuccess)
+        return hip_fail(e, "d2d_set_state: fresh scenarios");
     if ((e = rc_rebuild(h, (hipStream_t)stream)) != hipSuccess) return hip_fail(e, "d2d_set_state: cache rebuild");
     h->reset_done = true;
     return D2D_OK;
@@ -523,7 +597,7 @@ int32_t d2d_set_state(d2d_t* h, const double* state_dev, const int32_t* istate_d
 
 int32_t d2d_refresh_pool(d2d_t* h, const d2d_scn* scns, int32_t n_scn) {
     if (!h || !scns) return fail(D2D_E_ARG, "d2d_refresh_pool: null handle/scenarios");
-    if (!h->cfg.scn_pool) return fail(D2D_E_ARG, "d2d_refresh_pool: pool mode only (cfg.scn_pool = 1)");
+    if (h->cfg.scn_pool != 1) return fail(D2D_E_ARG, "d2d_refresh_pool: pool mode only (cfg.scn_pool = 1)");
     if (h->n_scn <= 0) return fail(D2D_E_STATE, "d2d_refresh_pool: call d2d_set_scenarios first");
     if (n_scn != h->pool_n) return fail(D2D_E_ARG, "d2d_refresh_pool: n_scn must equal the pool size");
     std::vector<d2d::Scn> tab((size_t)n_scn);
@@ -549,6 +623,7 @@ int32_t d2d_refresh_pool(d2d_t* h, const d2d_scn* scns, int32_t n_scn) {
         return fail(D2D_E_STATE, "d2d_refresh_pool: " + std::to_string(busy) +
                                      " envs still run episodes from the pool before the previous refresh");
     if ((e = hipMemcpy(h->scn + half, tab.data(), P * sizeof(d2d::Scn), hipMemcpyHostToDevice)) != hipSuccess ||
+        (h->abi && (e = hipMemcpy(h->abi + half, scns, P * sizeof(d2d_scn), hipMemcpyHostToDevice)) != hipSuccess) ||
         (e = hipMemset(h->brt + half, 0, P * sizeof(d2d::BrTab))) != hipSuccess)
         return hip_fail(e, "d2d_refresh_pool: upload");
     hipLaunchKernelGGL(d2d_brtab_kernel, dim3((2 * n_scn + 63) / 64), dim3(64), 0, 0, h->scn + half, n_scn, h->brt + half);
@@ -557,6 +632,7 @@ int32_t d2d_refresh_pool(d2d_t* h, const d2d_scn* scns, int32_t n_scn) {
     if ((e = hipMemcpy(h->pool_dev, &half, sizeof(int32_t), hipMemcpyHostToDevice)) != hipSuccess)
         return hip_fail(e, "d2d_refresh_pool: switch");
     h->pool_base = half;
+    h->pool_valid |= (half == 0) ? 1 : 2;
     // cached next-episode observations were drawn from the old half: drop and refill now (a
     // captured graph replays d2d_step's kernels without the host-side rebuild check)
     if ((e = rc_rebuild(h, nullptr)) != hipSuccess || (e = hipDeviceSynchronize()) != hipSuccess)
@@ -575,8 +651,9 @@ int32_t d2d_get_env_scenarios(d2d_t* h, int32_t* env_scn_dev, void* stream) {
 
 int32_t d2d_set_env_scenarios(d2d_t* h, const int32_t* env_scn_dev, void* stream) {
     if (!h || !env_scn_dev) return fail(D2D_E_ARG, "d2d_set_env_scenarios: null handle/map");
-    if (!h->cfg.scn_pool)
-        return fail(D2D_E_ARG, "d2d_set_env_scenarios: pool mode only (change a static map with d2d_set_scenarios)");
+    if (h->cfg.scn_pool != 1)
+        return fail(D2D_E_ARG, "d2d_set_env_scenarios: pool mode only (a static map changes with d2d_set_scenarios; "
+                               "fresh curriculum slots are restored by d2d_fresh_recipes)");
     if (h->n_scn <= 0) return fail(D2D_E_STATE, "d2d_set_env_scenarios: call d2d_set_scenarios first");
     DeviceGuard g(h->device);
     const hipStream_t s = (hipStream_t)stream;
@@ -584,13 +661,153 @@ int32_t d2d_set_env_scenarios(d2d_t* h, const int32_t* env_scn_dev, void* stream
     hipError_t e = hipMemcpyAsync(m.data(), env_scn_dev, sizeof(int32_t) * m.size(), hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) return hip_fail(e, "d2d_set_env_scenarios: read map");
-    for (int32_t v : m)
+    for (int32_t v : m) {
         if (v < 0 || v >= h->n_scn) return fail(D2D_E_ARG, "d2d_set_env_scenarios: scenario index out of range");
+        if (!(h->pool_valid & (v >= h->pool_n ? 2 : 1)))
+            return fail(D2D_E_ARG, "d2d_set_env_scenarios: index into a pool half that holds no scenarios");
+    }
     if ((e = hipMemcpyAsync(h->env_scn, m.data(), sizeof(int32_t) * m.size(), hipMemcpyHostToDevice, s)) != hipSuccess ||
         (e = hipStreamSynchronize(s)) != hipSuccess)
         return hip_fail(e, "d2d_set_env_scenarios");
     return D2D_OK;
 }
+
+int32_t d2d_pool_state(d2d_t* h, int32_t* active_base, int32_t* valid_mask) {
+    if (!h || !active_base || !valid_mask) return fail(D2D_E_ARG, "d2d_pool_state: null argument");
+    if (h->cfg.scn_pool != 1 || h->n_scn <= 0) return fail(D2D_E_STATE, "d2d_pool_state: pool mode with scenarios only");
+    *active_base = h->pool_base;
+    *valid_mask = h->pool_valid;
+    return D2D_OK;
+}
+
+int32_t d2d_restore_pool(d2d_t* h, const d2d_scn* scns, int32_t n_total, int32_t active_base, int32_t valid_mask) {
+    if (!h || !scns) return fail(D2D_E_ARG, "d2d_restore_pool: null argument");
+    if (h->cfg.scn_pool != 1 || h->n_scn <= 0) return fail(D2D_E_STATE, "d2d_restore_pool: pool mode with scenarios only");
+    const int P = h->pool_n;
+    if (n_total != 2 * P) return fail(D2D_E_ARG, "d2d_restore_pool: n_total must be twice the pool size");
+    if (active_base != 0 && active_base != P) return fail(D2D_E_ARG, "d2d_restore_pool: active_base must be 0 or pool_n");
+    if (!(valid_mask & (active_base ? 2 : 1)) || (valid_mask & ~3))
+        return fail(D2D_E_ARG, "d2d_restore_pool: the active half must be valid");
+    std::vector<d2d::Scn> tab((size_t)n_total);
+    for (int k = 0; k < n_total; ++k) {
+        if (!(valid_mask & (k >= P ? 2 : 1))) continue;
+        const d2d_scn& sc = scns[k];
+        if (sc.n_wps < 3 || sc.n_wps > D2D_MAX_WPS || sc.n_circles < 0 || sc.n_circles > D2D_MAX_CIRCLES ||
+            !d2d::scn_build(sc, tab[k]))
+            return fail(D2D_E_ARG, "d2d_restore_pool: invalid scenario");
+    }
+    DeviceGuard g(h->device);
+    hipError_t e;
+    if ((e = hipDeviceSynchronize()) != hipSuccess) return hip_fail(e, "d2d_restore_pool: sync");
+    for (int half = 0; half < 2; ++half) {
+        const size_t o = (size_t)half * P;
+        if (!(valid_mask & (1 << half))) {
+            if ((e = hipMemset(h->scn + o, 0, P * sizeof(d2d::Scn))) != hipSuccess ||
+                (e = hipMemset(h->abi + o, 0, P * sizeof(d2d_scn))) != hipSuccess ||
+                (e = hipMemset(h->brt + o, 0, P * sizeof(d2d::BrTab))) != hipSuccess)
+                return hip_fail(e, "d2d_restore_pool: clear");
+            continue;
+        }
+        if ((e = hipMemcpy(h->scn + o, tab.data() + o, P * sizeof(d2d::Scn), hipMemcpyHostToDevice)) != hipSuccess ||
+            (e = hipMemcpy(h->abi + o, scns + o, P * sizeof(d2d_scn), hipMemcpyHostToDevice)) != hipSuccess ||
+            (e = hipMemset(h->brt + o, 0, P * sizeof(d2d::BrTab))) != hipSuccess)
+            return hip_fail(e, "d2d_restore_pool: upload");
+        hipLaunchKernelGGL(d2d_brtab_kernel, dim3((2 * P + 63) / 64), dim3(64), 0, 0, h->scn + o, P, h->brt + o);
+        if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "d2d_restore_pool: d2d_brtab_kernel");
+    }
+    if ((e = hipMemcpy(h->pool_dev, &active_base, sizeof(int32_t), hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipDeviceSynchronize()) != hipSuccess)
+        return hip_fail(e, "d2d_restore_pool: switch");
+    h->pool_base = active_base;
+    h->pool_valid = valid_mask;
+    h->rc_dirty = true;
+    return D2D_OK;
+}
+
+int32_t d2d_set_curriculum(d2d_t* h, const d2d_curriculum* c) {
+    if (!h || !c) return fail(D2D_E_ARG, "d2d_set_curriculum: null argument");
+    if (!fresh_mode(h)) return fail(D2D_E_ARG, "d2d_set_curriculum: needs cfg.scn_pool = 2 (fresh curriculum)");
+    if (c->n_wps < 4 || c->n_wps > D2D_MAX_WPS) return fail(D2D_E_ARG, "d2d_set_curriculum: n_wps out of range [4, D2D_MAX_WPS]");
+    if (!(c->segment_length > 0.001)) return fail(D2D_E_ARG, "d2d_set_curriculum: segment_length must exceed 0.001");
+    if (c->stage < 0 || c->stage > 5) return fail(D2D_E_ARG, "d2d_set_curriculum: stage must be 0 (schedule) or 1..5");
+    if (c->random_path_spawn && (c->corner_lo < 1 || c->corner_hi > 4 || c->corner_lo > c->corner_hi))
+        return fail(D2D_E_ARG, "d2d_set_curriculum: spawn corners must satisfy 1 <= lo <= hi <= 4");
+    if (!(c->envs_total >= 1.0)) return fail(D2D_E_ARG, "d2d_set_curriculum: envs_total must be >= 1");
+    DeviceGuard g(h->device);
+    hipError_t e;
+    const size_t S = 2 * (size_t)h->n;
+    if (h->n_scn != (int)S || !h->scn_tag) {
+        if ((e = hipDeviceSynchronize()) != hipSuccess) return hip_fail(e, "d2d_set_curriculum: sync");
+        for (void* p : {(void*)h->scn, (void*)h->brt, (void*)h->abi, (void*)h->scn_tag, (void*)h->gclk})
+            if (p) (void)hipFree(p);
+        h->scn = nullptr;
+        h->brt = nullptr;
+        h->abi = nullptr;
+        h->scn_tag = nullptr;
+        h->gclk = nullptr;
+        h->n_scn = 0;
+        if ((e = hipMalloc(&h->scn, sizeof(d2d::Scn) * S)) != hipSuccess ||
+            (e = hipMalloc(&h->brt, sizeof(d2d::BrTab) * S)) != hipSuccess ||
+            (e = hipMalloc(&h->abi, sizeof(d2d_scn) * S)) != hipSuccess ||
+            (e = hipMalloc(&h->scn_tag, sizeof(int32_t) * S)) != hipSuccess ||
+            (e = hipMalloc(&h->gclk, sizeof(int64_t) * S)) != hipSuccess ||
+            (e = hipMemset(h->scn, 0, sizeof(d2d::Scn) * S)) != hipSuccess ||
+            (e = hipMemset(h->brt, 0, sizeof(d2d::BrTab) * S)) != hipSuccess ||
+            (e = hipMemset(h->abi, 0, sizeof(d2d_scn) * S)) != hipSuccess ||
+            (e = hipMemset(h->gclk, 0, sizeof(int64_t) * S)) != hipSuccess)
+            return hip_fail(e, "d2d_set_curriculum: hipMalloc");
+    }
+    if ((e = hipMemset(h->scn_tag, 0xFF, sizeof(int32_t) * S)) != hipSuccess ||
+        (e = hipDeviceSynchronize()) != hipSuccess)
+        return hip_fail(e, "d2d_set_curriculum: slots");
+    h->cur = *c;
+    h->n_scn = (int)S;
+    h->pool_n = 0;
+    h->fresh_seeded = false;
+    h->reset_done = false;  // every env starts over on the new curriculum (d2d_reset)
+    h->rc_dirty = true;
+    h->generation += 1;
+    return D2D_OK;
+}
+
+int32_t d2d_fresh_recipes(d2d_t* h, int32_t* keys, int64_t* clocks, int64_t* clock, int32_t set) {
+    if (!h || !keys || !clocks || !clock) return fail(D2D_E_ARG, "d2d_fresh_recipes: null argument");
+    if (!fresh_mode(h) || !h->scn_tag) return fail(D2D_E_STATE, "d2d_fresh_recipes: call d2d_set_curriculum first");
+    DeviceGuard g(h->device);
+    hipError_t e;
+    const size_t S = 2 * (size_t)h->n;
+    if ((e = hipDeviceSynchronize()) != hipSuccess) return hip_fail(e, "d2d_fresh_recipes: sync");
+    if (!set) {
+        if ((e = hipMemcpy(keys, h->scn_tag, sizeof(int32_t) * S, hipMemcpyDeviceToHost)) != hipSuccess ||
+            (e = hipMemcpy(clocks, h->gclk, sizeof(int64_t) * S, hipMemcpyDeviceToHost)) != hipSuccess ||
+            (e = hipMemcpy(clock, h->clock, sizeof(int64_t), hipMemcpyDeviceToHost)) != hipSuccess)
+            return hip_fail(e, "d2d_fresh_recipes: read");
+        return D2D_OK;
+    }
+    if (!h->fresh_seeded) return fail(D2D_E_STATE, "d2d_fresh_recipes: call d2d_reset (the seed) before restoring");
+    if ((e = hipMemcpy(h->scn_tag, keys, sizeof(int32_t) * S, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemcpy(h->gclk, clocks, sizeof(int64_t) * S, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemcpy(h->clock, clock, sizeof(int64_t), hipMemcpyHostToDevice)) != hipSuccess)
+        return hip_fail(e, "d2d_fresh_recipes: write");
+    if ((e = fresh_regen(h, nullptr, true)) != hipSuccess || (e = hipDeviceSynchronize()) != hipSuccess)
+        return hip_fail(e, "d2d_fresh_recipes: regenerate");
+    h->rc_dirty = true;
+    return D2D_OK;
+}
+
+int32_t d2d_get_scenario_table(d2d_t* h, int32_t first, int32_t count, d2d_scn* out) {
+    if (!h || !out || first < 0 || count < 0) return fail(D2D_E_ARG, "d2d_get_scenario_table: bad arguments");
+    if (!h->abi) return fail(D2D_E_STATE, "d2d_get_scenario_table: pool or fresh curriculum mode with scenarios only");
+    if (first + count > h->n_scn) return fail(D2D_E_ARG, "d2d_get_scenario_table: range beyond the table");
+    DeviceGuard g(h->device);
+    hipError_t e;
+    if ((e = hipDeviceSynchronize()) != hipSuccess ||
+        (e = hipMemcpy(out, h->abi + first, sizeof(d2d_scn) * (size_t)count, hipMemcpyDeviceToHost)) != hipSuccess)
+        return hip_fail(e, "d2d_get_scenario_table");
+    return D2D_OK;
+}
+
+int32_t d2d_generation(const d2d_t* h) { return h ? h->generation : -1; }
 
 int32_t d2d_episode_stats(d2d_t* h, double* out_dev, int32_t clear, void* stream) {
     if (!h || !out_dev) return fail(D2D_E_ARG, "d2d_episode_stats: null handle/out");

@@ -29,6 +29,7 @@
 // K4 d2d_fill_kernel: fills the auto-reset observation cache (the envs that need it compacted,
 // four waves per 64 of them: fill_split).
 #pragma once
+#include "d2d_curriculum.h"
 #include "d2d_device.h"
 
 namespace d2dk {
@@ -101,6 +102,10 @@ struct StepArgs {
     // stay indexed by env id.  Without the map slot == env.
     const int32_t* lane_env;  // [ns] slot -> env
     const int32_t* wg_scn;    // [ns / 64]  (-(s + 2): scenarios s and s + 1; -1: three or more)
+    // fresh curriculum (cfg.scn_pool == 2): the episode key each scenario slot holds (K4 fills a
+    // reset observation only once its scenario exists) and the step clock K1 advances
+    const int32_t* scn_tag;   // [2 n]
+    int64_t* clock;           // [1]
 };
 
 // Auto-reset observation cache.  The observation an env gets when it auto-resets depends only on
@@ -285,7 +290,11 @@ __device__ __forceinline__ bool flag_seen(const uint32_t& f) {
 __device__ __forceinline__ int pool_scenario(const StepArgs& a, int j, uint32_t ep) {
     return *a.pool_base + (a.pool_n > 1 ? pool_pick(a.seed, (uint32_t)a.cfg.env_id_base + (uint32_t)j, ep, a.pool_n) : 0);
 }
+// fresh curriculum: env j's two scenario slots alternate by episode key (d2d_fresh_kernel writes
+// the slot of key ep -- the episode the next reset starts -- one step ahead)
+__device__ __forceinline__ int fresh_slot(int j, uint32_t ep) { return 2 * j + (int)(ep & 1u); }
 __device__ __forceinline__ int next_scenario(const StepArgs& a, int j, uint32_t ep) {
+    if (a.cfg.scn_pool == 2) return fresh_slot(j, ep);
     if (a.cfg.scn_pool) return pool_scenario(a, j, ep);
     if (a.n_scn <= 1) return 0;
     return a.env_scn[j];
@@ -350,6 +359,8 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, Scn* s_scn, K1Shared&
     if (D2D_FILL_EVERY > 1 && wg == 0 && threadIdx.x == 0 && a.fill_ctl)  // K4's tick: publish its next value
         __hip_atomic_store(&a.fill_ctl[0], __hip_atomic_load(&a.fill_ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (wg == 0 && threadIdx.x == 0 && a.clock)  // the step clock (fresh curriculum stage schedule)
+        __hip_atomic_fetch_add(a.clock, (int64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int ws = (GRP && LDS) ? a.wg_scn[wg] : 0;
     const int s0 = ws >= 0 ? ws : -ws - 2;          // a straddling group: its two scenarios s0, s0 + 1
     const int ncopy = (GRP && LDS) ? (ws >= 0 ? 1 : 2) : a.n_scn;
@@ -880,7 +891,7 @@ __global__ __launch_bounds__(BLOCK) void d2d_reset_kernel(StepArgs a) {
     const int n = a.ns;
     int si = (a.env_scn && a.n_scn > 1) ? a.env_scn[ie] : 0;
     if (a.cfg.scn_pool) {
-        si = pool_scenario(a, ie, (uint32_t)fld(a.ist, D2D_I_EPISODE, n, i));
+        si = next_scenario(a, ie, (uint32_t)fld(a.ist, D2D_I_EPISODE, n, i));
         a.env_scn[ie] = si;
     }
     const Scn& s = scns[si];
@@ -1031,7 +1042,9 @@ __device__ __forceinline__ void fill_work(const StepArgs& a) {
     const bool need = ((int)threadIdx.x < D2D_RC_SLOTS * spb) && (i0 < n) &&
                       (!a.lane_env || a.lane_env[i0] >= 0) && [&] {
                           const int32_t key = fld(a.ist, D2D_I_EPISODE, n, i0) + which;
-                          return a.rc_tag[rc_entry(a, i0, (uint32_t)key)] != key;
+                          // fresh curriculum: only once the scenario of that episode exists
+                          return a.rc_tag[rc_entry(a, i0, (uint32_t)key)] != key &&
+                                 (a.cfg.scn_pool != 2 || a.scn_tag[fresh_slot(i0, (uint32_t)key)] == key);
                       }();
     int i = i0, total = 0;
     if (!D2D_FILL_COMPACT) {
@@ -1103,6 +1116,57 @@ __global__ __launch_bounds__(BLOCK) void d2d_fill_kernel(StepArgs a) {
             __hip_atomic_store(&a.fill_ctl[1], tick + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (run) fill_work<LDS>(a);
+}
+
+// ------------------------------------------------------------------------ fresh curriculum (K5)
+// Scenario generation for the fresh curriculum (d2d_curriculum.h), one thread per env: the scenario
+// of the episode env i's next reset starts (key = its episode counter) goes into slot 2 i + (key & 1)
+// unless that slot already holds it; the other slot holds the running episode's.  Launched after
+// every K1 (the slot is needed one step later at the earliest), before and after K2, and after
+// d2d_set_state; restore = 1 regenerates every slot from its recipe (key, clock) instead.
+struct FreshArgs {
+    int n;                   // envs (pool modes keep the identity slot layout: slot == env)
+    const int32_t* ist;      // [NISTATE][n] (episode counters)
+    int32_t* env_scn;        // [n] the running episode's slot, 2 i + ((ep - 1) & 1)
+    d2d_curriculum cur;
+    double W, H;
+    uint64_t seed;
+    uint32_t env_id_base;
+    d2d_scn* abi;            // [2 n] ABI records (read back for the oracle)
+    Scn* scn;                // [2 n]
+    BrTab* brt;              // [2 n] golden-march tables
+    int32_t* tag;            // [2 n] episode key of each slot (-1: empty)
+    int64_t* gclk;           // [2 n] clock at generation
+    const int64_t* clock;    // the step clock (K1 advances it)
+    int restore;
+};
+__global__ __launch_bounds__(64) void d2d_fresh_kernel(FreshArgs f) {
+    const int t = blockIdx.x * 64 + threadIdx.x;
+    int slot, key, i;
+    int64_t clk;
+    if (f.restore) {
+        if (t >= 2 * f.n) return;
+        slot = t;
+        key = f.tag[slot];
+        if (key < 0) return;
+        i = slot >> 1;
+        clk = f.gclk[slot];
+    } else {
+        if (t >= f.n) return;
+        i = t;
+        const int32_t ep = f.ist[(size_t)D2D_I_EPISODE * f.n + i];
+        f.env_scn[i] = fresh_slot(i, (uint32_t)(ep - 1));
+        key = ep;
+        slot = fresh_slot(i, (uint32_t)key);
+        if (f.tag[slot] == key) return;
+        clk = *f.clock;
+    }
+    const double sim = f.cur.sim_num0 + (double)clk * f.cur.envs_total;
+    gen_curriculum(f.cur, f.W, f.H, f.seed, f.env_id_base + (uint32_t)i, (uint32_t)key, sim, f.abi[slot], f.scn[slot]);
+    brtab_build(f.scn[slot], 0, f.brt[slot]);
+    brtab_build(f.scn[slot], 1, f.brt[slot]);
+    f.gclk[slot] = clk;
+    f.tag[slot] = key;
 }
 
 // ------------------------------------------------------------------------- golden-march tables

@@ -64,7 +64,7 @@ def build_scenarios(kwargs: dict) -> list[Scenario]:
             stage, chance = spec, None
         else:
             stage, chance = stage_for_sim_num(int(kwargs.get("sim_num", 0)))
-        return curriculum_pool(stage, kwargs, int(kwargs.get("curriculum_pool", 1024)),
+        return curriculum_pool(stage, kwargs, int(kwargs.get("curriculum_pool") or 1024),
                                seed=int(kwargs.get("curriculum_seed", 0)), spawn_chance=chance)
     if isinstance(spec, (str, Scenario)):
         spec = [spec]
@@ -87,6 +87,29 @@ def is_curriculum(kwargs: dict) -> bool:
     return kwargs.get("mode") == "curriculum" or (isinstance(spec, str) and spec in CURRICULUM_STAGES)
 
 
+def is_fresh_curriculum(kwargs: dict) -> bool:
+    """Curriculum episodes on scenarios generated on the device, one per reset (the default; the
+    reference's behaviour).  ``curriculum_pool=P`` selects the host-generated pool of P instead."""
+    return is_curriculum(kwargs) and kwargs.get("curriculum_pool") is None
+
+
+def make_curriculum(kwargs: dict, envs_total: int) -> abi.D2DCurriculum:
+    """The device generator's parameters from the reference kwargs: stage from scenario='stage_k'
+    (else the sim_num schedule from ``sim_num``), n_wps, path_segment_length, random_path_spawn,
+    spawn_corners (rl_config.py:10-44)."""
+    c = abi.D2DCurriculum()
+    spec = kwargs.get("scenario")
+    c.stage = int(spec[-1]) if isinstance(spec, str) and spec in CURRICULUM_STAGES else 0
+    c.n_wps = int(kwargs["n_wps"])
+    c.segment_length = float(kwargs["path_segment_length"])
+    c.random_path_spawn = 1 if kwargs.get("random_path_spawn", True) is True else 0
+    lo, hi = kwargs.get("spawn_corners", (1, 4))
+    c.corner_lo, c.corner_hi = int(lo), int(hi)
+    c.sim_num0 = float(kwargs.get("sim_num", 0))
+    c.envs_total = float(envs_total)
+    return c
+
+
 class Drone2dVecEnv:
     """``num_envs`` independent Drone2dEnv copies stepping together on one GPU.
 
@@ -97,17 +120,22 @@ class Drone2dVecEnv:
       env_id_offset   global id of env 0 (multi-GPU shards keep per-env RNG streams global)
       auto_reset      SB3 VecEnv semantics (done envs are reset inside the step kernel)
       timeup_truncates  report time-up as truncation instead of termination (reference: False)
-    Curriculum (``mode='curriculum'`` or ``scenario='stage_k'``): a pool of
-    ``kwargs['curriculum_pool']`` (default 1024) reference-identical curriculum resets is generated
-    from ``kwargs['curriculum_seed']`` for the stage (explicit, or from ``kwargs['sim_num']`` by the
-    reference's schedule) and every episode of every env draws one entry (drone2d_amd.curriculum).
-    ``set_curriculum(stage=..., sim_num=...)`` regenerates the pool and resets all envs.
+    Curriculum (``mode='curriculum'`` or ``scenario='stage_k'``), two forms:
+      fresh (default)  every reset runs on a scenario generated on the device for that episode
+                       alone (d2d_set_curriculum): the reference's behaviour.  The stage is
+                       explicit or follows the reference's sim_num schedule with
+                       sim_num = kwargs['sim_num'] + steps x ``envs_total`` (all ranks' envs;
+                       default num_envs), advanced on the device with no host call.
+      pool             ``kwargs['curriculum_pool'] = P``: P reference-identical resets generated
+                       on the host from ``kwargs['curriculum_seed']`` (drone2d_amd.curriculum);
+                       every episode draws one entry; ``refresh_curriculum`` swaps in a new pool.
+    ``set_curriculum(stage=..., sim_num=...)`` switches the stage / schedule and resets all envs.
     """
 
     def __init__(self, num_envs: int, device=None, seed: int = 0, *,
                  env_scenario: Sequence[int] | None = None, auto_reset: bool = True,
                  timeup_truncates: bool = False, with_info: bool = True, env_id_offset: int = 0,
-                 native_lib: str | None = None, **kwargs):
+                 native_lib: str | None = None, envs_total: int | None = None, **kwargs):
         self.kwargs = dict(kwargs)
         self._lib = load(native_lib)  # native_lib: alternative build (diagnostics only)
         if device is None:
@@ -120,9 +148,11 @@ class Drone2dVecEnv:
         self.num_envs = int(num_envs)
         self.cfg = make_cfg(self.kwargs, auto_reset=auto_reset, timeup_truncates=timeup_truncates,
                             env_id_base=env_id_offset)
-        self.scenarios = build_scenarios(self.kwargs)
-        # curriculum: every reset draws a fresh pool entry (d2d_cfg.scn_pool)
-        self.cfg.scn_pool = 1 if is_curriculum(self.kwargs) else 0
+        self.envs_total = int(envs_total) if envs_total is not None else self.num_envs
+        self.fresh = is_fresh_curriculum(self.kwargs)
+        self.scenarios = [] if self.fresh else build_scenarios(self.kwargs)
+        # curriculum: every reset draws a fresh device-generated scenario (2) or a pool entry (1)
+        self.cfg.scn_pool = (2 if self.fresh else 1) if is_curriculum(self.kwargs) else 0
         self.seed_value = int(seed)
         self.with_info = with_info
         self.action_space = _make_box(-np.ones(2), np.ones(2))
@@ -147,6 +177,11 @@ class Drone2dVecEnv:
 
     # ------------------------------------------------------------------ plumbing
     def _upload_scenarios(self, env_scenario=None):
+        if self.fresh:
+            self.curriculum = make_curriculum(self.kwargs, self.envs_total)
+            self.env_scenario = 2 * np.arange(self.num_envs, dtype=np.int32)
+            check(self._lib.d2d_set_curriculum(self._h, C.byref(self.curriculum)), "d2d_set_curriculum")
+            return
         n_scn = len(self.scenarios)
         arr = (abi.D2DScn * n_scn)(*[s.to_c() for s in self.scenarios])
         if env_scenario is None:
@@ -170,11 +205,11 @@ class Drone2dVecEnv:
             self.kwargs["scenario"] = "curriculum"
             self.kwargs["sim_num"] = int(sim_num)
         self.kwargs["mode"] = "curriculum"
-        if pool is not None:
+        if pool is not None and not self.fresh:
             self.kwargs["curriculum_pool"] = int(pool)
         if seed is not None:
             self.kwargs["curriculum_seed"] = int(seed)
-        self.scenarios = build_scenarios(self.kwargs)
+        self.scenarios = [] if self.fresh else build_scenarios(self.kwargs)
         torch.cuda.synchronize(self.device)
         self._upload_scenarios()
         return self.reset()
@@ -187,8 +222,9 @@ class Drone2dVecEnv:
         stage at each env's next reset, drone_2d_env.py:76-86).  Refresh at most once per
         ``n_steps`` steps (the library refuses while an env still runs an episode from the pool
         before the previous refresh)."""
-        if not self.cfg.scn_pool:
-            raise ValueError("refresh_curriculum needs an env created in curriculum mode (mode='curriculum')")
+        if self.cfg.scn_pool != 1:
+            raise ValueError("refresh_curriculum needs a curriculum pool (mode='curriculum', curriculum_pool=P); "
+                             "the fresh curriculum generates every episode's scenario itself")
         kw = dict(self.kwargs, mode="curriculum")
         if stage is not None:
             kw["scenario"] = stage
@@ -285,19 +321,73 @@ class Drone2dVecEnv:
             raise ValueError("env_scn must have shape [num_envs]")
         check(self._lib.d2d_set_env_scenarios(self._h, self._ptr(es), self._stream()), "d2d_set_env_scenarios")
 
+    @property
+    def generation(self) -> int:
+        """Changes whenever the library re-allocates what a captured step graph points at
+        (set_scenarios / set_curriculum): holders of a captured graph re-capture it."""
+        return int(self._lib.d2d_generation(self._h))
+
+    def scenario_table(self, first: int = 0, count: int | None = None):
+        """ABI records (abi.D2DScn array) of scenario-table slots [first, first + count): the pool's two
+        halves, or in the fresh curriculum env i's slots 2 i, 2 i + 1 (the oracle replays them)."""
+        total = 2 * self.num_envs if self.fresh else 2 * len(self.scenarios)
+        count = total - first if count is None else count
+        out = (abi.D2DScn * count)()
+        check(self._lib.d2d_get_scenario_table(self._h, first, count, out), "d2d_get_scenario_table")
+        return out
+
+    def fresh_recipes(self):
+        """Fresh curriculum: (keys int32[2n], clocks int64[2n], clock) -- every scenario slot's episode
+        key and generation clock, and the step clock (what a checkpoint needs to regenerate them)."""
+        k = np.zeros(2 * self.num_envs, np.int32)
+        c = np.zeros(2 * self.num_envs, np.int64)
+        t = C.c_int64()
+        check(self._lib.d2d_fresh_recipes(self._h, k.ctypes.data_as(C.c_void_p), c.ctypes.data_as(C.c_void_p),
+                                          C.byref(t), 0), "d2d_fresh_recipes")
+        return k, c, int(t.value)
+
     def state_dict(self) -> dict:
         """Checkpoint of the running batch: physics/bookkeeping state, per-env scenario indices and
-        the spawn seed (the reference has no resume path)."""
+        the spawn seed (the reference has no resume path).  Curriculum pool:
+        both pool halves' scenarios and which half resets draw from; fresh curriculum: every
+        scenario slot's recipe (episode key, clock) and the step clock."""
         st, ist = self.get_state()
-        return {"state": st, "istate": ist, "env_scn": self.get_env_scenarios(), "seed": self.seed_value}
+        sd = {"state": st, "istate": ist, "env_scn": self.get_env_scenarios(), "seed": self.seed_value}
+        if self.cfg.scn_pool == 1:
+            base, valid = C.c_int32(), C.c_int32()
+            check(self._lib.d2d_pool_state(self._h, C.byref(base), C.byref(valid)), "d2d_pool_state")
+            recs = self.scenario_table()
+            sd["pool"] = {"records": np.frombuffer(bytes(recs), np.uint8).copy(), "active_base": int(base.value),
+                          "valid_mask": int(valid.value), "size": len(self.scenarios)}
+        elif self.cfg.scn_pool == 2:
+            k, c, t = self.fresh_recipes()
+            sd["fresh"] = {"keys": k, "clocks": c, "clock": t}
+        return sd
 
     def load_state_dict(self, sd: dict):
-        """Restore a ``state_dict()`` into a batch built with the same kwargs (and, in pool mode,
-        the same curriculum pool): episodes continue exactly where they were."""
+        """Restore a ``state_dict()`` into a batch built with the same kwargs: episodes continue
+        exactly where they were (pool mode: on the saved pool, whatever this batch's own pool is)."""
         self.seed_value = int(sd["seed"])
         self.reset()  # installs the seed for later auto-resets; the state is overwritten below
-        if self.cfg.scn_pool:
+        if self.cfg.scn_pool == 1:
+            pool = sd.get("pool")
+            if pool is None:
+                raise ValueError("pool-mode checkpoint without its pool (saved by an older version)")
+            if int(pool["size"]) != len(self.scenarios):
+                raise ValueError("checkpoint pool size differs from this batch's curriculum_pool")
+            recs = (abi.D2DScn * (2 * int(pool["size"]))).from_buffer_copy(np.asarray(pool["records"]).tobytes())
+            check(self._lib.d2d_restore_pool(self._h, recs, len(recs), int(pool["active_base"]),
+                                             int(pool["valid_mask"])), "d2d_restore_pool")
             self.set_env_scenarios(sd["env_scn"])
+        elif self.cfg.scn_pool == 2:
+            f = sd["fresh"]
+            k = np.ascontiguousarray(f["keys"], np.int32)
+            c = np.ascontiguousarray(f["clocks"], np.int64)
+            if k.shape != (2 * self.num_envs,):
+                raise ValueError("checkpoint has a different number of envs")
+            t = C.c_int64(int(f["clock"]))
+            check(self._lib.d2d_fresh_recipes(self._h, k.ctypes.data_as(C.c_void_p), c.ctypes.data_as(C.c_void_p),
+                                              C.byref(t), 1), "d2d_fresh_recipes")
         elif not torch.equal(torch.as_tensor(sd["env_scn"]).cpu(), self.get_env_scenarios().cpu()):
             raise ValueError("checkpoint env -> scenario map differs from this batch's (static map)")
         self.set_state(sd["state"], sd["istate"])

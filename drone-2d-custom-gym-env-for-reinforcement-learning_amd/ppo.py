@@ -470,6 +470,7 @@ class PPO:
         self._ro = None          # rollout buffers (_alloc_rollout)
         self._ro_graph = None    # the captured rollout (GPU)
         self._ro_warm = False
+        self._ro_gen = None      # the env's generation the rollout graph was captured against
 
     # ------------------------------------------------------------------ rollout
     def _alloc_rollout(self):
@@ -527,6 +528,16 @@ class PPO:
 
     def collect_rollouts(self) -> dict:
         T, N = self.cfg.n_steps, self.n_envs
+        gen = getattr(self.venv, "generation", None)
+        if self._ro is not None and gen != self._ro_gen:
+            # the env re-allocated its scenario tables (set_curriculum / set_scenarios): a captured
+            # rollout would replay against freed memory, and the envs were reset -- drop the graph
+            # and start the next rollout from a reset
+            self._ro_graph = None
+            self._ro_warm = False
+            self._ro["obs"][0].copy_(self.venv.reset().to(self.device))
+            self._ro["start0"].fill_(True)
+        self._ro_gen = gen
         if self._ro is None:
             self._alloc_rollout()
             self._ro["obs"][0].copy_(self.venv.reset().to(self.device))
@@ -535,7 +546,10 @@ class PPO:
         R["fin"].zero_()
         R["ret"].zero_()
         torch.randn(R["noise"].shape, generator=self.gen, device=self.device, out=R["noise"])
-        graph_ok = self.cfg.graph and self.device.type == "cuda" and T % 2 == 0
+        # capture only whole fill periods: d2d_step launches the reset-cache fill after every 16th
+        # step, decided on the host, so a graph of another length would bake in a fill on every
+        # replay or on none (still correct through the synchronous reset path, but slower)
+        graph_ok = self.cfg.graph and self.device.type == "cuda" and T % 16 == 0
         if graph_ok and self._ro_graph is None and self._ro_warm:
             # second rollout: capture (the first one ran eagerly: library and allocator warm-up);
             # T even, so the env's double-buffered outputs are back at their start after a replay

@@ -68,9 +68,11 @@ def allreduce_stats(stats: torch.Tensor, group=None) -> torch.Tensor:
 def make_shard_venv(n_total: int, rank: int, world: int, *, device=None, seed: int = 0, **kwargs):
     """This rank's Drone2dVecEnv of a global batch of n_total envs (scenario i mod n_scenarios
     for global env i, as one unsharded batch would assign it)."""
-    from .env import Drone2dVecEnv, build_scenarios
+    from .env import Drone2dVecEnv, build_scenarios, is_fresh_curriculum
 
     offset, count = shard_range(n_total, world, rank)
+    if is_fresh_curriculum(kwargs):  # per-episode device scenarios; the stage clock counts all ranks' envs
+        return Drone2dVecEnv(count, device=device, seed=seed, env_id_offset=offset, envs_total=n_total, **kwargs)
     es = shard_env_scenario(global_env_scenario(n_total, len(build_scenarios(kwargs))), offset, count)
     return Drone2dVecEnv(count, device=device, seed=seed, env_id_offset=offset, env_scenario=es, **kwargs)
 

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define D2D_ABI_VERSION 3
+#define D2D_ABI_VERSION 4
 
 #define D2D_MAX_WPS 16                    /* largest test path: 'large' has 14 waypoints   */
 #define D2D_MAX_SEGS (D2D_MAX_WPS - 2)    /* QPMI2D fits n_wps-2 quadratics (predef_path.py:34) */
@@ -119,8 +119,24 @@ typedef struct d2d_cfg {
     int32_t scn_pool;                  /* 0: env i always runs scenario env_scn[i] (test mode);
                                           1: curriculum pool -- at every reset env i draws its next
                                           scenario uniformly from the n_scn uploaded, from its
-                                          Philox stream (counter (gid, episode, 2, 0))     */
+                                          Philox stream (counter (gid, episode, 2, 0));
+                                          2: fresh curriculum -- every reset runs on a scenario
+                                          generated on the device for that episode alone
+                                          (d2d_set_curriculum), as the reference's reset does */
 } d2d_cfg;
+
+/* Curriculum generator parameters (cfg.scn_pool = 2): the kwargs the reference's curriculum reset
+ * reads (rl_config.py:10-44; drone_2d_env.py:199-215, 318-372) plus the stage clock. */
+typedef struct d2d_curriculum {
+    int32_t stage;              /* 1..5: a fixed stage (scenario='stage_k'); 0: the sim_num schedule */
+    int32_t n_wps;              /* n_wps                                                         */
+    double segment_length;      /* path_segment_length                                           */
+    int32_t random_path_spawn;  /* 1: corner from spawn_corners (random.randint), 0: 'DR'        */
+    int32_t corner_lo, corner_hi;  /* spawn_corners: 1 DL, 2 DR, 3 UL, 4 UR                     */
+    int32_t pad;
+    double sim_num0;            /* schedule: sim_num = sim_num0 + clock * envs_total, clock = the  */
+    double envs_total;          /* number of d2d_step calls so far (all ranks' envs: envs_total)  */
+} d2d_curriculum;
 
 /* One scenario: a QPMI2D path + circle obstacles + spawn distribution.
  * Built on the host once (test_scenarios.py:169-246, predef_path.py:20-50). */
@@ -195,6 +211,35 @@ int32_t d2d_refresh_pool(d2d_t* h, const d2d_scn* scns, int32_t n_scn);
  * re-lays the state out) and synchronises `stream` to range-check the indices on the host. */
 int32_t d2d_get_env_scenarios(d2d_t* h, int32_t* env_scn_dev, void* stream);
 int32_t d2d_set_env_scenarios(d2d_t* h, const int32_t* env_scn_dev, void* stream);
+/* Pool-mode checkpoints: *active_base = the table index resets draw from (0 or pool_n), *valid_mask
+ * bit h = half h holds uploaded scenarios (d2d_set_env_scenarios rejects indices into an empty
+ * half).  d2d_restore_pool writes both halves (2 * pool_n ABI records, read back with
+ * d2d_get_scenario_table; a half whose bit is clear in valid_mask stays empty) and selects the
+ * active half, so a restored batch draws and runs exactly what the saved one did.  Synchronises. */
+int32_t d2d_pool_state(d2d_t* h, int32_t* active_base, int32_t* valid_mask);
+int32_t d2d_restore_pool(d2d_t* h, const d2d_scn* scns, int32_t n_total, int32_t active_base, int32_t valid_mask);
+
+/* Fresh curriculum (cfg.scn_pool = 2), the reference's curriculum reset: the episode that env i
+ * starts with episode counter k runs on scenario G(seed, gid i, k, stage) -- a random 12-waypoint
+ * path (predef_path.py:307-363) with its QPMI2D fit (:20-50), the stage's obstacles
+ * (drone_2d_env.py:318-372, obstacles.py:58-89) and spawn -- generated on the device from a Philox
+ * stream keyed by (seed, gid, k) one step ahead of the reset that needs it (after every d2d_step
+ * and around d2d_reset), with the stage of the clock at generation time.  Replaces
+ * d2d_set_scenarios in this mode (allocates 2 scenario slots per env; captured graphs must be
+ * recaptured after it, d2d_generation changes).  */
+int32_t d2d_set_curriculum(d2d_t* h, const d2d_curriculum* c);
+/* Checkpointing in fresh mode: each env's two scenario slots are described by their recipe
+ * (episode key, -1 = empty; clock at generation); get copies them to host int32[2 n] / int64[2 n]
+ * (slot 2 i + (key & 1) of env i) and the current clock to *clock; set uploads them (and the clock)
+ * and regenerates every slot from its recipe, so restored episodes continue on their own paths.
+ * Synchronises the device. */
+int32_t d2d_fresh_recipes(d2d_t* h, int32_t* keys, int64_t* clocks, int64_t* clock, int32_t set);
+/* Copy scenario slots [first, first + count) of the device table (pool or fresh mode) to the host as
+ * ABI records (parity tests hand them to the CPU oracle).  Synchronises the device. */
+int32_t d2d_get_scenario_table(d2d_t* h, int32_t first, int32_t count, d2d_scn* out);
+/* Bumped by every call that frees or re-allocates what a captured step graph points at
+ * (d2d_set_scenarios, d2d_set_curriculum): a caller holding a captured graph re-captures it. */
+int32_t d2d_generation(const d2d_t* h);
 
 /* Reduce the per-env finished-episode accumulators into out_dev (float64 [D2D_NSTATS]) with a
  * fixed-order (bitwise reproducible) block reduction; clear != 0 zeroes the accumulators after. */

@@ -22,6 +22,12 @@ int32_t d2dcpu_step_mt(d2dcpu_t* h, const float* act, float* obs, float* rew, ui
 int32_t d2dcpu_get_state(const d2dcpu_t* h, double* state, int32_t* istate);
 int32_t d2dcpu_set_state(d2dcpu_t* h, const double* state, const int32_t* istate);
 int32_t d2dcpu_episode_stats(d2dcpu_t* h, double* out, int32_t clear);
+/* fresh curriculum (cfg.scn_pool = 2): the device protocol of d2d_set_curriculum / d2d_fresh_recipes */
+int32_t d2dcpu_set_curriculum(d2dcpu_t* h, const d2d_curriculum* c);
+int32_t d2dcpu_fresh_recipes(d2dcpu_t* h, int32_t* keys, int64_t* clocks, int64_t* clock, int32_t set);
+int32_t d2dcpu_get_scenario_table(const d2dcpu_t* h, int32_t first, int32_t count, d2d_scn* out);
+void d2dcpu_gen_curriculum(const d2d_curriculum* c, double W, double H, uint64_t seed, uint32_t gid,
+                           uint32_t key, double sim, d2d_scn* s);
 
 /* single-function probes */
 void d2dcpu_path_eval(const d2d_scn* s, double u, double* x, double* y);

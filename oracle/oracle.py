@@ -60,6 +60,11 @@ def load() -> C.CDLL:
             "d2dcpu_moment_box": (D, [D, D, D]),
             "d2dcpu_spawn_uniforms": (None, [C.c_uint64, C.c_uint32, C.c_uint32, P(D)]),
             "d2dcpu_philox": (None, [P(C.c_uint32), P(C.c_uint32), P(C.c_uint32)]),
+            "d2dcpu_set_curriculum": (I32, [VP, P(abi.D2DCurriculum)]),
+            "d2dcpu_fresh_recipes": (I32, [VP, VP, VP, P(C.c_int64), I32]),
+            "d2dcpu_get_scenario_table": (I32, [VP, I32, I32, P(abi.D2DScn)]),
+            "d2dcpu_gen_curriculum": (None, [P(abi.D2DCurriculum), D, D, C.c_uint64, C.c_uint32, C.c_uint32, D,
+                                             P(abi.D2DScn)]),
         }
         for name, (res, args) in sigs.items():
             f = getattr(lib, name)
@@ -76,19 +81,25 @@ def _p(a):
 class OracleBatch:
     """Host-side batch with the same call shapes as the HIP library (numpy buffers)."""
 
-    def __init__(self, cfg, scenarios_c, n_envs: int, env_scenario=None):
+    def __init__(self, cfg, scenarios_c, n_envs: int, env_scenario=None, curriculum=None):
+        """``curriculum``: a D2DCurriculum for the fresh curriculum (cfg.scn_pool = 2; no scenarios)."""
         self.lib = load()
         abi = _abi()
         self.abi = abi
         self.n = int(n_envs)
         self.cfg = cfg
         self.h = self.lib.d2dcpu_create(C.byref(cfg), self.n)
-        arr = (abi.D2DScn * len(scenarios_c))(*scenarios_c)
-        self._scn = arr
-        es = None
-        if env_scenario is not None:
-            es = np.ascontiguousarray(np.asarray(env_scenario, dtype=np.int32))
-        self.lib.d2dcpu_set_scenarios(self.h, arr, len(scenarios_c), _p(es))
+        if curriculum is not None:
+            self._cur = curriculum
+            if self.lib.d2dcpu_set_curriculum(self.h, C.byref(curriculum)) != 0:
+                raise ValueError("d2dcpu_set_curriculum: cfg.scn_pool must be 2")
+        else:
+            arr = (abi.D2DScn * len(scenarios_c))(*scenarios_c)
+            self._scn = arr
+            es = None
+            if env_scenario is not None:
+                es = np.ascontiguousarray(np.asarray(env_scenario, dtype=np.int32))
+            self.lib.d2dcpu_set_scenarios(self.h, arr, len(scenarios_c), _p(es))
         n = self.n
         self.obs = np.zeros((n, abi.OBS_DIM), np.float32)
         self.rew = np.zeros(n, np.float32)
@@ -140,6 +151,24 @@ class OracleBatch:
         self.lib.d2dcpu_get_env_scenarios(self.h, _p(out))
         return out
 
+    def scenario_table(self, first: int, count: int):
+        out = (self.abi.D2DScn * count)()
+        if self.lib.d2dcpu_get_scenario_table(self.h, first, count, out) != 0:
+            raise ValueError("scenario table range")
+        return out
+
+    def fresh_recipes(self, keys=None, clocks=None, clock=None):
+        """get (no arguments) -> (keys int32[2n], clocks int64[2n], clock); set with all three."""
+        n2 = 2 * self.n
+        if keys is None:
+            k, c, t = np.zeros(n2, np.int32), np.zeros(n2, np.int64), C.c_int64()
+            self.lib.d2dcpu_fresh_recipes(self.h, _p(k), _p(c), C.byref(t), 0)
+            return k, c, t.value
+        k = np.ascontiguousarray(keys, np.int32)
+        c = np.ascontiguousarray(clocks, np.int64)
+        t = C.c_int64(int(clock))
+        self.lib.d2dcpu_fresh_recipes(self.h, _p(k), _p(c), C.byref(t), 1)
+
     def episode_stats(self, clear=True):
         out = np.zeros(self.abi.NSTATS, np.float64)
         self.lib.d2dcpu_episode_stats(self.h, _p(out), 1 if clear else 0)
@@ -185,3 +214,11 @@ def spawn_uniforms(seed: int, env_id: int, episode: int):
     u = (C.c_double * 3)()
     load().d2dcpu_spawn_uniforms(C.c_uint64(seed), env_id, episode, u)
     return list(u)
+
+
+def gen_curriculum(cur, W: float, H: float, seed: int, gid: int, key: int, sim: float):
+    """One fresh-curriculum scenario (the oracle's restatement of the device generator)."""
+    out = _abi().D2DScn()
+    load().d2dcpu_gen_curriculum(C.byref(cur), float(W), float(H), C.c_uint64(seed & (2 ** 64 - 1)), gid, key,
+                                 float(sim), C.byref(out))
+    return out

@@ -5,25 +5,29 @@ import torch
 
 
 class OracleVecBackend:
-    def __init__(self, num_envs, seed=0, env_scenario=None, timeup_truncates=False, env_id_offset=0, **kwargs):
+    def __init__(self, num_envs, seed=0, env_scenario=None, timeup_truncates=False, env_id_offset=0,
+                 envs_total=None, **kwargs):
         import oracle
 
         import drone2d_amd  # noqa: F401
         from drone2d_amd.config import make_cfg
-        from drone2d_amd.env import _make_box, build_scenarios, is_curriculum
+        from drone2d_amd.env import _make_box, build_scenarios, is_curriculum, is_fresh_curriculum, make_curriculum
 
         oracle.build()
         self.kwargs = dict(kwargs)
         self.num_envs = int(num_envs)
-        self.scenarios = build_scenarios(self.kwargs)
+        fresh = is_fresh_curriculum(self.kwargs)
+        self.scenarios = [] if fresh else build_scenarios(self.kwargs)
         if env_scenario is None:
-            env_scenario = np.arange(self.num_envs) % len(self.scenarios)
+            env_scenario = 2 * np.arange(self.num_envs) if fresh else np.arange(self.num_envs) % len(self.scenarios)
         self.env_scenario = np.ascontiguousarray(np.asarray(env_scenario, dtype=np.int32))
         self.cfg = make_cfg(dict(self.kwargs), auto_reset=True, timeup_truncates=timeup_truncates,
                             env_id_base=env_id_offset)
-        self.cfg.scn_pool = 1 if is_curriculum(self.kwargs) else 0  # as Drone2dVecEnv
+        # as Drone2dVecEnv: fresh curriculum (2), curriculum pool (1), test scenarios (0)
+        self.cfg.scn_pool = (2 if fresh else 1) if is_curriculum(self.kwargs) else 0
+        cur = make_curriculum(self.kwargs, envs_total or self.num_envs) if fresh else None
         self.orc = oracle.OracleBatch(self.cfg, [s.to_c() for s in self.scenarios], self.num_envs,
-                                      env_scenario=self.env_scenario)
+                                      env_scenario=self.env_scenario, curriculum=cur)
         self.seed_value = int(seed)
         self.action_space = _make_box(-np.ones(2), np.ones(2))
         self.observation_space = _make_box(-np.ones(27), np.ones(27))

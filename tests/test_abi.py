@@ -29,7 +29,8 @@ def test_struct_layout_matches_ctypes(tmp_path, d2):
     from drone2d_amd import abi
 
     prog = ["#include <stdio.h>", "#include <stddef.h>", f'#include "{HEADER}"', "int main(void){"]
-    for cname, cls in (("d2d_cfg", abi.D2DCfg), ("d2d_scn", abi.D2DScn)):
+    structs = (("d2d_cfg", abi.D2DCfg), ("d2d_scn", abi.D2DScn), ("d2d_curriculum", abi.D2DCurriculum))
+    for cname, cls in structs:
         prog.append(f'printf("{cname} %zu\\n", sizeof({cname}));')
         for fname, _ in cls._fields_:
             prog.append(f'printf("{cname}.{fname} %zu\\n", offsetof({cname}, {fname}));')
@@ -43,9 +44,8 @@ def test_struct_layout_matches_ctypes(tmp_path, d2):
     subprocess.run(["gcc", "-o", str(exe), str(c)], check=True)
     out = dict(line.rsplit(" ", 1) for line in subprocess.run([str(exe)], capture_output=True, text=True,
                                                                 check=True).stdout.splitlines())
-    assert int(out["d2d_cfg"]) == C.sizeof(abi.D2DCfg)
-    assert int(out["d2d_scn"]) == C.sizeof(abi.D2DScn)
-    for cname, cls in (("d2d_cfg", abi.D2DCfg), ("d2d_scn", abi.D2DScn)):
+    for cname, cls in structs:
+        assert int(out[cname]) == C.sizeof(cls), cname
         for fname, _ in cls._fields_:
             assert int(out[f"{cname}.{fname}"]) == getattr(cls, fname).offset, (cname, fname)
     assert int(out["D2D_NSTATE"]) == abi.NSTATE and int(out["D2D_NISTATE"]) == abi.NISTATE
@@ -68,7 +68,7 @@ def test_hip_library_exports_every_header_symbol(hip_lib):
     for f in header_functions():
         assert hasattr(hip_lib, f), f
         assert f in _native.SIGNATURES, f  # and the ctypes binding declares it
-    assert hip_lib.d2d_abi_version() == abi.ABI_VERSION == 3
+    assert hip_lib.d2d_abi_version() == abi.ABI_VERSION == 4
 
 
 def test_hip_library_is_gfx950(d2):

@@ -1,0 +1,139 @@
+"""Fresh curriculum (cfg.scn_pool = 2): every curriculum episode runs on a scenario the device
+generates for it (csrc/d2d_curriculum.h), as the reference's curriculum reset does
+(drone_2d_env.py:199-215, 318-372) -- needs an MI355X.
+
+* the device's scenario slots are bit-identical to the CPU oracle's restatement of the generator,
+  and stepping is in parity with the oracle, teacher-forced, across many auto-resets and a stage
+  change of the sim_num schedule;
+* the stage follows the schedule through 700 k / 1 M / 1.6 M / 2 M with no host call but ``step``,
+  and every episode gets its own scenario (distinct scenarios per n_steps steps >= num_envs);
+* a checkpoint (slot recipes + state) restores into a new handle bit-identically.
+"""
+import numpy as np
+import pytest
+import torch
+
+from parity_util import OBS_ATOL, compare_step
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = ("n_wps", "n_circles", "us", "xa", "xb", "xc", "ya", "yb", "yc", "cx", "cy", "cr", "wp_last_x",
+          "wp_last_y", "spawn_xmin", "spawn_xmax", "spawn_ymin", "spawn_ymax", "spawn_amin", "spawn_amax")
+
+
+def _kw(**over):
+    from drone2d_amd.config import ENV_TRAIN_CONFIG
+
+    return dict(ENV_TRAIN_CONFIG, mode="curriculum", scenario="curriculum", **over)
+
+
+def _pair(d2, n, seed, kw):
+    import oracle
+    from drone2d_amd.config import make_cfg
+    from drone2d_amd.env import make_curriculum
+
+    venv = d2.Drone2dVecEnv(n, seed=seed, **kw)
+    assert venv.cfg.scn_pool == 2 and venv.fresh
+    cfg = make_cfg(dict(kw))
+    cfg.scn_pool = 2
+    orc = oracle.OracleBatch(cfg, [], n, curriculum=make_curriculum(kw, n))
+    np.testing.assert_allclose(venv.reset().cpu().numpy(), orc.reset(seed), rtol=0, atol=OBS_ATOL)
+    return venv, orc
+
+
+def _tables_equal(venv, orc):
+    n2 = 2 * venv.num_envs
+    g, o = venv.scenario_table(0, n2), orc.scenario_table(0, n2)
+    assert bytes(g) == bytes(o) or _diff(g, o)
+    kg, cg, tg = venv.fresh_recipes()
+    ko, co, to = orc.fresh_recipes()
+    np.testing.assert_array_equal(kg, ko)
+    np.testing.assert_array_equal(cg, co)
+    assert tg == to
+
+
+def _diff(g, o):
+    for s in range(len(g)):
+        for f in FIELDS:
+            a, b = getattr(g[s], f), getattr(o[s], f)
+            a = np.array(a[:] if hasattr(a, "__len__") else a)
+            b = np.array(b[:] if hasattr(b, "__len__") else b)
+            assert np.array_equal(a, b), (s, f, a, b)
+    return True
+
+
+def test_fresh_generator_bitwise_and_step_parity(d2):
+    n, rng = 2048, np.random.default_rng(3)
+    # sim_num = 1.95e6 + 2048 / step: stage 4 (on-path obstacles) -> stage 5 after 25 steps
+    venv, orc = _pair(d2, n, 17, _kw(sim_num=1950000))
+    _tables_equal(venv, orc)
+    dones = 0
+    for t in range(120):
+        compare_step(venv, orc, rng.uniform(-1, 1, (n, 2)).astype(np.float32))
+        dones += int(orc.term.sum())
+        if t % 20 == 19:
+            _tables_equal(venv, orc)
+            np.testing.assert_array_equal(venv.get_env_scenarios().cpu().numpy(), 2 * np.arange(n) +
+                                          ((venv.get_state()[1][2].cpu().numpy() - 1) & 1))
+    assert dones > 300
+    venv.close()
+
+
+def _stage_of(sim):
+    return 1 if sim <= 7e5 else 2 if sim <= 1e6 else 3 if sim <= 1.6e6 else 4 if sim <= 2e6 else 5
+
+
+def test_fresh_stage_schedule_on_device(d2):
+    """Only ``step`` is called: the device clock moves sim_num = steps x 4096 through every stage."""
+    n, rng = 4096, np.random.default_rng(4)
+    venv = d2.Drone2dVecEnv(n, seed=5, **_kw(sim_num=0))
+    venv.reset()
+    ep0 = venv.get_state()[1][2].clone()
+    stages_seen = set()
+    for t in range(1, 601):
+        venv.step(torch.rand(n, 2, device=venv.device) * 2 - 1)
+        if t % 60 == 0:
+            keys, clocks, clock = venv.fresh_recipes()
+            assert clock == t
+            tab = venv.scenario_table(0, 2 * n)
+            for s in np.flatnonzero(keys >= 0)[::7]:
+                st = _stage_of(float(clocks[s]) * n)
+                stages_seen.add(st)
+                sc = tab[s]
+                box = (sc.spawn_xmin, sc.spawn_xmax, sc.spawn_ymin, sc.spawn_ymax) == (100.0, 1200.0, 100.0, 1200.0)
+                assert box == (st == 2), (s, st)
+                if st <= 2:
+                    assert sc.n_circles == 0
+                if st in (3, 4):
+                    assert sc.n_circles <= 1
+                if st != 2:
+                    assert sc.spawn_xmin == sc.spawn_xmax  # spawn at the first waypoint
+        if t == 540:  # every env started >= 1 episode in the last n_steps steps; each on its own path
+            started = int((venv.get_state()[1][2] - ep0).sum())
+            assert started >= n
+    assert stages_seen == {1, 2, 3, 4, 5}
+    tab = venv.scenario_table(0, 2 * n)
+    keys = venv.fresh_recipes()[0]
+    paths = {(round(tab[s].wp_last_x, 9), round(tab[s].wp_last_y, 9)) for s in np.flatnonzero(keys >= 0)}
+    assert len(paths) == int((keys >= 0).sum())
+    venv.close()
+
+
+def test_fresh_checkpoint_restore(d2):
+    n, rng = 1024, np.random.default_rng(6)
+    kw = _kw(sim_num=2500000)
+    a = d2.Drone2dVecEnv(n, seed=8, **kw)
+    a.reset()
+    for _ in range(80):
+        a.step(torch.as_tensor(rng.uniform(-1, 1, (n, 2)).astype(np.float32)))
+    sd = a.state_dict()
+    b = d2.Drone2dVecEnv(n, seed=1, **kw)
+    b.load_state_dict(sd)
+    assert bytes(a.scenario_table()) == bytes(b.scenario_table())
+    for _ in range(100):
+        act = torch.as_tensor(rng.uniform(-1, 1, (n, 2)).astype(np.float32))
+        oa, ra, ta, _, _ = a.step(act)
+        ob, rb, tb, _, _ = b.step(act)
+        assert torch.equal(oa, ob) and torch.equal(ra, rb) and torch.equal(ta, tb)
+    a.close()
+    b.close()

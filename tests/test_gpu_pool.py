@@ -89,6 +89,38 @@ def test_pool_checkpoint_restore(d2):
     b.close()
 
 
+def test_pool_checkpoint_after_refresh(d2):
+    """a checkpoint taken after refresh_curriculum (envs on both pool halves) restores
+    into a handle whose own pool is different -- the saved pool halves come with the checkpoint --
+    and continues bit-identically; indices into a pool half that was never filled are refused."""
+    from drone2d_amd._native import NativeError
+
+    n, rng = 512, np.random.default_rng(13)
+    a = d2.Drone2dVecEnv(n, seed=3, **_kw(n_steps=60))
+    a.reset()
+    for _ in range(70):
+        a.step(torch.as_tensor(rng.uniform(-1, 1, (n, 2)).astype(np.float32)))
+    a.refresh_curriculum(seed=77)
+    for _ in range(20):  # some envs reset into the new half, others still run first-half episodes
+        a.step(torch.as_tensor(rng.uniform(-1, 1, (n, 2)).astype(np.float32)))
+    sd = a.state_dict()
+    es = sd["env_scn"].cpu().numpy()
+    assert (es < 16).any() and (es >= 16).any() and sd["pool"]["active_base"] == 16
+    assert sd["pool"]["valid_mask"] == 3
+    b = d2.Drone2dVecEnv(n, seed=999, **_kw(n_steps=60, curriculum_seed=6))  # its own, different pool
+    with pytest.raises(NativeError, match="no scenarios"):  # b never filled its second half
+        b.set_env_scenarios(torch.full((n,), 20, dtype=torch.int32))
+    b.load_state_dict(sd)
+    for _ in range(100):
+        act = torch.as_tensor(rng.uniform(-1, 1, (n, 2)).astype(np.float32))
+        oa, ra, ta, _, _ = a.step(act)
+        ob, rb, tb, _, _ = b.step(act)
+        assert torch.equal(oa, ob) and torch.equal(ra, rb) and torch.equal(ta, tb)
+    np.testing.assert_array_equal(a.get_env_scenarios().cpu().numpy(), b.get_env_scenarios().cpu().numpy())
+    a.close()
+    b.close()
+
+
 def test_rejected_scenarios_leave_handle_usable(d2):
     from drone2d_amd import abi
     from drone2d_amd._native import NativeError

@@ -249,7 +249,7 @@ def test_rollout_graph_matches_eager(d2):
     outs = []
     for graph in (False, True):
         venv = d2.Drone2dVecEnv(2048, seed=4, with_info=True, **_kw(scenario="corridor"))
-        cfg = PPOConfig.gpu_defaults(n_steps=8, batch_size=4096)
+        cfg = PPOConfig.gpu_defaults(n_steps=16, batch_size=4096)
         cfg.graph = graph
         algo = PPO(venv, cfg, seed=2)
         rec = []
