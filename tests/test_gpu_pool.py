@@ -18,7 +18,7 @@ pytestmark = pytest.mark.gpu
 def _kw(**over):
     from drone2d_amd.config import ENV_TRAIN_CONFIG
 
-    return dict(ENV_TRAIN_CONFIG, scenario="stage_5", mode="curriculum", curriculum_pool=16, curriculum_seed=5,
+    return dict(dict(ENV_TRAIN_CONFIG, scenario="stage_5", mode="curriculum", curriculum_pool=16, curriculum_seed=5),
                 **over)
 
 
