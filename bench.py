@@ -78,6 +78,22 @@ def setup_dist(args):
     return rank, world, local
 
 
+def _upload_graphs(graphs, stream):
+    """hipGraphUpload each instantiated graph (its first replay then does not pay the upload); the
+    symbol comes from the HIP runtime torch loaded (through libdrone2d_hip.so's dependency tree)."""
+    try:
+        from drone2d_amd import _native
+        import ctypes as C
+
+        up = _native.load().hipGraphUpload
+        up.restype, up.argtypes = C.c_int, [C.c_void_p, C.c_void_p]
+        for g in graphs:
+            up(C.c_void_p(g.raw_cuda_graph_exec()), C.c_void_p(stream.cuda_stream))
+        torch.cuda.synchronize()
+    except (AttributeError, RuntimeError, OSError):
+        pass
+
+
 def barrier_sync(world):
     if world > 1:
         dist.barrier()
@@ -176,27 +192,31 @@ def main():
     venv.reset()
     stream = torch.cuda.current_stream(dev)
 
+    # The timed steps replay captured HIP graphs: one graph of all args.steps steps (longer runs: a
+    # 256-step graph replayed + one graph of the remainder).  The graphs are captured and uploaded
+    # BEFORE the warmup, so the warmup steps run right before the timed region (no idle GPU, no
+    # host-side capture in between) and the timed region holds as few replay boundaries as possible.
+    glen = args.steps if args.steps <= 512 else 256
+    reps, rem = divmod(args.steps, glen)
+    graph = tail = None
+    hipgraph = not args.eager
+    if hipgraph:
+        def capture(n_steps):
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for k in range(n_steps):
+                    venv.step(bank[k % ACTION_BANK])
+            return g
+        if reps:
+            graph = capture(glen)
+        if rem:
+            tail = capture(rem)
+        torch.cuda.synchronize()
+        _upload_graphs([g for g in (graph, tail) if g is not None], stream)
+
     for k in range(args.warmup):
         venv.step(bank[k % ACTION_BANK])
     venv.episode_stats(clear=True)
-
-    # exactly args.steps timed steps: reps replays of a 16-step graph + one graph of the remainder
-    reps, rem = divmod(args.steps, ACTION_BANK)
-    graph = tail = None
-    if not args.eager:
-        # capture ACTION_BANK steps (even count: the output double-buffer returns to its start)
-        if reps:
-            graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
-                for k in range(ACTION_BANK):
-                    venv.step(bank[k])
-        if rem:
-            tail = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(tail):
-                for k in range(rem):
-                    venv.step(bank[k])
-        torch.cuda.synchronize()
-    hipgraph = not args.eager
 
     segs = (reps + (1 if rem else 0)) if hipgraph else args.steps
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(segs)]

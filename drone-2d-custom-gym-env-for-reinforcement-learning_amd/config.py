@@ -73,6 +73,12 @@ REQUIRED_KEYS = (
 TEST_SCENARIOS = ("perpendicular", "parallel", "S_parallel", "corridor", "S_corridor", "large", "impossible")
 CURRICULUM_STAGES = ("stage_1", "stage_2", "stage_3", "stage_4", "stage_5")
 
+# Relative step-kernel cost of each test scenario (us per step at 65 536 envs of that scenario alone,
+# MI355X, DESIGN.md "Every test scenario alone"): the quad workgroups pair heavy with light scenarios
+# on each SIMD by these weights (d2d_set_scenario_costs; placement only, never results).
+SCENARIO_STEP_COST = {"perpendicular": 31.2, "parallel": 31.3, "S_parallel": 43.8, "corridor": 32.4,
+                      "S_corridor": 45.1, "large": 41.5, "impossible": 32.4}
+
 FORCE_SCALE = 1000.0   # drone_2d_env.py:150
 SPACE_DAMPING = 1.0    # body.damping = 0.9 (drone_2d_env.py:376-380) has no effect in pymunk 6
 

@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -77,6 +78,13 @@ struct d2d_handle {
     uint64_t fresh_seed = 0;
     bool fresh_seeded = false;
     int32_t generation = 0;      // bumped whenever captured graphs' pointers go stale
+    // quad workgroups (d2d_step_quad_kernel): one per QuadDesc
+    QuadDesc* quad = nullptr;
+    int n_quads = 0;
+    int n_cu = 0;                      // compute units of the device
+    std::vector<double> scn_cost;      // relative step cost per scenario (d2d_set_scenario_costs)
+    int quad_mode = 0;                 // D2D_QUAD: 0 off (default: measured slower), 1 on,
+                                       // -1 when there is at least one quad per CU
 };
 
 namespace {
@@ -108,7 +116,117 @@ StepArgs make_args(const d2d_t* h) {
     a.wg_scn = h->wg_scn;
     a.scn_tag = h->scn_tag;
     a.clock = h->clock;
+    a.quad = h->quad;
     return a;
+}
+
+// Quad workgroups for the current layout (identity with one scenario, or the scenario-grouped
+// layout; pool / fresh curriculum keep the 256-thread kernels).  Groups are dealt by step cost:
+// sorted heaviest first, quad j takes the heavy pair 2j, 2j + 1 as quarters 0 and 2 and the light
+// pair from the other end as quarters 1 and 3; wave 4 r + c (SIMD class c) runs role r of quarter
+// (c + r) % 4, so every SIMD runs one wave of each role and, of its path (role 2) and sensing (role
+// 1) waves, one belongs to a heavy quarter and one to a light one.  Each quad stages up to four
+// scenarios (+ probe tables) once; a quarter whose scenarios do not fit reads them from global memory.
+hipError_t make_quads(d2d_t* h) {
+    if (h->quad) (void)hipFree(h->quad);
+    h->quad = nullptr;
+    h->n_quads = 0;
+    const bool grouped = h->lane_env != nullptr;
+    if (h->cfg.scn_pool || !h->brt || (!grouped && h->n_scn != 1)) return hipSuccess;
+    const int ng = (h->ns + EPB - 1) / EPB;
+    const int nq = (ng + 3) / 4;
+    if (h->quad_mode == 0 || (h->quad_mode < 0 && nq < h->n_cu)) return hipSuccess;
+    std::vector<int32_t> ws((size_t)ng, 0);
+    if (grouped) {
+        hipError_t e = hipMemcpy(ws.data(), h->wg_scn, sizeof(int32_t) * (size_t)ng, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) return e;
+    }
+    auto cost = [&](int g) {
+        if (g < 0) return -1.0;
+        const int w = ws[(size_t)g];
+        auto c = [&](int s) { return (s >= 0 && s < (int)h->scn_cost.size()) ? h->scn_cost[(size_t)s] : 1.0; };
+        return w >= 0 ? c(w) : (w <= -2 ? std::max(c(-w - 2), c(-w - 1)) : 2.0);
+    };
+    // quads in XCD chunks (xcd_group: XCD x runs quad numbers [first_x, first_x + cnt_x)); a chunk's
+    // quads take the groups of one contiguous range of group numbers (= of env ids: make_groups
+    // numbers groups by their first env), so the env-ordered output rows one XCD writes stay together
+    // in its L2, and inside the chunk the groups are dealt by cost
+    std::vector<int32_t> order((size_t)(4 * nq), -1);
+    {
+        const int per = nq / 8, rem = nq % 8;
+        int qfirst = 0;
+        for (int x = 0; x < 8; ++x) {
+            const int cnt = per + (x < rem ? 1 : 0);
+            const int g0 = std::min(ng, 4 * qfirst), g1 = std::min(ng, 4 * (qfirst + cnt));
+            std::vector<int32_t> ch;
+            for (int g = g0; g < g1; ++g) ch.push_back(g);
+            while ((int)ch.size() < 4 * cnt) ch.push_back(-1);
+            if (grouped)  // heaviest first (ties: group order); empty quarters last
+                std::stable_sort(ch.begin(), ch.end(), [&](int32_t u, int32_t v) { return cost(u) > cost(v); });
+            for (int k = 0; k < 4 * cnt; ++k) order[(size_t)(4 * qfirst + k)] = ch[(size_t)k];
+            qfirst += cnt;
+        }
+    }
+    std::vector<QuadDesc> Q((size_t)nq);
+    for (int j = 0; j < nq; ++j) {
+        QuadDesc& D = Q[(size_t)j];
+        std::memset(&D, 0, sizeof D);
+        if (grouped) {
+            // chunk c of this quad: its groups are order[4 f, 4 f + 4 m) sorted by cost; quad f + i takes
+            // the heavy pair 2 i, 2 i + 1 and the light pair from the chunk's other end
+            const int per = nq / 8, rem = nq % 8;
+            int f = 0, m = 0;
+            for (int x = 0, first = 0; x < 8; ++x) {
+                const int cnt = per + (x < rem ? 1 : 0);
+                if (j >= first && j < first + cnt) {
+                    f = first;
+                    m = cnt;
+                }
+                first += cnt;
+            }
+            const int i = j - f;
+            const size_t base = (size_t)(4 * f), last = base + (size_t)(4 * m) - 1;
+            D.group[0] = order[base + (size_t)(2 * i)];
+            D.group[2] = order[base + (size_t)(2 * i + 1)];
+            D.group[1] = order[last - (size_t)(2 * i)];
+            D.group[3] = order[last - (size_t)(2 * i + 1)];
+        } else {
+            for (int q = 0; q < 4; ++q) D.group[q] = (4 * j + q < ng) ? 4 * j + q : -1;
+        }
+        for (int k = 0; k < 4; ++k) D.stage[k] = -1;
+        int used = 0;
+        for (int q = 0; q < 4; ++q) {
+            const int g = D.group[q];
+            const int w = (g >= 0 && grouped) ? ws[(size_t)g] : 0;
+            const int lo = w >= 0 ? w : -w - 2, cnt = w >= 0 ? 1 : (w <= -2 ? 2 : 0);
+            D.s0[q] = lo;
+            D.qslot[q] = -1;
+            if (cnt == 0) continue;  // three or more scenarios in the group: global memory
+            int at = -1;
+            for (int k = 0; k + cnt <= used && at < 0; ++k)
+                if (D.stage[k] == lo && (cnt == 1 || D.stage[k + 1] == lo + 1)) at = k;
+            if (at < 0 && used + cnt <= 4) {
+                at = used;
+                for (int k = 0; k < cnt; ++k) D.stage[used++] = lo + k;
+            }
+            D.qslot[q] = at;
+        }
+        uint64_t roles = 0;
+        for (int w = 0; w < 16; ++w) {
+            const int r = w / 4, c = w % 4, q = (c + r) % 4;
+            roles |= (uint64_t)((q << 2) | r) << (4 * w);
+        }
+        D.roles = roles;
+    }
+    hipError_t e = hipMalloc(&h->quad, sizeof(QuadDesc) * (size_t)nq);
+    if (e == hipSuccess) e = hipMemcpy(h->quad, Q.data(), sizeof(QuadDesc) * (size_t)nq, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        if (h->quad) (void)hipFree(h->quad);
+        h->quad = nullptr;
+        return e;
+    }
+    h->n_quads = nq;
+    return hipSuccess;
 }
 
 // K5: the fresh curriculum's scenario slots (restore: every slot from its recipe), on `stream`
@@ -141,10 +259,12 @@ hipError_t rc_fill(d2d_t* h, hipStream_t stream, bool force = false) {
     a.fill_force = force ? 1 : 0;
     const int spb = (D2D_FILL_SPLIT && D2D_FILL_COMPACT) ? FILL_SPB : BLOCK;
     const dim3 grid((h->ns + spb - 1) / spb);
+    // (D2D_FILL_RESIDENT: dynamic LDS padded to K1's per-workgroup LDS, so K4 is resident 4 per CU as K1)
+    const size_t pad = D2D_FILL_RESIDENT ? sizeof(d2d::Scn) + sizeof(d2d::BtHot) + sizeof(K1Shared) - 2048 : 0;
     if (sizeof(d2d::Scn) * (size_t)h->n_scn <= K2_LDS_BUDGET)
-        hipLaunchKernelGGL(d2d_fill_kernel<true>, grid, dim3(BLOCK), sizeof(d2d::Scn) * h->n_scn, stream, a);
+        hipLaunchKernelGGL(d2d_fill_kernel<true>, grid, dim3(BLOCK), std::max(sizeof(d2d::Scn) * h->n_scn, pad), stream, a);
     else
-        hipLaunchKernelGGL(d2d_fill_kernel<false>, grid, dim3(BLOCK), 0, stream, a);
+        hipLaunchKernelGGL(d2d_fill_kernel<false>, grid, dim3(BLOCK), pad, stream, a);
     return hipGetLastError();
 }
 // drop every entry (new seed, counters or scenarios) and refill, ordered on `stream`
@@ -318,6 +438,8 @@ int32_t d2d_create(const d2d_cfg* cfg, int32_t n_envs, int32_t device, d2d_t** o
     h->cfg = *cfg;
     h->n = n_envs;
     h->device = device;
+    if (hipDeviceGetAttribute(&h->n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) h->n_cu = 256;
+    if (const char* qm = std::getenv("D2D_QUAD")) h->quad_mode = std::atoi(qm);  // A/B switch (diagnostics)
     const size_t n = (size_t)n_envs;
     Layout L;
     if ((e = hipMalloc(&h->env_scn, sizeof(int32_t) * n)) != hipSuccess ||
@@ -352,6 +474,7 @@ void d2d_destroy(d2d_t* h) {
     if (h->pool_dev) (void)hipFree(h->pool_dev);
     if (h->fill_ctl) (void)hipFree(h->fill_ctl);
     if (h->clock) (void)hipFree(h->clock);
+    if (h->quad) (void)hipFree(h->quad);
     if (h->abi) (void)hipFree(h->abi);
     if (h->scn_tag) (void)hipFree(h->scn_tag);
     if (h->gclk) (void)hipFree(h->gclk);
@@ -451,6 +574,7 @@ int32_t d2d_set_scenarios(d2d_t* h, const d2d_scn* scns, int32_t n_scn, const in
     h->pool_valid = 1;
     h->generation += 1;  // the old tables are freed: captured graphs point at them
     h->rc_dirty = true;  // cached reset observations belong to the old scenarios
+    if ((int)h->scn_cost.size() != n_scn) h->scn_cost.assign((size_t)n_scn, 1.0);
     e = env_scn_host ? hipMemcpy(h->env_scn, env_scn_host, sizeof(int32_t) * (size_t)h->n, hipMemcpyHostToDevice)
                      : hipMemset(h->env_scn, 0, sizeof(int32_t) * (size_t)h->n);
     if (e != hipSuccess) {
@@ -459,6 +583,20 @@ int32_t d2d_set_scenarios(d2d_t* h, const d2d_scn* scns, int32_t n_scn, const in
         h->reset_done = false;
         return hip_fail(e, "d2d_set_scenarios: env_scn upload");
     }
+    if ((e = make_quads(h)) != hipSuccess) return hip_fail(e, "d2d_set_scenarios: quad workgroups");
+    return D2D_OK;
+}
+
+int32_t d2d_set_scenario_costs(d2d_t* h, const double* cost, int32_t n_scn) {
+    if (!h || !cost) return fail(D2D_E_ARG, "d2d_set_scenario_costs: null argument");
+    if (h->cfg.scn_pool || n_scn != h->n_scn) return fail(D2D_E_ARG, "d2d_set_scenario_costs: one cost per scenario (test mode)");
+    for (int k = 0; k < n_scn; ++k)
+        if (!(cost[k] >= 0.0)) return fail(D2D_E_ARG, "d2d_set_scenario_costs: costs must be >= 0");
+    DeviceGuard g(h->device);
+    hipError_t e;
+    if ((e = hipDeviceSynchronize()) != hipSuccess) return hip_fail(e, "d2d_set_scenario_costs: sync");
+    h->scn_cost.assign(cost, cost + n_scn);
+    if ((e = make_quads(h)) != hipSuccess) return hip_fail(e, "d2d_set_scenario_costs: quad workgroups");
     return D2D_OK;
 }
 
@@ -519,7 +657,14 @@ int32_t d2d_step(d2d_t* h, const float* act_dev, float* obs_dev, float* rew_dev,
     const dim3 grid((h->n + EPB - 1) / EPB);
     const size_t lds_scn = sizeof(d2d::Scn) * (size_t)h->n_scn, lds_hot = sizeof(d2d::BtHot) * (size_t)h->n_scn;
     static_assert(sizeof(d2d::Scn) + sizeof(d2d::BtHot) + sizeof(K1Shared) <= K1_LDS_BUDGET, "grouped K1 LDS");
-    if (h->lane_env)
+    static_assert(4 * (sizeof(d2d::Scn) + sizeof(d2d::BtHot) + sizeof(K1Shared)) <= 160 * 1024, "quad K1 LDS");
+    if (h->quad) {
+        const size_t dyn = 4 * (sizeof(d2d::Scn) + sizeof(d2d::BtHot));
+        if (h->lane_env)
+            hipLaunchKernelGGL(d2d_step_quad_kernel<true>, dim3(h->n_quads), dim3(QUAD_THREADS), dyn, (hipStream_t)stream, a);
+        else
+            hipLaunchKernelGGL(d2d_step_quad_kernel<false>, dim3(h->n_quads), dim3(QUAD_THREADS), dyn, (hipStream_t)stream, a);
+    } else if (h->lane_env)
         hipLaunchKernelGGL(d2d_step_grouped_kernel, dim3(h->n_groups), dim3(K1_THREADS),
                            sizeof(d2d::Scn) + sizeof(d2d::BtHot), (hipStream_t)stream, a);
     else if (a.brt && lds_scn + lds_hot + sizeof(K1Shared) <= K1_LDS_BUDGET)

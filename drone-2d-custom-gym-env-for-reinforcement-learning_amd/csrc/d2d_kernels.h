@@ -61,6 +61,22 @@ constexpr size_t K2_LDS_BUDGET = 64 * 1024;
         if ((p) != 0) __builtin_amdgcn_s_setprio(p);  \
     } while (0)
 
+// Quad workgroup (d2d_step_quad_kernel): four 64-env groups in one 1 024-thread workgroup.  Waves w
+// and w + 4 k share a SIMD (wave w lands on SIMD cycle[(start + w) % 4] whatever the start), so the
+// host decides which (quarter, role) each SIMD runs -- one wave of every role per SIMD, heavy and
+// light scenarios' path and sensing waves paired (d2d_hip.hip, make_quads) -- instead of relying on
+// how the dispatcher rotates the wave placement of co-resident 256-thread workgroups.
+struct QuadDesc {
+    int32_t group[4];   // quarter q's 64-env group (slots [64 g, 64 g + 64)); -1: empty quarter
+    int32_t stage[4];   // scenario staged in LDS slot j (scenario + probe table); -1: unused
+    int32_t qslot[4];   // LDS slot of quarter q's scenario s0 (a straddling pair: s0 + 1 in qslot + 1);
+                        // -1: the quarter reads its scenarios from global memory
+    int32_t s0[4];      // quarter q's (first) scenario
+    uint64_t roles;     // wave w -> bits [4w, 4w + 4): quarter << 2 | role
+    uint64_t pad;
+};
+static_assert(sizeof(QuadDesc) == 80, "QuadDesc size");
+
 struct StepArgs {
     int n;                   // envs
     int ns;                  // state slots: the column count of every [F][ns] internal array (= n
@@ -106,6 +122,7 @@ struct StepArgs {
     // reset observation only once its scenario exists) and the step clock K1 advances
     const int32_t* scn_tag;   // [2 n]
     int64_t* clock;           // [1]
+    const QuadDesc* quad;     // quad workgroups (d2d_step_quad_kernel), or null
 };
 
 // Auto-reset observation cache.  The observation an env gets when it auto-resets depends only on
@@ -169,11 +186,12 @@ constexpr int FILL_SPB = (D2D_RC_SLOTS == 2) ? 64 : 128;
 #define STAMP(k)                                                                                       \
     do {                                                                                               \
         if (a.stamps && (threadIdx.x & 63) == 0)                                                       \
-            a.stamps[(size_t)(blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
+            a.stamps[(size_t)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
         if (a.stamps && (threadIdx.x & 63) == 0 && (k) == 0)                                           \
-            a.stamps[(size_t)(blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + 7] =                          \
+            a.stamps[(size_t)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8 + 7] =                          \
                 ((uint64_t)__builtin_amdgcn_s_getreg((3 << 11) | 20) << 32) |                          \
-                (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4);                                   \
+                (uint32_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) | ((uint64_t)(wave & 3) << 36) |   \
+                ((uint64_t)(uint32_t)(wg + 1) << 40);                                                  \
     } while (0)
 // K4: the same per wave, at offset D2D_FSTAMP_BASE of the buffer (0 start, 1 staged + compacted,
 // 2 spawn state, 3 the wave's first part, 4 first barrier, 5 continuation, 6 path part, 7 end)
@@ -181,7 +199,7 @@ constexpr int FILL_SPB = (D2D_RC_SLOTS == 2) ? 64 : 128;
 #define FSTAMP(k)                                                                                      \
     do {                                                                                               \
         if (a.stamps && (threadIdx.x & 63) == 0)                                                       \
-            a.stamps[D2D_FSTAMP_BASE + (size_t)(blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + (k)] =      \
+            a.stamps[D2D_FSTAMP_BASE + (size_t)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8 + (k)] =      \
                 __builtin_amdgcn_s_memtime();                                                          \
     } while (0)
 #else
@@ -319,6 +337,7 @@ struct K1Shared {
     uint32_t ep[EPB];         // W0 -> W1, W3: episode counter (the state's copy changes at a reset)
     double sina[EPB];         // W0 -> W2: sin of the post-step frame angle (AA reward)
     uint32_t f_done, f_ca, f_gs, f_pre, f_ver, f_ver1;
+    uint32_t f_end;           // quad workgroups: the group's roles that reached the epilogue
     double pe[2][EPB];        // W3 -> W0: path_err, total_reward (prefetched for the epilogue)
     union {
         struct {
@@ -342,30 +361,18 @@ __device__ __forceinline__ void flag_wait(const uint32_t& f) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-// LDS: scenario tables in LDS; LTAB: the golden-march probe tables too (after the scenarios);
-// GRP: grouped slot layout (a.lane_env) -- with LDS, the group is pure and stages only its own
-// scenario.  s_scn: the dynamic LDS (scenario tables [+ probe tables], sized at launch).
+// Scenario staging of a 256-thread K1 workgroup (group wg).  LDS: scenario tables in LDS; LTAB: the
+// golden-march probe tables too (after the scenarios); GRP: grouped slot layout (a.lane_env) -- with
+// LDS, the group is pure and stages only its own scenario.  s_scn: the dynamic LDS (scenario tables
+// [+ probe tables], sized at launch).  Returns the tables indexed by global scenario id and the
+// group's (first) scenario s0.
 template <bool LDS, bool LTAB, bool GRP>
-__device__ __forceinline__ void k1_body(const StepArgs& a, Scn* s_scn, K1Shared& sh, int wg) {
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    const int e0 = wg * EPB;
-    const int i = e0 + lane;                     // slot: internal arrays, reset cache
-    const int ie = GRP ? a.lane_env[i] : i;      // env: caller's buffers, scenario map, spawn RNG
-    const bool valid = GRP ? ie >= 0 : i < a.n;
-    const int n = a.ns;
-    const bool auto_reset = a.cfg.auto_reset != 0;
-    STAMP(0);
-    if (D2D_FILL_EVERY > 1 && wg == 0 && threadIdx.x == 0 && a.fill_ctl)  // K4's tick: publish its next value
-        __hip_atomic_store(&a.fill_ctl[0], __hip_atomic_load(&a.fill_ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (wg == 0 && threadIdx.x == 0 && a.clock)  // the step clock (fresh curriculum stage schedule)
-        __hip_atomic_fetch_add(a.clock, (int64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ void k1_stage(const StepArgs& a, Scn* s_scn, int wg, const Scn*& scns,
+                                         const BtHot*& hots, int& s0) {
     const int ws = (GRP && LDS) ? a.wg_scn[wg] : 0;
-    const int s0 = ws >= 0 ? ws : -ws - 2;          // a straddling group: its two scenarios s0, s0 + 1
+    s0 = ws >= 0 ? ws : -ws - 2;          // a straddling group: its two scenarios s0, s0 + 1
     const int ncopy = (GRP && LDS) ? (ws >= 0 ? 1 : 2) : a.n_scn;
-    const Scn* scns;
-    const BtHot* hots = nullptr;
+    hots = nullptr;
     if (D2D_GLDS && LDS && (ncopy == 1 || !LTAB)) {
         // one scenario (+ its probe table) or scenarios only: contiguous sources, LDS-DMA
         glds_copy<K1_THREADS / 64>(s_scn, a.scn + s0, (int)sizeof(Scn) * ncopy);
@@ -376,6 +383,32 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, Scn* s_scn, K1Shared&
         scns = stage_scenarios<LDS, K1_THREADS>(a, s_scn, s0, ncopy);
         if (LTAB) hots = stage_hot<K1_THREADS>(a, reinterpret_cast<BtHot*>(s_scn + ncopy), s0, ncopy);
     }
+}
+
+// One env step for the 64 envs of group wg (slots [64 wg, 64 wg + 64); wg < 0: an empty quarter of a
+// quad workgroup, every lane invalid) by the calling wave in role `role` (0..3, wave-uniform); qt =
+// 64 role + lane, the thread's index among the group's 256.  scns / hots: the scenario and probe
+// tables indexed by global scenario id (LDS when staged: LDS / LTAB), s0 the group's scenario.
+// All 256 threads of the group call it once; the workgroup's barriers are block-wide, so every
+// wave of the block runs k1_body exactly once.
+template <bool LDS, bool LTAB, bool GRP, bool QSYNC = false>
+__device__ __forceinline__ void k1_body(const StepArgs& a, const Scn* scns, const BtHot* hots, int s0, K1Shared& sh,
+                                        int wg, int role, int qt) {
+    const int wave = role;
+    const int lane = threadIdx.x & 63;
+    const bool gvalid = wg >= 0;
+    const int e0 = gvalid ? wg * EPB : 0;
+    const int i = e0 + lane;                     // slot: internal arrays, reset cache
+    const int ie = (GRP && gvalid) ? a.lane_env[i] : i;  // env: caller's buffers, scenario map, spawn RNG
+    const bool valid = gvalid && (GRP ? ie >= 0 : i < a.n);
+    const int n = a.ns;
+    const bool auto_reset = a.cfg.auto_reset != 0;
+    STAMP(0);
+    if (D2D_FILL_EVERY > 1 && wg == 0 && qt == 0 && a.fill_ctl)  // K4's tick: publish its next value
+        __hip_atomic_store(&a.fill_ctl[0], __hip_atomic_load(&a.fill_ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (wg == 0 && qt == 0 && a.clock)  // the step clock (fresh curriculum stage schedule)
+        __hip_atomic_fetch_add(a.clock, (int64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (wave == 0) sh.scn[lane] = (valid && a.env_scn && a.n_scn > 1) ? a.env_scn[ie] : s0;
     if (D2D_SPLIT3 && wave == 0) sh.pflags[lane] = 0x7fffffffu;  // W1 and W3 min their table parts in
     // state loads issued before the staging barrier, so their HBM latency overlaps the staging:
@@ -407,13 +440,14 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, Scn* s_scn, K1Shared&
             PB[0] = load_frame(a, i);
         }
     }
-    if (threadIdx.x == 0) {
+    if (qt == 0) {
         sh.f_done = 0u;
         sh.f_ca = 0u;
         sh.f_gs = 0u;
         sh.f_pre = 0u;
         sh.f_ver = 0u;
         sh.f_ver1 = 0u;
+        sh.f_end = 0u;
     }
     __syncthreads();
     STAMP(1);
@@ -771,20 +805,29 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, Scn* s_scn, K1Shared&
         }
     }
     STAMP(2);
-    __syncthreads();
+    if (QSYNC) {
+        // quad workgroup: only the group's own four waves meet before its epilogue (the other
+        // groups of the workgroup finish on their own time); an LDS count instead of the barrier
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) __hip_atomic_fetch_add(&sh.f_end, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        while (__builtin_amdgcn_readfirstlane(*(const volatile LdsU32*)&sh.f_end) < 4u) __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    } else {
+        __syncthreads();
+    }
     STAMP(3);
 
     // ---------------------------------------------------------------- epilogue
     // obs tile: rows [e0, e0+rows) are one contiguous span of global memory (grouped: one
     // contiguous 108-byte row per env)
     if (GRP && !(D2D_ABLATE & 32)) {
-        for (int k = threadIdx.x; k < EPB * D2D_OBS_DIM; k += K1_THREADS) {
+        for (int k = qt; gvalid && k < EPB * D2D_OBS_DIM; k += K1_THREADS) {
             const int r = k / D2D_OBS_DIM;
             const int e = a.lane_env[e0 + r];
             if (e >= 0) a.obs[(size_t)e * D2D_OBS_DIM + (k - r * D2D_OBS_DIM)] = sh.u.p.obs[k];
         }
     } else {
-        const int rows = max(0, min(EPB, a.n - e0));  // (D2D_ABLATE & 32: timing-only slot-order rows)
+        const int rows = gvalid ? max(0, min(EPB, a.n - e0)) : 0;  // (D2D_ABLATE & 32: timing-only slot-order rows)
         const int words = rows * D2D_OBS_DIM;
         float* dst = a.obs + (size_t)e0 * D2D_OBS_DIM;
         // a full tile is 64 x 27 floats = 432 float4 at a 16-B aligned offset (e0 * 108 B, e0 % 64
@@ -793,10 +836,10 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, Scn* s_scn, K1Shared&
         if (D2D_OBS_VEC && rows == EPB && ((uintptr_t)a.obs & 15u) == 0) {
             float4* d4 = reinterpret_cast<float4*>(dst);
             const float4* s4 = reinterpret_cast<const float4*>(sh.u.p.obs);
-            for (int k = threadIdx.x; k < words / 4; k += K1_THREADS) d4[k] = s4[k];
+            for (int k = qt; k < words / 4; k += K1_THREADS) d4[k] = s4[k];
             k0 = words;
         }
-        for (int k = k0 + threadIdx.x; k < words; k += K1_THREADS) dst[k] = sh.u.p.obs[k];
+        for (int k = k0 + qt; k < words; k += K1_THREADS) dst[k] = sh.u.p.obs[k];
     }
     if (wave == 0 && valid) {
         path_err = sh.pe[0][lane];
@@ -853,11 +896,20 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, Scn* s_scn, K1Shared&
     STAMP(6);
 }
 
+template <bool LDS, bool LTAB, bool GRP>
+__device__ __forceinline__ void k1_group(const StepArgs& a, Scn* s_scn, K1Shared& sh, int wg) {
+    const Scn* scns;
+    const BtHot* hots;
+    int s0;
+    k1_stage<LDS, LTAB, GRP>(a, s_scn, wg, scns, hots, s0);
+    k1_body<LDS, LTAB, GRP>(a, scns, hots, s0, sh, wg, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6),
+                            (int)threadIdx.x);
+}
 template <bool LDS, bool LTAB>
 __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
     extern __shared__ __attribute__((aligned(16))) Scn s_scn[];
     __shared__ __attribute__((aligned(16))) K1Shared sh;
-    k1_body<LDS, LTAB, false>(a, s_scn, sh, blockIdx.x);
+    k1_group<LDS, LTAB, false>(a, s_scn, sh, blockIdx.x);
 }
 // grouped slot layout: a pure group stages its scenario and probe table in LDS; a group that
 // straddles two scenarios (at most n_scn - 1 of them: the layout has no padding between scenarios)
@@ -870,11 +922,42 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_grouped_kernel(StepArg
     const int wg = xcd_group(blockIdx.x, gridDim.x);
     const int ws = a.wg_scn[wg];
     if (a.brt && ws >= 0)
-        k1_body<true, true, true>(a, s_scn, sh, wg);
+        k1_group<true, true, true>(a, s_scn, sh, wg);
     else if (D2D_STRADDLE_LDS && ws <= -2)
-        k1_body<true, false, true>(a, s_scn, sh, wg);
+        k1_group<true, false, true>(a, s_scn, sh, wg);
     else
-        k1_body<false, false, true>(a, s_scn, sh, wg);
+        k1_group<false, false, true>(a, s_scn, sh, wg);
+}
+
+// Quad kernel: 16 waves = 4 groups x 4 roles; the QuadDesc tells each wave its quarter and role and
+// which scenarios (+ probe tables) the workgroup stages once for its four groups.  Static LDS 4 x
+// K1Shared + dynamic 4 x (Scn + BtHot): 163 776 of the CU's 163 840 bytes (one workgroup per CU).
+constexpr int QUAD_THREADS = 4 * K1_THREADS;
+template <bool GRP>
+__global__ __launch_bounds__(QUAD_THREADS, 1) void d2d_step_quad_kernel(StepArgs a) {
+    extern __shared__ __attribute__((aligned(16))) Scn q_scn[];  // [4] Scn, then [4] BtHot
+    __shared__ __attribute__((aligned(16))) K1Shared shq[4];
+    const int qi = GRP ? xcd_group(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const QuadDesc& D = a.quad[qi];
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const uint32_t code = (uint32_t)(D.roles >> (4 * w)) & 15u;
+    const int q = __builtin_amdgcn_readfirstlane((int)(code >> 2)), role = __builtin_amdgcn_readfirstlane((int)(code & 3u));
+    Scn* stS = q_scn;
+    BtHot* stH = reinterpret_cast<BtHot*>(q_scn + 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int sj = D.stage[j];
+        if (sj >= 0) {
+            glds_copy<QUAD_THREADS / 64>(stS + j, a.scn + sj, (int)sizeof(Scn));
+            glds_copy<QUAD_THREADS / 64>(stH + j, &a.brt[sj].hot, (int)sizeof(BtHot));
+        }
+    }
+    const int g = D.group[q], sl = D.qslot[q], s0 = D.s0[q];
+    const int qt = role * 64 + lane;
+    if (sl >= 0)  // the quarter's scenarios staged at slots sl (, sl + 1): indexed by global scenario id
+        k1_body<true, true, GRP, true>(a, stS + sl - s0, stH + sl - s0, s0, shq[q], g, role, qt);
+    else
+        k1_body<false, false, GRP, true>(a, a.scn, nullptr, s0, shq[q], g, role, qt);
 }
 
 // ------------------------------------------------------------------------------------------ K2
@@ -1104,8 +1187,15 @@ __device__ __forceinline__ void fill_work(const StepArgs& a) {
 // by a device tick (so a replayed graph alternates too): every workgroup reads ctl[0], workgroup 0
 // writes the next value to ctl[1], and the next K1 launch copies it to ctl[0] -- no workgroup
 // writes what another may still read, and no atomics contend on one address.
+// D2D_FILL_RESIDENT: K4 with K1's residency (4 waves per SIMD, K1's LDS per workgroup: exactly 4
+// workgroups per CU, one round).  K4 (1 024 workgroups at 65 536 envs) otherwise ran 3 per CU and
+// left the CUs' wave-placement rotation uneven, and the next K1 then put two path waves of one CU
+// on one SIMD on a few CUs (+7 us on that step, tools/ubench_after_stamps.py).
+#ifndef D2D_FILL_RESIDENT
+#define D2D_FILL_RESIDENT 1
+#endif
 template <bool LDS>
-__global__ __launch_bounds__(BLOCK) void d2d_fill_kernel(StepArgs a) {
+__global__ __launch_bounds__(BLOCK, D2D_FILL_RESIDENT ? 4 : 1) void d2d_fill_kernel(StepArgs a) {
     const bool ticked = !a.fill_force && a.fill_every > 1;
     bool run = true;
     if (ticked) {

@@ -18,7 +18,7 @@ import torch
 
 from . import abi
 from ._native import check, load
-from .config import CURRICULUM_STAGES, TEST_SCENARIOS, make_cfg
+from .config import CURRICULUM_STAGES, SCENARIO_STEP_COST, TEST_SCENARIOS, make_cfg
 from .scenarios import Scenario, create_test_scenario, free_flight
 
 INFO_KEYS = ("reward", "collision_avoidance_reward", "path_adherence", "path_progression", "collision_reward",
@@ -192,6 +192,10 @@ class Drone2dVecEnv:
         self.env_scenario = es  # in curriculum mode: the initial map only (resets redraw on device)
         check(self._lib.d2d_set_scenarios(self._h, arr, n_scn, es.ctypes.data_as(C.POINTER(C.c_int32))),
               "d2d_set_scenarios")
+        if not self.cfg.scn_pool and n_scn > 1:  # step costs for the quad workgroups' heavy / light pairing
+            cost = (C.c_double * n_scn)(*[SCENARIO_STEP_COST.get(s.name.removesuffix("_free"), 32.0)
+                                          for s in self.scenarios])
+            check(self._lib.d2d_set_scenario_costs(self._h, cost, n_scn), "d2d_set_scenario_costs")
 
     def set_curriculum(self, stage: str | None = None, sim_num: int | None = None, pool: int | None = None,
                        seed: int | None = None) -> torch.Tensor:

@@ -169,6 +169,11 @@ int32_t d2d_n_envs(const d2d_t* h);
  * envs use scenario 0).  (replaces create_test_scenario + QPMI2D fit in init_pymunk, :218-311) */
 int32_t d2d_set_scenarios(d2d_t* h, const d2d_scn* scns, int32_t n_scn, const int32_t* env_scn_host);
 
+/* Relative step cost of each scenario of the last d2d_set_scenarios (test mode; default 1.0 each): the
+ * step kernel's quad workgroups (4 groups of 64 envs, 16 waves, one per CU) pair heavy and light
+ * scenarios on each SIMD by these weights.  Placement only: results do not depend on it.  Synchronises. */
+int32_t d2d_set_scenario_costs(d2d_t* h, const double* cost, int32_t n_scn);
+
 /* Reset the envs whose mask byte is non-zero (mask_dev NULL = all envs) and write their
  * observation rows into obs_dev (float32 [n_envs][27]; NULL = do not write).  Spawn draws come
  * from a counter-based Philox4x32-10 stream keyed by (seed, env id, episode number), so results
