@@ -20,6 +20,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--scenario", default="corridor")
 ap.add_argument("--envs", type=int, default=65536)
 ap.add_argument("--warm", type=int, default=300)
+ap.add_argument("--dump", default="")
 a = ap.parse_args()
 MIXED = ["perpendicular", "parallel", "S_parallel", "corridor", "S_corridor", "large", "impossible"]
 scn = MIXED if a.scenario == "mixed" else a.scenario
@@ -76,4 +77,7 @@ for c in sorted(cu_end, key=cu_end.get)[-3:] + sorted(cu_end, key=cu_end.get)[:1
         desc = ", ".join(f"r{role[w]}:{names[gscn[grp[w]]] if grp[w] >= 0 and gscn[grp[w]] >= 0 else '?'}"
                          f"[{start[w]:.0f}-{end[w]:.0f}]" for w in ws)
         print(f"     simd {sd}: {desc}")
+if a.dump:
+    np.savez(a.dump, block=np.arange(len(s)) // 4, wave=np.arange(len(s)) % 4, cu=cu, simd=simd, role=role, grp=grp,
+             start=start, end=end, gscn=gscn)
 venv.close()
