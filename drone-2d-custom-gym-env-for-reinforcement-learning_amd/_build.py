@@ -36,8 +36,11 @@ def needs_build(out: str = OUT, src: str = SRC, hdrs=None) -> bool:
     return any(os.path.getmtime(p) > t for p in [src, *(HDRS if hdrs is None else hdrs)])
 
 
-# the PPO update is float32 training arithmetic with no reference rounding to follow: contracted FMAs
-PPO_FLAGS = [f if f != "-ffp-contract=off" else "-ffp-contract=fast" for f in HIPCC_FLAGS]
+# the PPO update is float32 training arithmetic with no reference rounding to follow: FMAs contracted
+# within an expression (-ffp-contract=on, which honours `#pragma clang fp contract(off)`: the rollout's
+# GAE recursion keeps torch's operation-by-operation rounding; "fast" fuses across statements in the
+# backend whatever the pragma says)
+PPO_FLAGS = [f if f != "-ffp-contract=off" else "-ffp-contract=on" for f in HIPCC_FLAGS]
 
 
 def _compile(src: str, out: str, verbose: bool, flags=None):

@@ -277,11 +277,14 @@ __device__ __forceinline__ void store_tile(const MlpPair& P, int s0, int m, cons
         }
     }
 }
-__global__ __launch_bounds__(256) void mlp_forward_mfma_kernel(MlpPair P, int m, const int64_t* __restrict__ idx,
-                                                               const float* __restrict__ obs,
-                                                               float* __restrict__ xg,
-                                                               const float* __restrict__ adv,
-                                                               double* __restrict__ ws) {
+__device__ void rollout_epilogue(const d2d_ppo_rollout& R, int m, const float (*outs)[FM_TILES * FM_SPB]);
+// RO: the rollout step (d2d_ppo_rollout_step): rows are the envs in order (idx == nullptr), h1 / h2
+// stay on chip, the outputs go to LDS for the action / GAE epilogue instead of to P.net[].out
+template <bool RO>
+__device__ __forceinline__ void mlp_forward_mfma_body(const MlpPair& P, int m, const int64_t* __restrict__ idx,
+                                                      const float* __restrict__ obs, float* __restrict__ xg,
+                                                      const float* __restrict__ adv, double* __restrict__ ws,
+                                                      const d2d_ppo_rollout* R) {
     // One LDS region, used first to stage both nets' W1 and W2 (read with coalesced loads: the
     // register operands below gathered straight from global memory touch 32 cache lines per
     // instruction, which made the kernel address-bound), then for the inputs and hidden tiles.
@@ -329,7 +332,8 @@ __global__ __launch_bounds__(256) void mlp_forward_mfma_kernel(MlpPair P, int m,
             if (j == 0) w3s[orow][HID] = P.net[on].b3[r];
         }
     }
-    if (tid < FM_TILES * FM_SPB) rows[tid] = sb + tid < m ? idx[sb + tid] : -1;
+    if (tid < FM_TILES * FM_SPB) rows[tid] = sb + tid < m ? (RO ? (int64_t)(sb + tid) : idx[sb + tid]) : -1;
+    __shared__ float outs[RO ? 3 : 1][FM_TILES * FM_SPB];  // RO: mean (2 rows) and value per sample
     const float b1 = N.b1[j0 + ci], b2 = N.b2[j0 + ci];
     __syncthreads();  // weights staged, rows
     static_assert(FM_TILES * FM_SPB == D2D_PPO_HEAD_BLOCK, "one advantage partial per workgroup");
@@ -367,7 +371,7 @@ __global__ __launch_bounds__(256) void mlp_forward_mfma_kernel(MlpPair P, int m,
             if (e < NX) {
                 xs[sl][k] = xv[c];
                 // the gathered minibatch observations, for the weight gradients
-                if (sb + sl < m) xg[(size_t)sb * OBS + e] = xv[c];
+                if (xg != nullptr && sb + sl < m) xg[(size_t)sb * OBS + e] = xv[c];
             }
         }
     }
@@ -386,7 +390,7 @@ __global__ __launch_bounds__(256) void mlp_forward_mfma_kernel(MlpPair P, int m,
             hs[net][i][j0 + ci] = y;
         }
         __syncthreads();
-        store_tile(P, s0, m, hs, tid, false);
+        if (!RO) store_tile(P, s0, m, hs, tid, false);
         // layer 2
         acc = f32x16{};
 #pragma unroll
@@ -400,7 +404,7 @@ __global__ __launch_bounds__(256) void mlp_forward_mfma_kernel(MlpPair P, int m,
             hs[net][i][j0 + ci] = y;
         }
         __syncthreads();
-        store_tile(P, s0, m, hs, tid, true);
+        if (!RO) store_tile(P, s0, m, hs, tid, true);
         // output layers: thread t -> (output row t / 32 of both nets' od0 + od1 rows, sample t % 32),
         // weights and biases from LDS
         if (tid < (od0 + P.net[1].od) * FM_SPB) {
@@ -409,9 +413,133 @@ __global__ __launch_bounds__(256) void mlp_forward_mfma_kernel(MlpPair P, int m,
             float o = w3s[orow][HID];
 #pragma unroll 16
             for (int j = 0; j < HID; ++j) o += w3s[orow][j] * hs[on][sl][j];
-            if (i < m) P.net[on].out[(size_t)i * P.net[on].od + r] = o;
+            if (RO)
+                outs[orow][tile * FM_SPB + sl] = o;
+            else if (i < m)
+                P.net[on].out[(size_t)i * P.net[on].od + r] = o;
         }
     }
+    if (RO) {
+        __syncthreads();
+        if (tid < FM_TILES * FM_SPB) rollout_epilogue(*R, m, outs);  // wave 0: one env per lane
+    }
+}
+__global__ __launch_bounds__(256) void mlp_forward_mfma_kernel(MlpPair P, int m, const int64_t* __restrict__ idx,
+                                                               const float* __restrict__ obs,
+                                                               float* __restrict__ xg,
+                                                               const float* __restrict__ adv,
+                                                               double* __restrict__ ws) {
+    mlp_forward_mfma_body<false>(P, m, idx, obs, xg, adv, ws, nullptr);
+}
+
+// The rollout step's epilogue, lane l of wave 0 = env sb + l.  Operation order as the torch
+// restatement (ppo.py _rollout_body / compute_gae), without contraction: the GAE recursion gives the
+// bits torch computes from the same rewards, values and dones.
+__device__ void rollout_epilogue(const d2d_ppo_rollout& R, int m, const float (*outs)[FM_TILES * FM_SPB]) {
+#pragma clang fp contract(off)
+    const int l = threadIdx.x, i = blockIdx.x * (FM_TILES * FM_SPB) + l, n = m, t = R.t, T = R.T;
+    const bool ok = i < n;
+    float rew_p = 0.0f;
+    uint8_t d_p = 0;
+    if (t > 0) {  // step t-1's env outputs
+        double fin = 0.0, ret = 0.0;
+        if (ok) {
+            rew_p = R.prev_rew[i];
+            d_p = (R.prev_term[i] | R.prev_trunc[i]) != 0;
+            R.rew_buf[(size_t)(t - 1) * n + i] = rew_p;
+            R.done_buf[(size_t)(t - 1) * n + i] = d_p;
+            if (d_p) {
+                fin = 1.0;
+                if (R.prev_info != nullptr) ret = (double)R.prev_info[(size_t)i * R.info_dim + R.info_totrew];
+            }
+        }
+        fin = wave_sum(fin);
+        ret = wave_sum(ret);
+        if (l == 0) {
+            double* st = R.stats + ((size_t)(t - 1) * gridDim.x + blockIdx.x) * 2;
+            st[0] = fin;
+            st[1] = ret;
+        }
+    }
+    if (!ok) return;
+    const float v = outs[2][l];
+    if (t < T) {
+        const size_t row = (size_t)t * n + i;
+        const float ls0 = R.log_std[0], ls1 = R.log_std[1];
+        const float mu0 = outs[0][l], mu1 = outs[1][l];
+        const float a0 = mu0 + expf(ls0) * R.noise[2 * i], a1 = mu1 + expf(ls1) * R.noise[2 * i + 1];
+        const float z0 = (a0 - mu0) * expf(-ls0), z1 = (a1 - mu1) * expf(-ls1);
+        const float lp = ((-0.5f * z0 * z0 - ls0) - HALF_LOG_2PI) + ((-0.5f * z1 * z1 - ls1) - HALF_LOG_2PI);
+        R.act_buf[2 * row] = a0;
+        R.act_buf[2 * row + 1] = a1;
+        R.logp_buf[row] = lp;
+        R.val_buf[row] = v;
+        R.act_env[2 * i] = fminf(fmaxf(a0, -1.0f), 1.0f);
+        R.act_env[2 * i + 1] = fminf(fmaxf(a1, -1.0f), 1.0f);
+        return;
+    }
+    // t == T: GAE (RolloutBuffer.compute_returns_and_advantage); episode start of step s + 1 = done of s
+    const float g = R.gamma, gl = R.gae_lambda_gamma;
+    float last_gae = 0.0f, next_v = v;
+    for (int s = T - 1; s >= 0; --s) {
+        const size_t row = (size_t)s * n + i;
+        const float vs = R.val_buf[row];
+        const float rs = s == T - 1 ? rew_p : R.rew_buf[row];
+        const float nnt = 1.0f - (float)(s == T - 1 ? d_p : R.done_buf[row]);
+        const float delta = (rs + g * next_v * nnt) - vs;
+        last_gae = delta + gl * nnt * last_gae;
+        R.adv_buf[row] = last_gae;
+        R.ret_buf[row] = last_gae + vs;
+        next_v = vs;
+    }
+    R.start0[i] = d_p;
+}
+__global__ __launch_bounds__(256) void rollout_step_kernel(MlpPair P, int m, float* __restrict__ xg, d2d_ppo_rollout R) {
+    mlp_forward_mfma_body<true>(P, m, nullptr, R.obs, xg, nullptr, nullptr, &R);
+}
+
+// ---------------------------------------------------------------- per-epoch minibatch shuffles
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {  // the splitmix64 finaliser
+    z ^= z >> 30;
+    z *= 0xbf58476d1ce4e5b9ull;
+    z ^= z >> 27;
+    z *= 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+// x = (a << wb) | b on `bits` bits; a round maps (a, b) -> (b, a ^ F(b)) and swaps the widths, so
+// every round (and the network) is a bijection of [0, 2^bits)
+__device__ __forceinline__ uint64_t feistel(uint64_t x, int bits, const uint64_t (&key)[8]) {
+    int wa = bits / 2, wb = bits - wa;
+    uint64_t a = x >> wb, b = x & ((1ull << wb) - 1);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+        const uint64_t f = mix64(b ^ key[r]) & ((1ull << wa) - 1);
+        const uint64_t na = b;
+        b = a ^ f;
+        a = na;
+        const int tw = wa;
+        wa = wb;
+        wb = tw;
+    }
+    return (a << wb) | b;
+}
+__global__ __launch_bounds__(256) void permute_kernel(int64_t n, int bits, uint64_t seed,
+                                                      const uint64_t* __restrict__ counter,
+                                                      int64_t* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t e = counter[0] + blockIdx.y;
+    uint64_t key[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) key[r] = mix64(seed ^ mix64(e * 8 + r + 0x5045524d00000000ull));  // "PERM"
+    uint64_t x = (uint64_t)i;
+    do {
+        x = feistel(x, bits, key);
+    } while (x >= (uint64_t)n);  // cycle walking: ends inside [0, n) (i's cycle holds i)
+    out[(int64_t)blockIdx.y * n + i] = (int64_t)x;
+}
+__global__ void counter_add_kernel(uint64_t* c, uint64_t k) {
+    if (threadIdx.x == 0) c[0] += k;
 }
 
 // the loss head (policy: the clipped surrogate's d/d mean; value: the squared error's d/d V) and the
@@ -1077,6 +1205,41 @@ int32_t d2d_ppo_mlp_forward(int32_t m, const int64_t* idx, const float* obs, con
 }
 
 int32_t d2d_ppo_mlp_partial_rows(int32_t m) { return 2 * ((m + MLP_SPB - 1) / MLP_SPB); }
+
+int32_t d2d_ppo_permute(int64_t n, int32_t n_perm, uint64_t seed, uint64_t* counter, int64_t* out, void* stream) {
+    if (n <= 0 || n_perm <= 0) return 0;
+    if (counter == nullptr || out == nullptr || n > ((int64_t)1 << 40) || n_perm > 65535)
+        return (int32_t)hipErrorInvalidValue;
+    int bits = 0;
+    while (((int64_t)1 << bits) < n) ++bits;
+    hipLaunchKernelGGL(permute_kernel, dim3((unsigned)((n + 255) / 256), (unsigned)n_perm), dim3(256), 0,
+                       (hipStream_t)stream, n, bits, seed, counter, out);
+    hipLaunchKernelGGL(counter_add_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, counter, (uint64_t)n_perm);
+    return rc(hipGetLastError());
+}
+
+int32_t d2d_ppo_rollout_step(const d2d_ppo_rollout* r, const float* const* weights, void* stream) {
+    if (r == nullptr || weights == nullptr) return (int32_t)hipErrorInvalidValue;
+    const d2d_ppo_rollout& R = *r;
+    if (R.n <= 0) return 0;
+    if (R.T <= 0 || R.t < 0 || R.t > R.T || R.obs == nullptr || R.log_std == nullptr || R.val_buf == nullptr)
+        return (int32_t)hipErrorInvalidValue;
+    if (R.t < R.T && (R.noise == nullptr || R.obs_buf == nullptr || R.act_buf == nullptr || R.logp_buf == nullptr ||
+                      R.act_env == nullptr))
+        return (int32_t)hipErrorInvalidValue;
+    if (R.t > 0 && (R.prev_rew == nullptr || R.prev_term == nullptr || R.prev_trunc == nullptr ||
+                    R.rew_buf == nullptr || R.done_buf == nullptr || R.stats == nullptr ||
+                    (R.prev_info != nullptr && (R.info_totrew < 0 || R.info_totrew >= R.info_dim))))
+        return (int32_t)hipErrorInvalidValue;
+    if (R.t == R.T && (R.adv_buf == nullptr || R.ret_buf == nullptr || R.start0 == nullptr))
+        return (int32_t)hipErrorInvalidValue;
+    float* none[10] = {};
+    MlpPair P = make_pair(weights, none);
+    float* xg = R.t < R.T ? R.obs_buf + (size_t)R.t * R.n * OBS : nullptr;
+    hipLaunchKernelGGL(rollout_step_kernel, dim3((R.n + FM_TILES * FM_SPB - 1) / (FM_TILES * FM_SPB)), dim3(256), 0,
+                       (hipStream_t)stream, P, R.n, xg, R);
+    return rc(hipGetLastError());
+}
 
 int32_t d2d_ppo_mlp_backward(int32_t m, const int64_t* idx, const float* act, const float* old_logp, const float* adv,
                              const float* ret, const float* log_std, const double* ws, int32_t normalize, float clip,

@@ -120,6 +120,17 @@ class ActorCritic(nn.Module):
 
 _PPO_LIB = None
 
+import ctypes as _C  # noqa: E402
+
+
+class D2DPPORollout(_C.Structure):
+    """include/d2d_ppo.h ``d2d_ppo_rollout`` (one fused rollout step, ABI v4)."""
+    _fields_ = [(k, _C.c_int32) for k in ("n", "t", "T", "info_dim", "info_totrew")] + \
+               [("gamma", _C.c_float), ("gae_lambda_gamma", _C.c_float), ("pad", _C.c_int32)] + \
+               [(k, _C.c_void_p) for k in ("obs", "noise", "log_std", "prev_rew", "prev_term", "prev_trunc",
+                                           "prev_info", "obs_buf", "act_buf", "logp_buf", "val_buf", "rew_buf",
+                                           "done_buf", "start0", "act_env", "adv_buf", "ret_buf", "stats")]
+
 
 def ppo_native():
     """ctypes binding of libd2d_ppo.so (include/d2d_ppo.h), loaded once; no fallback on a GPU."""
@@ -154,11 +165,13 @@ def ppo_native():
             "d2d_ppo_mlp_forward_adv": [i32, vp, vp, vp, vp, vp, vp, vp, vp],
             "d2d_ppo_mlp_backward": [i32, vp, vp, vp, vp, vp, vp, vp, i32, f32, f32, vp, vp, vp, vp, vp],
             "d2d_ppo_mlp_partial_rows": [i32],
+            "d2d_ppo_permute": [i64, i32, C.c_uint64, vp, vp, vp],
+            "d2d_ppo_rollout_step": [C.POINTER(D2DPPORollout), vp, vp],
         }
         for name, args in sig.items():
             fn = getattr(lib, name)
             fn.restype, fn.argtypes = C.c_int32, args
-        if lib.d2d_ppo_abi_version() != 3:
+        if lib.d2d_ppo_abi_version() != 4:
             raise RuntimeError("libd2d_ppo.so ABI mismatch")
         _PPO_LIB = lib
     return _PPO_LIB
@@ -291,9 +304,7 @@ class ManualStep:
             self._bufs[M] = (hb, prow)
         hb, prow = self._bufs[M]
         pn, vn = pol.mlp_extractor.policy_net, pol.mlp_extractor.value_net
-        ws = [pn[0].weight, pn[0].bias, pn[2].weight, pn[2].bias, pol.action_net.weight, pol.action_net.bias,
-              vn[0].weight, vn[0].bias, vn[2].weight, vn[2].bias, pol.value_net.weight, pol.value_net.bias]
-        wptr = (C.c_void_p * 12)(*[w.data_ptr() for w in ws])
+        wptr = self.weight_ptrs()
         bptr = (C.c_void_p * 10)(*[hb[k].data_ptr() for k in ("h1p", "h2p", "mean", "g1p", "g2p",
                                                               "h1v", "h2v", "val", "g1v", "g2v")])
         gptr = (C.c_void_p * 2)(hb["gm"].data_ptr(), hb["gv"].data_ptr())
@@ -315,6 +326,17 @@ class ManualStep:
                 acc["policy_loss"].data_ptr(), acc["value_loss"].data_ptr(), acc["entropy"].data_ptr(),
                 acc["clip_fraction"].data_ptr())
         self._wgrad_hip(M, layers, hb["wpart"], head, adam)
+
+    def weight_ptrs(self):
+        """The 12 weight / bias device pointers of include/d2d_ppo.h (policy net, then value net);
+        views of the flat parameter buffer, so the addresses never change."""
+        import ctypes as C
+
+        pol = self.pol
+        pn, vn = pol.mlp_extractor.policy_net, pol.mlp_extractor.value_net
+        ws = [pn[0].weight, pn[0].bias, pn[2].weight, pn[2].bias, pol.action_net.weight, pol.action_net.bias,
+              vn[0].weight, vn[0].bias, vn[2].weight, vn[2].bias, pol.value_net.weight, pol.value_net.bias]
+        return (C.c_void_p * 12)(*[w.data_ptr() for w in ws])
 
     @staticmethod
     def _tanh_grad_torch(h, g):
@@ -471,19 +493,79 @@ class PPO:
         self._ro_graph = None    # the captured rollout (GPU)
         self._ro_warm = False
         self._ro_gen = None      # the env's generation the rollout graph was captured against
+        # the libd2d_ppo.so path (GPU, ManualStep): the epochs' shuffles from d2d_ppo_permute (a device
+        # counter keys them, so the whole update -- shuffles and every minibatch step -- replays as one
+        # HIP graph) and the rollout as one fused launch per step (d2d_ppo_rollout_step)
+        self._hip = self.manual is not None and self.manual.lib is not None
+        self._perm = None
+        self._perm_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+        self._perm_seed = (seed * 0x9E3779B97F4A7C15 + rank * 0xD1B54A32D192ED03 + 1) % (1 << 64)
+        self._upd_warm = False
+        self._fused = None       # decided at the first rollout (_alloc_rollout)
 
     # ------------------------------------------------------------------ rollout
     def _alloc_rollout(self):
+        from .env import Drone2dVecEnv
+
         T, N, dev = self.cfg.n_steps, self.n_envs, self.device
         f64 = dict(dtype=torch.float64, device=dev)
-        self._ro = {"obs": torch.empty(T + 1, N, 27, device=dev), "act": torch.empty(T, N, 2, device=dev),
-                    "logp": torch.empty(T, N, device=dev), "val": torch.empty(T, N, device=dev),
-                    "rew": torch.empty(T, N, device=dev), "done": torch.empty(T, N, dtype=torch.bool, device=dev),
+        # time-limit truncations are bootstrapped with V(terminal obs); the reference never truncates
+        self._truncates = bool(getattr(getattr(self.venv, "cfg", None), "timeup_truncates", 1))
+        # the fused rollout: the HIP env batch, no truncation bootstrap (its extra value pass stays in torch)
+        self._fused = bool(self._hip and isinstance(self.venv, Drone2dVecEnv) and not self._truncates)
+        self._ro = {"val": torch.empty(T, N, device=dev), "rew": torch.empty(T, N, device=dev),
+                    "done": torch.empty(T, N, dtype=torch.bool, device=dev),
                     "start0": torch.empty(N, dtype=torch.bool, device=dev),
                     "noise": torch.empty(T, N, 2, device=dev), "fin": torch.zeros((), **f64),
                     "ret": torch.zeros((), **f64)}
-        # time-limit truncations are bootstrapped with V(terminal obs); the reference never truncates
-        self._truncates = bool(getattr(getattr(self.venv, "cfg", None), "timeup_truncates", 1))
+        if self._fused:
+            self._ro["act_env"] = torch.empty(N, 2, device=dev)
+            self._ro["stats"] = torch.zeros(T, (N + 63) // 64, 2, **f64)
+            self._ro["obs_cur"] = None
+        else:
+            self._ro.update(obs=torch.empty(T + 1, N, 27, device=dev), act=torch.empty(T, N, 2, device=dev),
+                            logp=torch.empty(T, N, device=dev))
+
+    def _set_first_obs(self, obs):
+        if self._fused:
+            self._ro["obs_cur"] = obs  # the env's output tensor; the fused step reads it in place
+        else:
+            self._ro["obs"][0].copy_(obs.to(self.device))
+        self._ro["start0"].fill_(True)
+
+    @torch.no_grad()
+    def _rollout_body_fused(self):
+        """_rollout_body as T + 1 libd2d_ppo.so launches around the T env steps: step t's launch runs
+        both MLPs on the env's observation tensor, samples and stores the action, log-density and
+        value, copies the observations into the flat buffer and records step t-1's reward / done /
+        episode statistics; the last one adds the bootstrap value and GAE (d2d_ppo_rollout_step)."""
+        import ctypes as C
+
+        from . import abi
+
+        R, T, N, lib = self._ro, self.cfg.n_steps, self.n_envs, self.manual.lib
+        st = self.manual._stream()
+        wptr = self.manual.weight_ptrs()
+        obs_buf, act_buf, logp_buf, adv_buf, ret_buf = self._flat
+        ptr = lambda x: x.data_ptr() if x is not None else None  # noqa: E731
+        r = D2DPPORollout(n=N, T=T, info_dim=abi.INFO_DIM, info_totrew=abi.INFO_TOTREW, gamma=self.cfg.gamma,
+                          gae_lambda_gamma=self.cfg.gamma * self.cfg.gae_lambda,
+                          log_std=ptr(self.policy.log_std), obs_buf=ptr(obs_buf), act_buf=ptr(act_buf),
+                          logp_buf=ptr(logp_buf), val_buf=ptr(R["val"]), rew_buf=ptr(R["rew"]),
+                          done_buf=ptr(R["done"]), start0=ptr(R["start0"]), act_env=ptr(R["act_env"]),
+                          adv_buf=ptr(adv_buf), ret_buf=ptr(ret_buf), stats=ptr(R["stats"]))
+        obs = R["obs_cur"]
+        for t in range(T + 1):
+            r.t = t
+            r.obs = ptr(obs)
+            r.noise = ptr(R["noise"][t]) if t < T else None
+            _ok(lib.d2d_ppo_rollout_step(C.byref(r), wptr, st), "d2d_ppo_rollout_step")
+            if t < T:
+                obs, rew, term, trunc, info = self.venv.step(R["act_env"])
+                r.prev_rew, r.prev_term, r.prev_trunc, r.prev_info = ptr(rew), ptr(term), ptr(trunc), ptr(info)
+        R["obs_cur"] = obs  # T even: the same double-buffer slot as at the start
+        R["fin"].copy_(R["stats"][..., 0].sum())
+        R["ret"].copy_(R["stats"][..., 1].sum())
 
     @torch.no_grad()
     def _rollout_body(self):
@@ -535,14 +617,13 @@ class PPO:
             # and start the next rollout from a reset
             self._ro_graph = None
             self._ro_warm = False
-            self._ro["obs"][0].copy_(self.venv.reset().to(self.device))
-            self._ro["start0"].fill_(True)
+            self._set_first_obs(self.venv.reset())
         self._ro_gen = gen
         if self._ro is None:
             self._alloc_rollout()
-            self._ro["obs"][0].copy_(self.venv.reset().to(self.device))
-            self._ro["start0"].fill_(True)
+            self._set_first_obs(self.venv.reset())
         R = self._ro
+        body = self._rollout_body_fused if self._fused else self._rollout_body
         R["fin"].zero_()
         R["ret"].zero_()
         torch.randn(R["noise"].shape, generator=self.gen, device=self.device, out=R["noise"])
@@ -556,12 +637,12 @@ class PPO:
             torch.cuda.synchronize(self.device)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                self._rollout_body()
+                body()
             self._ro_graph = g
         if self._ro_graph is not None:
             self._ro_graph.replay()
         else:
-            self._rollout_body()
+            body()
             self._ro_warm = True
         self.num_timesteps += T * N
         f, r = float(R["fin"]), float(R["ret"])
@@ -622,8 +703,39 @@ class PPO:
             self._acc[k].copy_(v)
         self._graph = g
 
+    def _train_body_hip(self):
+        """One update on the libd2d_ppo.so path: the n_epochs shuffles in one launch
+        (d2d_ppo_permute), then every minibatch step; nothing waits for the host, so on one rank the
+        whole update is captured and replayed as one HIP graph."""
+        M, bs, E = self._flat[0].shape[0], self.cfg.batch_size, self.cfg.n_epochs
+        for v in self._acc.values():
+            v.zero_()
+        _ok(self.manual.lib.d2d_ppo_permute(M, E, self._perm_seed, self._perm_ctr.data_ptr(), self._perm.data_ptr(),
+                                            self.manual._stream()), "d2d_ppo_permute")
+        for e in range(E):
+            for s in range(0, M, bs):
+                self._minibatch(self._perm[e * M + s:e * M + min(s + bs, M)])
+
     def train(self) -> dict:
         M, bs = self._flat[0].shape[0], self.cfg.batch_size
+        if self._hip:
+            if self._perm is None:
+                self._perm = torch.empty(self.cfg.n_epochs * M, dtype=torch.int64, device=self.device)
+            if self.use_graph and self._graph is None and self._upd_warm:
+                # second update: capture the whole update (the first ran eagerly: kernels loaded, every
+                # minibatch size's work buffers allocated)
+                torch.cuda.synchronize(self.device)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self._train_body_hip()
+                self._graph = g
+            if self._graph is not None:
+                self._graph.replay()
+            else:
+                self._train_body_hip()
+                self._upd_warm = True
+            n_upd = self.cfg.n_epochs * -(-M // bs)
+            return {k: float(v) / n_upd for k, v in self._acc.items()}
         for v in self._acc.values():
             v.zero_()
         n_upd = 0

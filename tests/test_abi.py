@@ -27,9 +27,13 @@ def test_header_declares_expected_api():
 
 def test_struct_layout_matches_ctypes(tmp_path, d2):
     from drone2d_amd import abi
+    from drone2d_amd.ppo import D2DPPORollout
 
-    prog = ["#include <stdio.h>", "#include <stddef.h>", f'#include "{HEADER}"', "int main(void){"]
-    structs = (("d2d_cfg", abi.D2DCfg), ("d2d_scn", abi.D2DScn), ("d2d_curriculum", abi.D2DCurriculum))
+    ppo_h = os.path.join(REPO, "include", "d2d_ppo.h")
+    prog = ["#include <stdio.h>", "#include <stddef.h>", f'#include "{HEADER}"', f'#include "{ppo_h}"',
+            "int main(void){"]
+    structs = (("d2d_cfg", abi.D2DCfg), ("d2d_scn", abi.D2DScn), ("d2d_curriculum", abi.D2DCurriculum),
+               ("d2d_ppo_rollout", D2DPPORollout))
     for cname, cls in structs:
         prog.append(f'printf("{cname} %zu\\n", sizeof({cname}));')
         for fname, _ in cls._fields_:
@@ -179,8 +183,16 @@ def test_ppo_library_exports_every_header_symbol(d2):
     for f in fns:
         assert hasattr(lib, f), f
         assert getattr(lib, f).argtypes is not None, f  # declared in ppo_native's signatures
-    assert lib.d2d_ppo_abi_version() == 3
+    assert lib.d2d_ppo_abi_version() == 4
     assert b"gfx950" in open(_build.PPO_OUT, "rb").read()
+    # v4: the shuffles and the fused rollout step check their arguments before any launch
+    assert lib.d2d_ppo_permute(0, 3, 1, None, None, None) == 0
+    assert lib.d2d_ppo_permute(100, 3, 1, None, None, None) == 1
+    r = ppo.D2DPPORollout(n=64, t=0, T=16)
+    assert lib.d2d_ppo_rollout_step(C.byref(r), None, None) == 1
+    assert lib.d2d_ppo_rollout_step(C.byref(r), (C.c_void_p * 12)(), None) == 1  # no obs / buffers
+    r.n = 0
+    assert lib.d2d_ppo_rollout_step(C.byref(r), (C.c_void_p * 12)(), None) == 0
     # out-of-range shapes are refused (hipErrorInvalidValue = 1) without a launch
     assert lib.d2d_ppo_adam(0, None, None, None, None, None, 1e-3, 0.9, 0.999, 1e-5, 0.5, None) == 0  # no launch
     assert lib.d2d_ppo_adam(1 << 20, None, None, None, None, None, 1e-3, 0.9, 0.999, 1e-5, 0.5, None) == 1

@@ -82,8 +82,8 @@ def test_ppo_on_hip_batch(d2):
 @pytest.mark.gpu
 @pytest.mark.parametrize("bs", [4096, 12288])
 def test_ppo_graph_update_matches_eager(d2, bs):
-    """The HIP-graph replayed minibatch step computes what the eager step computes (bs = 12288:
-    every epoch ends with a ragged 8 192-sample minibatch that runs eagerly between replays)."""
+    """The HIP-graph replayed update (shuffles + every minibatch step) computes what the eager update
+    computes (bs = 12288: every epoch ends with a ragged 8 192-sample minibatch)."""
     from drone2d_amd.ppo import PPO, PPOConfig
 
     params = []
@@ -93,7 +93,7 @@ def test_ppo_graph_update_matches_eager(d2, bs):
         cfg.graph = graph
         algo = PPO(venv, cfg, seed=0)
         assert algo.use_graph == graph
-        hist = algo.learn(8 * 4096)
+        hist = algo.learn(3 * 8 * 4096)  # the first update runs eagerly, the next two replay the graph
         assert (algo._graph is not None) == graph and np.isfinite(hist[-1]["value_loss"])
         params.append([p.detach().clone() for p in algo.policy.parameters()])
         venv.close()
@@ -263,3 +263,118 @@ def test_rollout_graph_matches_eager(d2):
         for a, b in zip(fa, fb):
             assert torch.equal(a, b)
         assert sa["episodes"] == sb["episodes"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 5, 1000, 32775, 1 << 20])
+def test_permute_gives_permutations(d2, n):
+    """d2d_ppo_permute: every epoch's row is a permutation of [0, n), the epochs differ, and the
+    device counter advances so the next call (a graph replay) draws new shuffles."""
+    from drone2d_amd.ppo import ppo_native
+
+    lib = ppo_native()
+    E = 3
+    ctr = torch.zeros(1, dtype=torch.int64, device="cuda")
+    out = torch.empty(E * n, dtype=torch.int64, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    assert lib.d2d_ppo_permute(n, E, 12345, ctr.data_ptr(), out.data_ptr(), st) == 0
+    first = out.clone()
+    assert lib.d2d_ppo_permute(n, E, 12345, ctr.data_ptr(), out.data_ptr(), st) == 0
+    torch.cuda.synchronize()
+    assert int(ctr) == 2 * E
+    ar = torch.arange(n, device="cuda")
+    for rows in (first, out):
+        for e in range(E):
+            assert torch.equal(torch.sort(rows[e * n:(e + 1) * n]).values, ar)
+    if n >= 1000:
+        assert not torch.equal(first[:n], first[n:2 * n]) and not torch.equal(first, out)
+        # a shuffle, not a shift: the first half of a permutation holds about half of every residue
+        lo = first[:n // 2]
+        assert abs(float((lo < n // 2).float().mean()) - 0.5) < 0.06
+
+
+def _torch_policy_step(pol, obs, noise):
+    with torch.no_grad():
+        mean, value = pol(obs)
+        act = mean + pol.log_std.exp() * noise
+        return act, pol.log_prob(mean, act), value
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [37, 4096, 65536 + 100])
+def test_rollout_step_matches_torch(d2, n):
+    """d2d_ppo_rollout_step against the torch restatement (ppo.py _rollout_body, compute_gae): step
+    0's actions / log-densities / values / clipped env actions / observation copy, step t's record
+    of step t-1's rewards, dones and episode statistics, and step T's bootstrap value + GAE (bit for
+    bit where the bootstrap value drops out, to the MLP's float tolerance where it enters)."""
+    import ctypes as C
+
+    from drone2d_amd import abi
+    from drone2d_amd.ppo import ActorCritic, D2DPPORollout, ManualStep, PPOConfig, compute_gae
+
+    torch.manual_seed(0)
+    pol = ActorCritic()
+    with torch.no_grad():
+        pol.log_std.copy_(torch.tensor([-0.4, 0.3]))
+        pol.action_net.weight.mul_(60.0)  # actions beyond [-1, 1]: the clip is exercised
+    pol = pol.cuda()
+    man = ManualStep(pol, PPOConfig(), "cuda")
+    g = torch.Generator(device="cuda").manual_seed(1)
+    T = 4
+    obs = torch.rand(n, 27, device="cuda", generator=g) * 2 - 1
+    noise = torch.randn(T, n, 2, device="cuda", generator=g)
+    f = lambda *sh, dt=torch.float32: torch.full(sh, float("nan"), device="cuda").to(dt)  # noqa: E731
+    obs_buf, act_buf, logp_buf, val_buf, rew_buf = f(T, n, 27), f(T, n, 2), f(T, n), f(T, n), f(T, n)
+    adv_buf, ret_buf, act_env = f(T, n), f(T, n), f(n, 2)
+    done_buf = torch.zeros(T, n, dtype=torch.bool, device="cuda")
+    start0 = torch.ones(n, dtype=torch.bool, device="cuda")
+    stats = torch.zeros(T, (n + 63) // 64, 2, dtype=torch.float64, device="cuda")
+    ptr = lambda x: x.data_ptr() if x is not None else None  # noqa: E731
+    cfg = PPOConfig()
+    r = D2DPPORollout(n=n, T=T, info_dim=abi.INFO_DIM, info_totrew=abi.INFO_TOTREW, gamma=cfg.gamma,
+                      gae_lambda_gamma=cfg.gamma * cfg.gae_lambda, log_std=ptr(pol.log_std), obs_buf=ptr(obs_buf),
+                      act_buf=ptr(act_buf), logp_buf=ptr(logp_buf), val_buf=ptr(val_buf), rew_buf=ptr(rew_buf),
+                      done_buf=ptr(done_buf), start0=ptr(start0), act_env=ptr(act_env), adv_buf=ptr(adv_buf),
+                      ret_buf=ptr(ret_buf), stats=ptr(stats))
+    st = torch.cuda.current_stream().cuda_stream
+    lib = man.lib
+    # step 0 (no previous step)
+    r.t, r.obs, r.noise = 0, ptr(obs), ptr(noise[0])
+    assert lib.d2d_ppo_rollout_step(C.byref(r), man.weight_ptrs(), st) == 0
+    a_ref, lp_ref, v_ref = _torch_policy_step(pol, obs, noise[0])
+    torch.cuda.synchronize()
+    assert torch.equal(obs_buf[0], obs)
+    torch.testing.assert_close(act_buf[0], a_ref, rtol=1e-5, atol=2e-5)
+    torch.testing.assert_close(logp_buf[0], lp_ref, rtol=1e-5, atol=2e-5)
+    torch.testing.assert_close(val_buf[0], v_ref, rtol=1e-5, atol=2e-5)
+    assert torch.equal(act_env, act_buf[0].clamp(-1.0, 1.0))
+    frac = float((act_buf[0].abs() > 1).float().mean())
+    assert n < 1000 or 0.05 < frac < 0.95
+    # steps 1 .. T-1: each records its predecessor's env outputs
+    rews = torch.randn(T, n, device="cuda", generator=g)
+    terms = torch.rand(T, n, device="cuda", generator=g) < 0.2
+    truncs = torch.rand(T, n, device="cuda", generator=g) < 0.05
+    info = torch.randn(T, n, abi.INFO_DIM, device="cuda", generator=g)
+    for t in range(1, T + 1):
+        o = obs if t < T else torch.rand(n, 27, device="cuda", generator=g)
+        r.t, r.obs, r.noise = t, ptr(o), ptr(noise[t]) if t < T else None
+        r.prev_rew, r.prev_term, r.prev_trunc, r.prev_info = (ptr(rews[t - 1]), ptr(terms[t - 1]),
+                                                             ptr(truncs[t - 1]), ptr(info[t - 1]))
+        assert lib.d2d_ppo_rollout_step(C.byref(r), man.weight_ptrs(), st) == 0
+    torch.cuda.synchronize()
+    dones = terms | truncs
+    assert torch.equal(rew_buf, rews) and torch.equal(done_buf, dones)
+    assert torch.equal(start0, dones[T - 1])
+    ep = stats.sum(1)
+    assert torch.equal(ep[:, 0], dones.sum(1).double())
+    ret_ref = torch.where(dones, info[..., abi.INFO_TOTREW].double(), 0.0).sum(1)
+    torch.testing.assert_close(ep[:, 1], ret_ref, rtol=1e-12, atol=1e-9)
+    # GAE against compute_gae on the kernel's own values
+    last_v = _torch_policy_step(pol, o, noise[0])[2]
+    starts = torch.cat([torch.ones(1, n, dtype=torch.bool, device="cuda"), dones[:-1]])
+    adv_ref, ret_ref = compute_gae(rew_buf, val_buf, starts, last_v, dones[T - 1], cfg.gamma, cfg.gae_lambda)
+    torch.testing.assert_close(adv_buf, adv_ref, rtol=1e-5, atol=2e-5)
+    torch.testing.assert_close(ret_buf, ret_ref, rtol=1e-5, atol=2e-5)
+    # where step T-1 ended the episode, the bootstrap value drops out: same bits as torch
+    d = dones[T - 1]
+    assert torch.equal(adv_buf[:, d], adv_ref[:, d]) and torch.equal(ret_buf[:, d], ret_ref[:, d])

@@ -30,7 +30,7 @@ def main():
     ap.add_argument("--epochs", type=int, default=10)
     ap.add_argument("--scenario", default="corridor")
     ap.add_argument("--curriculum", action="store_true")
-    ap.add_argument("--pool", type=int, default=4096)
+    ap.add_argument("--pool", type=int, default=4096, help="curriculum pool size; 0: the fresh curriculum")
     ap.add_argument("--refresh", type=int, default=100, help="updates between curriculum pool refreshes")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--no-graph", action="store_true", help="eager minibatch updates (A/B against the HIP graph)")
@@ -46,8 +46,9 @@ def main():
     torch.cuda.set_device(0)
     kw = dict(ENV_TRAIN_CONFIG, scenario=a.scenario)
     if a.curriculum:
-        kw.update(mode="curriculum", scenario="curriculum", sim_num=0, curriculum_pool=a.pool,
-                  curriculum_seed=a.seed)
+        kw.update(mode="curriculum", scenario="curriculum", sim_num=0, curriculum_seed=a.seed)
+        if a.pool > 0:  # a host-generated pool; --pool 0: every reset on a fresh device-generated scenario
+            kw["curriculum_pool"] = a.pool
     venv = d2.Drone2dVecEnv(a.envs, seed=a.seed, **kw)
     cfg = PPOConfig.gpu_defaults(n_steps=a.n_steps, batch_size=a.batch, n_epochs=a.epochs)
     cfg.graph = not a.no_graph
@@ -58,7 +59,7 @@ def main():
     out = open(os.path.join(REPO, "gpurun_out", f"ppo{tag}.jsonl"), "w")
     t0 = time.perf_counter()
     for u in range(a.updates):
-        if a.curriculum and u and u % a.refresh == 0:
+        if a.curriculum and a.pool > 0 and u and u % a.refresh == 0:
             # the reference's stage clock is the global step count (checkpoint names, :76-86)
             venv.refresh_curriculum(sim_num=algo.num_timesteps)
         rec = algo.learn(algo.num_timesteps + a.n_steps * a.envs)[-1]
