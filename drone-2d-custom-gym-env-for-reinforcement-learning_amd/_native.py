@@ -34,6 +34,8 @@ SIGNATURES = {
     "d2d_episode_stats": (C.c_int32, [_VP, _VP, C.c_int32, _VP]),
     "d2d_selftest": (C.c_int32, [C.c_int32, C.c_int64, C.c_uint64, C.POINTER(C.c_uint64)]),
     "d2d_group_layout": (C.c_int32, [C.c_int32, _VP, C.c_int32, _VP, _VP]),
+    "d2d_get_group_layout": (C.c_int32, [_VP, _VP, _VP]),
+    "d2d_balanced_group_layout": (C.c_int32, [C.c_int32, _VP, C.c_int32, _VP, C.c_int32, _VP, _VP]),
     "d2d_pool_state": (C.c_int32, [_VP, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "d2d_restore_pool": (C.c_int32, [_VP, C.POINTER(abi.D2DScn), C.c_int32, C.c_int32, C.c_int32]),
     "d2d_set_curriculum": (C.c_int32, [_VP, C.POINTER(abi.D2DCurriculum)]),

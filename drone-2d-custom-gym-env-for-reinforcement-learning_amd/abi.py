@@ -7,7 +7,7 @@ from __future__ import annotations
 
 import ctypes as C
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 MAX_WPS = 16
 MAX_SEGS = MAX_WPS - 2

@@ -285,6 +285,74 @@ hipError_t rc_rebuild(d2d_t* h, hipStream_t stream) {
 // of three or more (everything through L1/L2).  Groups are then
 // ordered by their first env id, so groups whose envs interleave (e.g. scenario = id mod 7) get
 // consecutive numbers (xcd_group places consecutive numbers on one XCD).
+// host copy of the kernels' block -> group numbering (d2d_kernels.h xcd_group)
+int xcd_group_host(int b, int nb) {
+    const int per = nb / 8, rem = nb % 8, x = b % 8, k = b / 8;
+    return (x < rem) ? x * (per + 1) + k : rem * (per + 1) + (x - rem) * per + k;
+}
+// Co-residency balance (mixed batches).  When every workgroup of K1 is resident at once (ng <= 4 x
+// CUs), the dispatcher fills the CUs round by round in one fixed CU order, so blocks b, b + n_cu,
+// b + 2 n_cu, ... share a CU (measured on MI355X: blocks congruent mod 256 share a CU, in every step
+// of a replayed graph, tools/cu_map.py).  A step lasts as long as its slowest workgroup, and a heavy
+// scenario's workgroup slows down when its CU also runs other heavy ones, so the groups of each XCD's
+// chunk (xcd_group keeps a chunk of consecutive group numbers on one XCD) are dealt over the chunk's
+// CUs by cost, heaviest first onto the least-loaded CU (straddling groups count 1.25 x their heavier
+// scenario).  Renumbers the groups (lanes / ws) in place; the arithmetic is unchanged.
+void balance_groups(int n_cu, const double* cost, int n_cost, std::vector<int32_t>& lanes, std::vector<int32_t>& ws) {
+    const int ng = (int)ws.size();
+    if (n_cu <= 0 || n_cu % 8 != 0 || ng > 4 * n_cu || ng < 2) return;
+    double cmax = 0.0;
+    for (int k = 0; k < n_cost; ++k) cmax = std::max(cmax, cost[k]);
+    auto c = [&](int sc) { return (sc >= 0 && sc < n_cost) ? cost[sc] : cmax; };
+    auto gcost = [&](int g) {
+        const int w = ws[(size_t)g];
+        return w >= 0 ? c(w) : (w <= -2 ? 1.25 * std::max(c(-w - 2), c(-w - 1)) : 1.5 * cmax);
+    };
+    std::vector<int32_t> block_of((size_t)ng);  // group number -> the block that runs it
+    for (int b = 0; b < ng; ++b) block_of[(size_t)xcd_group_host(b, ng)] = b;
+    std::vector<int32_t> newnum((size_t)ng, -1);
+    const int per = ng / 8, rem = ng % 8;
+    for (int x = 0, first = 0; x < 8; ++x) {
+        const int cnt = per + (x < rem ? 1 : 0);
+        // the chunk's positions grouped by CU, each CU's positions in dispatch order
+        std::vector<std::pair<int, int>> pos;  // (cu, position)
+        for (int p = first; p < first + cnt; ++p) pos.emplace_back(block_of[(size_t)p] % n_cu, p);
+        std::stable_sort(pos.begin(), pos.end(), [&](const std::pair<int, int>& u, const std::pair<int, int>& v) {
+            return u.first != v.first ? u.first < v.first : block_of[(size_t)u.second] < block_of[(size_t)v.second];
+        });
+        std::vector<int> cus;
+        std::vector<std::vector<int>> free_pos;
+        for (const auto& q : pos) {
+            if (cus.empty() || cus.back() != q.first) {
+                cus.push_back(q.first);
+                free_pos.emplace_back();
+            }
+            free_pos.back().push_back(q.second);
+        }
+        std::vector<double> load(cus.size(), 0.0);
+        std::vector<size_t> used(cus.size(), 0);
+        std::vector<int> gs;
+        for (int g = first; g < first + cnt; ++g) gs.push_back(g);
+        std::stable_sort(gs.begin(), gs.end(), [&](int u, int v) { return gcost(u) > gcost(v); });
+        for (int g : gs) {
+            size_t best = cus.size();
+            for (size_t k = 0; k < cus.size(); ++k)
+                if (used[k] < free_pos[k].size() && (best == cus.size() || load[k] < load[best])) best = k;
+            newnum[(size_t)g] = free_pos[best][used[best]++];
+            load[best] += gcost(g);
+        }
+        first += cnt;
+    }
+    std::vector<int32_t> l2(lanes.size(), -1), w2((size_t)ng, 0);
+    for (int g = 0; g < ng; ++g) {
+        const size_t d = (size_t)newnum[(size_t)g];
+        w2[d] = ws[(size_t)g];
+        for (int l = 0; l < EPB; ++l) l2[d * EPB + (size_t)l] = lanes[(size_t)g * EPB + (size_t)l];
+    }
+    lanes.swap(l2);
+    ws.swap(w2);
+}
+
 void make_groups(int n, const int32_t* env_scn, int n_scn, std::vector<int32_t>& lanes, std::vector<int32_t>& ws) {
     std::vector<int32_t> order((size_t)n);
     for (int i = 0; i < n; ++i) order[(size_t)i] = i;
@@ -546,7 +614,10 @@ int32_t d2d_set_scenarios(d2d_t* h, const d2d_scn* scns, int32_t n_scn, const in
     // slot layout: grouped for a static mixed map (pool mode redraws scenarios at every reset);
     // the current state moves into the new layout
     std::vector<int32_t> lanes, ws;
-    if (D2D_GROUP && env_scn_host && n_scn > 1 && !h->cfg.scn_pool) make_groups(h->n, env_scn_host, n_scn, lanes, ws);
+    if (D2D_GROUP && env_scn_host && n_scn > 1 && !h->cfg.scn_pool) {
+        make_groups(h->n, env_scn_host, n_scn, lanes, ws);
+        if ((int)h->scn_cost.size() == n_scn) balance_groups(h->n_cu, h->scn_cost.data(), n_scn, lanes, ws);
+    }
     Layout to;
     const bool relayout = !lanes.empty() || h->lane_env;
     if (relayout) {
@@ -596,8 +667,42 @@ int32_t d2d_set_scenario_costs(d2d_t* h, const double* cost, int32_t n_scn) {
     hipError_t e;
     if ((e = hipDeviceSynchronize()) != hipSuccess) return hip_fail(e, "d2d_set_scenario_costs: sync");
     h->scn_cost.assign(cost, cost + n_scn);
+    if (h->lane_env && !h->quad_mode) {
+        // grouped layout: deal the groups over the CUs by the new costs (balance_groups); the state
+        // moves into the renumbered layout, the reset cache refills
+        std::vector<int32_t> es((size_t)h->n);
+        if ((e = hipMemcpy(es.data(), h->env_scn, sizeof(int32_t) * (size_t)h->n, hipMemcpyDeviceToHost)) != hipSuccess)
+            return hip_fail(e, "d2d_set_scenario_costs: env_scn");
+        std::vector<int32_t> lanes, ws;
+        make_groups(h->n, es.data(), n_scn, lanes, ws);
+        balance_groups(h->n_cu, h->scn_cost.data(), n_scn, lanes, ws);
+        Layout to;
+        if ((e = alloc_layout(to, h->n, lanes, ws)) != hipSuccess) return hip_fail(e, "d2d_set_scenario_costs: layout");
+        if ((e = move_state(take_layout(h), to, h->n)) != hipSuccess) {
+            free_layout(to);
+            return hip_fail(e, "d2d_set_scenario_costs: layout move");
+        }
+        Layout from = take_layout(h);
+        put_layout(h, to);
+        free_layout(from);
+        h->generation += 1;  // captured graphs hold the old layout's buffers
+        h->rc_dirty = true;
+    }
     if ((e = make_quads(h)) != hipSuccess) return hip_fail(e, "d2d_set_scenario_costs: quad workgroups");
     return D2D_OK;
+}
+
+int32_t d2d_get_group_layout(d2d_t* h, int32_t* slot_env, int32_t* group_scn) {
+    if (!h) return fail(D2D_E_ARG, "d2d_get_group_layout: null handle"), -1;
+    if (!h->lane_env) return 0;
+    if (!slot_env || !group_scn) return fail(D2D_E_ARG, "d2d_get_group_layout: null output"), -1;
+    DeviceGuard g(h->device);
+    hipError_t e;
+    if ((e = hipDeviceSynchronize()) != hipSuccess ||
+        (e = hipMemcpy(slot_env, h->lane_env, sizeof(int32_t) * (size_t)h->ns, hipMemcpyDeviceToHost)) != hipSuccess ||
+        (e = hipMemcpy(group_scn, h->wg_scn, sizeof(int32_t) * (size_t)h->n_groups, hipMemcpyDeviceToHost)) != hipSuccess)
+        return hip_fail(e, "d2d_get_group_layout"), -1;
+    return h->n_groups;
 }
 
 int32_t d2d_reset(d2d_t* h, const uint8_t* mask_dev, uint64_t seed, float* obs_dev, void* stream) {
@@ -972,6 +1077,21 @@ int32_t d2d_group_layout(int32_t n, const int32_t* env_scn, int32_t n_scn, int32
             return fail(D2D_E_ARG, "d2d_group_layout: env scenario index out of range"), -1;
     std::vector<int32_t> lanes, ws;
     make_groups(n, env_scn, n_scn, lanes, ws);
+    std::copy(lanes.begin(), lanes.end(), slot_env);
+    std::copy(ws.begin(), ws.end(), group_scn);
+    return (int32_t)ws.size();
+}
+
+int32_t d2d_balanced_group_layout(int32_t n, const int32_t* env_scn, int32_t n_scn, const double* cost, int32_t n_cu,
+                                  int32_t* slot_env, int32_t* group_scn) {
+    if (n <= 0 || n_scn <= 0 || !env_scn || !cost || !slot_env || !group_scn || n_cu < 0)
+        return fail(D2D_E_ARG, "d2d_balanced_group_layout: bad arguments"), -1;
+    for (int i = 0; i < n; ++i)
+        if (env_scn[i] < 0 || env_scn[i] >= n_scn)
+            return fail(D2D_E_ARG, "d2d_balanced_group_layout: env scenario index out of range"), -1;
+    std::vector<int32_t> lanes, ws;
+    make_groups(n, env_scn, n_scn, lanes, ws);
+    balance_groups(n_cu, cost, n_scn, lanes, ws);
     std::copy(lanes.begin(), lanes.end(), slot_env);
     std::copy(ws.begin(), ws.end(), group_scn);
     return (int32_t)ws.size();

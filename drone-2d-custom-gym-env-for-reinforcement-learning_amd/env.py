@@ -325,6 +325,17 @@ class Drone2dVecEnv:
             raise ValueError("env_scn must have shape [num_envs]")
         check(self._lib.d2d_set_env_scenarios(self._h, self._ptr(es), self._stream()), "d2d_set_env_scenarios")
 
+    def group_layout(self):
+        """The slot layout in use (include/drone2d.h d2d_get_group_layout): (slot_env [ns] int32,
+        group_scn [groups] int32), or None for the identity layout (one scenario / pool modes)."""
+        ng = (self.num_envs + 63) // 64
+        se = np.zeros(ng * 64, np.int32)
+        gs = np.zeros(ng, np.int32)
+        k = self._lib.d2d_get_group_layout(self._h, se.ctypes.data_as(C.c_void_p), gs.ctypes.data_as(C.c_void_p))
+        if k < 0:
+            check(k, "d2d_get_group_layout")
+        return (se, gs) if k > 0 else None
+
     @property
     def generation(self) -> int:
         """Changes whenever the library re-allocates what a captured step graph points at

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define D2D_ABI_VERSION 4
+#define D2D_ABI_VERSION 5
 
 #define D2D_MAX_WPS 16                    /* largest test path: 'large' has 14 waypoints   */
 #define D2D_MAX_SEGS (D2D_MAX_WPS - 2)    /* QPMI2D fits n_wps-2 quadratics (predef_path.py:34) */
@@ -169,9 +169,12 @@ int32_t d2d_n_envs(const d2d_t* h);
  * envs use scenario 0).  (replaces create_test_scenario + QPMI2D fit in init_pymunk, :218-311) */
 int32_t d2d_set_scenarios(d2d_t* h, const d2d_scn* scns, int32_t n_scn, const int32_t* env_scn_host);
 
-/* Relative step cost of each scenario of the last d2d_set_scenarios (test mode; default 1.0 each): the
- * step kernel's quad workgroups (4 groups of 64 envs, 16 waves, one per CU) pair heavy and light
- * scenarios on each SIMD by these weights.  Placement only: results do not depend on it.  Synchronises. */
+/* Relative step cost of each scenario of the last d2d_set_scenarios (test mode; default 1.0 each).
+ * With a grouped layout (several scenarios), the groups are renumbered so that the workgroups that
+ * share a CU carry a balanced load (d2d_get_group_layout; the state moves along, cached reset
+ * observations are recomputed, d2d_generation changes); the optional quad workgroups (D2D_QUAD=1)
+ * pair heavy and light scenarios by these weights.  Placement only: results do not depend on it.
+ * Synchronises. */
 int32_t d2d_set_scenario_costs(d2d_t* h, const double* cost, int32_t n_scn);
 
 /* Reset the envs whose mask byte is non-zero (mask_dev NULL = all envs) and write their
@@ -265,6 +268,16 @@ int32_t d2d_selftest(int32_t which, int64_t n, uint64_t seed, uint64_t* mismatch
  * -(s + 2) if it straddles exactly scenarios s and s + 1, or -1 if it holds three or more.  slot_env: int32[ceil(n/64) * 64], group_scn: int32[ceil(n/64)].
  * Returns the number of groups, or -1 on bad arguments (d2d_last_error says which). */
 int32_t d2d_group_layout(int32_t n, const int32_t* env_scn, int32_t n_scn, int32_t* slot_env, int32_t* group_scn);
+/* The slot layout the handle uses now (slot_env [ns], group_scn [n_groups], as d2d_group_layout
+ * describes them): d2d_group_layout's groups renumbered by d2d_set_scenario_costs so that each CU's
+ * co-resident workgroups carry a balanced load (no effect on results).  Returns the number of
+ * groups, 0 for the identity layout (outputs untouched), -1 on error.  Added in ABI v5. */
+int32_t d2d_get_group_layout(d2d_t* h, int32_t* slot_env, int32_t* group_scn);
+/* The renumbering itself, host-only (tests): d2d_group_layout's groups dealt over n_cu CUs by
+ * cost[n_scn] -- what d2d_set_scenario_costs installs on a device with n_cu compute units (n_cu not a
+ * multiple of 8, or more groups than 4 x n_cu: d2d_group_layout's order).  Added in ABI v5. */
+int32_t d2d_balanced_group_layout(int32_t n, const int32_t* env_scn, int32_t n_scn, const double* cost, int32_t n_cu,
+                                  int32_t* slot_env, int32_t* group_scn);
 
 /* Error codes */
 #define D2D_OK 0

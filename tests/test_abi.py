@@ -72,7 +72,7 @@ def test_hip_library_exports_every_header_symbol(hip_lib):
     for f in header_functions():
         assert hasattr(hip_lib, f), f
         assert f in _native.SIGNATURES, f  # and the ctypes binding declares it
-    assert hip_lib.d2d_abi_version() == abi.ABI_VERSION == 4
+    assert hip_lib.d2d_abi_version() == abi.ABI_VERSION == 5
 
 
 def test_hip_library_is_gfx950(d2):
@@ -149,6 +149,54 @@ def test_group_layout_properties(hip_lib, case):
     bad = np.array([0, 9], np.int32)
     assert hip_lib.d2d_group_layout(2, p(bad), 3, p(slot_env), p(group_scn)) == -1
     assert b"out of range" in hip_lib.d2d_last_error()
+
+
+def _xcd_group(b, nb):
+    per, rem, x, k = nb // 8, nb % 8, b % 8, b // 8
+    return x * (per + 1) + k if x < rem else rem * (per + 1) + (x - rem) * per + k
+
+
+@pytest.mark.parametrize("n,n_cu", [(65536, 256), (32768, 256), (65536 + 37, 256), (1001, 256), (65536, 0),
+                                    (65536, 100)])
+def test_balanced_group_layout(hip_lib, n, n_cu):
+    """d2d_balanced_group_layout (what d2d_set_scenario_costs installs): the same groups as
+    d2d_group_layout, renumbered only inside each XCD chunk, dealt so that the workgroups sharing a
+    CU (blocks congruent mod n_cu) carry a balanced cost: on the mixed batch no CU holds more heavy
+    groups than the even share rounded up, and the straddling groups sit on distinct CUs.  With
+    n_cu = 0, n_cu not a multiple of 8, or more groups than 4 n_cu: the natural order."""
+    import numpy as np
+
+    from drone2d_amd.config import SCENARIO_STEP_COST
+
+    names = ["perpendicular", "parallel", "S_parallel", "corridor", "S_corridor", "large", "impossible"]
+    k = len(names)
+    cost = np.array([SCENARIO_STEP_COST[x] for x in names], np.float64)
+    es = np.ascontiguousarray(np.arange(n) % k, dtype=np.int32)
+    ng = (n + 63) // 64
+    p = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+    se0, gs0 = np.zeros(ng * 64, np.int32), np.zeros(ng, np.int32)
+    se, gs = np.zeros(ng * 64, np.int32), np.zeros(ng, np.int32)
+    assert hip_lib.d2d_group_layout(n, p(es), k, p(se0), p(gs0)) == ng
+    assert hip_lib.d2d_balanced_group_layout(n, p(es), k, p(cost), n_cu, p(se), p(gs)) == ng
+    nat = {tuple(r): j for j, r in enumerate(se0.reshape(ng, 64))}
+    new_of = np.array([nat[tuple(r)] for r in se.reshape(ng, 64)])   # same groups, renumbered
+    assert sorted(new_of.tolist()) == list(range(ng)) and (gs == gs0[new_of]).all()
+    if n_cu == 0 or n_cu % 8 or ng > 4 * n_cu:
+        assert (new_of == np.arange(ng)).all()
+        return
+    per, rem = ng // 8, ng % 8
+    chunk = np.concatenate([np.full(per + (x < rem), x) for x in range(8)])
+    assert (chunk[new_of] == chunk[np.arange(ng)]).all()               # XCD chunks kept
+    cu_groups = {}
+    for b in range(ng):
+        cu_groups.setdefault(b % n_cu, []).append(_xcd_group(b, ng))
+    heavy = {2, 4, 5}
+    hv = [sum(1 for g in gl if gs[g] in heavy or gs[g] < 0) for gl in cu_groups.values()]
+    if n >= 32768:
+        share = -(-sum(1 for x in gs if x in heavy or x < 0) // len(cu_groups))
+        assert max(hv) <= share, (max(hv), share)
+        strad = [c for c, gl in cu_groups.items() for g in gl if gs[g] < 0]
+        assert len(strad) == len(set(strad))
 
 
 def test_philox_known_answers(oracle_mod):

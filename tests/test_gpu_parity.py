@@ -92,6 +92,35 @@ def test_quad_workgroups_vs_oracle(d2, scn, monkeypatch):
     venv.close()
 
 
+def test_balanced_mixed_layout_full_size(d2):
+    """65 536 mixed envs (BASELINE configs[4] per GPU): the layout in use is the host's co-residency
+    balanced renumbering for this device's CU count (d2d_balanced_group_layout), not the natural
+    order, and the full batch steps in parity with the oracle on it (teacher-forced, auto-resets)."""
+    import ctypes as C
+
+    from drone2d_amd.config import SCENARIO_STEP_COST
+
+    n = FULL
+    venv, orc = make_pair(d2, n, SCENARIOS, seed=17, kwargs=_cfgkw())
+    se, gs = venv.group_layout()
+    es = np.ascontiguousarray(venv.env_scenario, np.int32)
+    cost = np.array([SCENARIO_STEP_COST[x] for x in SCENARIOS], np.float64)
+    ng = (n + 63) // 64
+    se_h, gs_h, se_n, gs_n = np.zeros(ng * 64, np.int32), np.zeros(ng, np.int32), np.zeros(ng * 64, np.int32), \
+        np.zeros(ng, np.int32)
+    p = lambda a: a.ctypes.data_as(C.c_void_p)  # noqa: E731
+    n_cu = torch.cuda.get_device_properties(0).multi_processor_count
+    lib = venv._lib
+    assert lib.d2d_balanced_group_layout(n, p(es), len(SCENARIOS), p(cost), n_cu, p(se_h), p(gs_h)) == ng
+    assert lib.d2d_group_layout(n, p(es), len(SCENARIOS), p(se_n), p(gs_n)) == ng
+    assert (se == se_h).all() and (gs == gs_h).all()
+    assert n_cu % 8 or not (se == se_n).all()
+    rng = np.random.default_rng(5)
+    for t in range(24):
+        compare_step(venv, orc, np.clip(rng.normal(0.0, 0.6, (n, 2)), -1, 1).astype(np.float32))
+    venv.close()
+
+
 def test_grouped_lane_map_irregular(d2):
     """Static mixed env -> scenario map with ragged groups: the step kernel's scenario-grouped lane
     map (partial groups padded, a scenario with 3 envs, one with none, n not a multiple of 64)."""

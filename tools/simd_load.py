@@ -46,15 +46,8 @@ cu = (xcc << 8) | (((hw >> 13) & 7) << 5) | (((hw >> 12) & 1) << 4) | ((hw >> 8)
 simd = (hw >> 4) & 3
 es = venv.env_scenario
 slot_env = None
-try:
-    ng = (venv.num_envs + 63) // 64
-    se = np.zeros(ng * 64, np.int32)
-    gs = np.zeros(ng, np.int32)
-    p = lambda x: x.ctypes.data_as(C.c_void_p)  # noqa: E731
-    lib.d2d_group_layout(venv.num_envs, p(np.ascontiguousarray(es, np.int32)), len(venv.scenarios), p(se), p(gs))
-    gscn = gs
-except Exception:  # noqa: BLE001
-    gscn = np.zeros(nw // 4, np.int32)
+lay = venv.group_layout()
+gscn = lay[1] if lay is not None else np.zeros(nw // 4, np.int32)
 names = [x.name for x in venv.scenarios]
 t0 = np.zeros(16, np.int64)
 for x in range(16):
