@@ -262,6 +262,21 @@ __global__ __launch_bounds__(MLP_BLOCK) void mlp_forward_kernel(MlpPair P, int m
 #define D2D_PPO_FWD_MFMA 1
 #endif
 constexpr int FM_SPB = 32, FM_TILES = 2, XS = OBS + 2, HS = HID + 1;  // LDS row strides: bank spread
+// tanh for the matrix-core forward (D2D_PPO_FTANH=1): |x| < 0.25 an odd Taylor polynomial (next term
+// < 3e-8 relative), else (1 - t) / (1 + t) with t = exp(-2 |x|) from v_exp_f32 and v_rcp_f32 (no
+// cancellation: 1 - t >= 0.39): a few ulp, 15 instructions instead of the library's ~60, which made
+// the hidden layers' activations the longest part of a forward workgroup.
+#ifndef D2D_PPO_FTANH
+#define D2D_PPO_FTANH 1
+#endif
+__device__ __forceinline__ float ftanh(float x) {
+    if (!D2D_PPO_FTANH) return tanhf(x);
+    const float ax = fabsf(x), x2 = x * x;
+    const float p = x * (1.0f + x2 * (-0.333333333f + x2 * (0.133333333f + x2 * (-0.0539682540f + x2 * 0.0218694885f))));
+    const float t = __builtin_amdgcn_exp2f(ax * -2.88539008f);  // exp(-2 |x|)
+    const float r = (1.0f - t) * __builtin_amdgcn_rcpf(1.0f + t);
+    return ax < 0.25f ? p : copysignf(r, x);
+}
 // h1 or h2 of a 32-sample tile (both nets), LDS -> global as 16-byte row-contiguous stores: 4 per
 // thread instead of 16 dword column stores per lane (the MFMA's C/D layout holds a unit's column),
 // which made the forward store-issue-bound.
@@ -278,6 +293,20 @@ __device__ __forceinline__ void store_tile(const MlpPair& P, int s0, int m, cons
     }
 }
 __device__ void rollout_epilogue(const d2d_ppo_rollout& R, int m, const float (*outs)[FM_TILES * FM_SPB]);
+// diagnostic builds only (-DD2D_PPO_STAMPS, tools/ubench_ppo_fwd.py --stamps): s_memtime at the
+// forward's phase boundaries, lane 0 of every wave, [workgroup][wave][8]
+#ifdef D2D_PPO_STAMPS
+__device__ uint64_t* d2d_ppo_stamp_buf;
+#define PPO_STAMP(k)                                                                                  \
+    do {                                                                                              \
+        if (d2d_ppo_stamp_buf && (threadIdx.x & 63) == 0)                                             \
+            d2d_ppo_stamp_buf[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define PPO_STAMP(k) \
+    do {             \
+    } while (0)
+#endif
 // RO: the rollout step (d2d_ppo_rollout_step): rows are the envs in order (idx == nullptr), h1 / h2
 // stay on chip, the outputs go to LDS for the action / GAE epilogue instead of to P.net[].out
 template <bool RO>
@@ -299,6 +328,7 @@ __device__ __forceinline__ void mlp_forward_mfma_body(const MlpPair& P, int m, c
     const int w = tid >> 6, lane = tid & 63, ci = lane & 31, h = lane >> 5;
     const int net = w >> 1, j0 = (w & 1) * 32;
     const MlpNet& N = P.net[net];
+    PPO_STAMP(0);
     {
         constexpr int NWE = 2 * WST1 + 2 * HID * HID, NWI = (NWE + 255) / 256;
         float wv[NWI];
@@ -336,6 +366,7 @@ __device__ __forceinline__ void mlp_forward_mfma_body(const MlpPair& P, int m, c
     __shared__ float outs[RO ? 3 : 1][FM_TILES * FM_SPB];  // RO: mean (2 rows) and value per sample
     const float b1 = N.b1[j0 + ci], b2 = N.b2[j0 + ci];
     __syncthreads();  // weights staged, rows
+    PPO_STAMP(1);
     static_assert(FM_TILES * FM_SPB == D2D_PPO_HEAD_BLOCK, "one advantage partial per workgroup");
     if (adv != nullptr && tid < 64) {  // d2d_ppo_adv_stats' partials of this workgroup's 64 rows
         const int64_t r = rows[tid];
@@ -363,6 +394,7 @@ __device__ __forceinline__ void mlp_forward_mfma_body(const MlpPair& P, int m, c
 #pragma unroll
     for (int t = 0; t < HID / 2; ++t) w2r[t] = ubuf[net * WSTN + WST1 + (j0 + ci) * HS + 2 * t + h];
     __syncthreads();  // every wave holds its operands: the region becomes xs / hs
+    PPO_STAMP(2);
     if (tid < FM_TILES * FM_SPB) xs[tid][OBS] = 0.0f;  // the k padding of the 28-deep layer-1 product
     {
 #pragma unroll
@@ -378,6 +410,7 @@ __device__ __forceinline__ void mlp_forward_mfma_body(const MlpPair& P, int m, c
     for (int tile = 0; tile < FM_TILES; ++tile) {
         const int s0 = sb + tile * FM_SPB;
         __syncthreads();  // staging done / the previous tile's outputs have read hs
+        PPO_STAMP(3 + tile);
         // layer 1 (k = 27 inputs, padded to 28)
         f32x16 acc = {};
 #pragma unroll
@@ -386,7 +419,7 @@ __device__ __forceinline__ void mlp_forward_mfma_body(const MlpPair& P, int m, c
 #pragma unroll
         for (int v = 0; v < 16; ++v) {
             const int i = (v & 3) + 8 * (v >> 2) + 4 * h;  // sample of register v (C/D map)
-            const float y = tanhf(acc[v] + b1);
+            const float y = ftanh(acc[v] + b1);
             hs[net][i][j0 + ci] = y;
         }
         __syncthreads();
@@ -400,7 +433,7 @@ __device__ __forceinline__ void mlp_forward_mfma_body(const MlpPair& P, int m, c
 #pragma unroll
         for (int v = 0; v < 16; ++v) {
             const int i = (v & 3) + 8 * (v >> 2) + 4 * h;
-            const float y = tanhf(acc[v] + b2);
+            const float y = ftanh(acc[v] + b2);
             hs[net][i][j0 + ci] = y;
         }
         __syncthreads();
@@ -419,10 +452,12 @@ __device__ __forceinline__ void mlp_forward_mfma_body(const MlpPair& P, int m, c
                 P.net[on].out[(size_t)i * P.net[on].od + r] = o;
         }
     }
+    PPO_STAMP(5);
     if (RO) {
         __syncthreads();
         if (tid < FM_TILES * FM_SPB) rollout_epilogue(*R, m, outs);  // wave 0: one env per lane
     }
+    PPO_STAMP(6);
 }
 __global__ __launch_bounds__(256) void mlp_forward_mfma_kernel(MlpPair P, int m, const int64_t* __restrict__ idx,
                                                                const float* __restrict__ obs,
@@ -670,6 +705,147 @@ __global__ __launch_bounds__(MLP_BLOCK) void mlp_backward_kernel(MlpPair P, int 
         *reinterpret_cast<float4*>(N.g1 + (size_t)i * HID + ub(k)) =
             make_float4(g1[k] * (1.0f - hv.x * hv.x), g1[k + 1] * (1.0f - hv.y * hv.y),
                         g1[k + 2] * (1.0f - hv.z * hv.z), g1[k + 3] * (1.0f - hv.w * hv.w));
+    }
+}
+
+// The same loss head and backward pass with g1 = g2 W2 on the matrix cores (D2D_PPO_BWD_MFMA=1): a
+// workgroup takes 64 samples and both nets.  Threads 0-63 compute the policy head of one sample
+// each, 64-127 the value head; then g2 = (gout W3) (1 - h2^2) for every (sample, net, unit) into
+// global memory (the weight gradients read it) and into LDS as the A operand; wave w computes the
+// 32 (samples) x 32 (units) tiles [net w / 2, units 32 (w % 2) ..] of g1 = g2 W2 for both 32-sample
+// halves with v_mfma_f32_32x32x2_f32, its B operands (W2's rows, 128-byte coalesced) held in
+// registers.  Partial rows: row b holds all five sums, row nb + b zeros (head_finish adds all rows).
+#ifndef D2D_PPO_BWD_MFMA
+#define D2D_PPO_BWD_MFMA 0
+#endif
+__global__ __launch_bounds__(256) void mlp_backward_mfma_kernel(MlpPair P, int m, const int64_t* __restrict__ idx,
+                                                                const float* __restrict__ act,
+                                                                const float* __restrict__ old_logp,
+                                                                const float* __restrict__ adv,
+                                                                const float* __restrict__ ret,
+                                                                const float* __restrict__ log_std,
+                                                                const double* __restrict__ ws, int nbs,
+                                                                int normalize, float clip, float vf_coef,
+                                                                float* __restrict__ partial) {
+    constexpr int SPB = FM_TILES * FM_SPB;  // 64 samples per workgroup
+    __shared__ double red[5 * 4];
+    __shared__ float g2s[2][SPB][HS];       // g2 of both nets, one sample per row (A operands)
+    __shared__ float gos[3][SPB];           // d loss / d (mean0, mean1, value)
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, ci = lane & 31, h = lane >> 5;
+    const int sb = blockIdx.x * SPB, net = w >> 1, k0 = (w & 1) * 32;
+    // this wave's B operands: W2[net][2 t + h][k0 + ci], issued first (consumed after the head)
+    float w2r[HID / 2];
+    {
+        const float* W2 = P.net[net].w2 + k0 + ci;
+#pragma unroll
+        for (int t = 0; t < HID / 2; ++t) w2r[t] = W2[(2 * t + h) * HID];
+    }
+    float adv_mean = 0.0f, adv_inv = 1.0f;
+    if (normalize) {
+        double sm = 0.0, sq = 0.0;
+        for (int b = tid; b < nbs; b += 256) {
+            sm += ws[2 * b];
+            sq += ws[2 * b + 1];
+        }
+        double sv[2] = {sm, sq};
+        block_sum_n(sv, red);
+        const double mu = sv[0] / m, var = (sv[1] - sv[0] * mu) / (m > 1 ? m - 1 : 1);
+        adv_mean = (float)mu;
+        adv_inv = 1.0f / ((float)sqrt(var > 0.0 ? var : 0.0) + 1e-8f);
+    }
+    double q[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+    if (tid < 2 * SPB) {
+        const int sl = tid & (SPB - 1), i = sb + sl;
+        float g0 = 0.0f, g1v = 0.0f;
+        if (i < m) {
+            const int64_t j = idx[i];
+            if (tid < SPB) {  // the policy head (mlp_backward_kernel's arithmetic)
+                const MlpNet& N = P.net[0];
+                const float ls0 = log_std[0], ls1 = log_std[1];
+                const float is0 = expf(-ls0), is1 = expf(-ls1);
+                const float z0 = (act[2 * j] - N.out[2 * i]) * is0, z1 = (act[2 * j + 1] - N.out[2 * i + 1]) * is1;
+                const float logp = (-0.5f * z0 * z0 - ls0 - HALF_LOG_2PI) + (-0.5f * z1 * z1 - ls1 - HALF_LOG_2PI);
+                const float a = normalize ? (adv[j] - adv_mean) * adv_inv : adv[j];
+                const float ratio = expf(logp - old_logp[j]);
+                const float s1 = a * ratio, s2 = a * fminf(fmaxf(ratio, 1.0f - clip), 1.0f + clip);
+                const float g_lp = (s1 <= s2) ? a * ratio * (-1.0f / m) : 0.0f;
+                g0 = g_lp * z0 * is0;
+                g1v = g_lp * z1 * is1;
+                N.gout[2 * i] = g0;
+                N.gout[2 * i + 1] = g1v;
+                q[0] = fminf(s1, s2);
+                q[2] = fabsf(ratio - 1.0f) > clip ? 1.0 : 0.0;
+                q[3] = (double)g_lp * (z0 * z0 - 1.0f);
+                q[4] = (double)g_lp * (z1 * z1 - 1.0f);
+            } else {  // the value head
+                const MlpNet& N = P.net[1];
+                const float err = ret[j] - N.out[i];
+                g0 = err * (-2.0f * vf_coef / m);
+                N.gout[i] = g0;
+                q[1] = (double)err * err;
+            }
+        }
+        if (tid < SPB) {
+            gos[0][sl] = g0;
+            gos[1][sl] = g1v;
+        } else {
+            gos[2][sl] = g0;
+        }
+    }
+    block_sum_n(q, red);  // (its barriers also publish gos)
+    if (tid == 0) {
+        float* o = partial + (size_t)blockIdx.x * 5;
+        float* z = partial + ((size_t)gridDim.x + blockIdx.x) * 5;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            o[k] = (float)q[k];
+            z[k] = 0.0f;
+        }
+    }
+    // g2 = (gout W3) (1 - h2^2), as float4s in row order: element e = it 256 + tid is float4 e % 16 of
+    // row (e / 16) % 64 of net e / 1024, so a wave reads / writes four whole 256-byte rows
+#pragma unroll
+    for (int it = 0; it < 2 * SPB * HID / 4 / 256; ++it) {
+        const int e = it * 256 + tid, gn = e >> 10, sl = (e >> 4) & (SPB - 1), u = (e & 15) * 4, i = sb + sl;
+        float g[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        if (i < m) {
+            const MlpNet& Nn = P.net[gn];
+            const float go0 = gn ? gos[2][sl] : gos[0][sl], go1 = gn ? 0.0f : gos[1][sl];
+            const float4 hv = *reinterpret_cast<const float4*>(Nn.h2 + (size_t)i * HID + u);
+            const float4 wa = *reinterpret_cast<const float4*>(Nn.w3 + u);
+            float4 wb = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (gn == 0) wb = *reinterpret_cast<const float4*>(Nn.w3 + HID + u);
+            const float hh[4] = {hv.x, hv.y, hv.z, hv.w}, a4[4] = {wa.x, wa.y, wa.z, wa.w},
+                        b4[4] = {wb.x, wb.y, wb.z, wb.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                float d = go0 * a4[k];
+                if (gn == 0) d += go1 * b4[k];
+                g[k] = d * (1.0f - hh[k] * hh[k]);
+            }
+            *reinterpret_cast<float4*>(Nn.g2 + (size_t)i * HID + u) = make_float4(g[0], g[1], g[2], g[3]);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) g2s[gn][sl][u + k] = g[k];
+    }
+    __syncthreads();
+    // g1 = (g2 W2) (1 - h1^2) on the matrix cores
+    const MlpNet& N = P.net[net];
+#pragma unroll
+    for (int tile = 0; tile < FM_TILES; ++tile) {
+        f32x16 acc = {};
+#pragma unroll
+        for (int t = 0; t < HID / 2; ++t)
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(g2s[net][tile * FM_SPB + ci][2 * t + h], w2r[t], acc, 0, 0, 0);
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+            const int i = sb + tile * FM_SPB + (v & 3) + 8 * (v >> 2) + 4 * h;  // the C/D map
+            if (i < m) {
+                const size_t o = (size_t)i * HID + k0 + ci;
+                const float hv = N.h1[o];
+                N.g1[o] = acc[v] * (1.0f - hv * hv);
+            }
+        }
     }
 }
 
@@ -1061,6 +1237,11 @@ inline int32_t rc(hipError_t e) { return e == hipSuccess ? 0 : (int32_t)e; }
 extern "C" {
 
 int32_t d2d_ppo_abi_version(void) { return D2D_PPO_ABI_VERSION; }
+#ifdef D2D_PPO_STAMPS
+int32_t d2d_ppo_debug_stamps(uint64_t* buf) {
+    return rc(hipMemcpyToSymbol(HIP_SYMBOL(d2d_ppo_stamp_buf), &buf, sizeof(buf)));
+}
+#endif
 
 int32_t d2d_ppo_adv_stats(int32_t m, const int64_t* idx, const float* adv, double* ws, void* stream) {
     if (m <= 0) return 0;
@@ -1250,9 +1431,15 @@ int32_t d2d_ppo_mlp_backward(int32_t m, const int64_t* idx, const float* act, co
     P.net[0].gout = gout[0];
     P.net[1].gout = gout[1];
     const int nbs = (m + D2D_PPO_HEAD_BLOCK - 1) / D2D_PPO_HEAD_BLOCK;
-    hipLaunchKernelGGL(mlp_backward_kernel, dim3((m + MLP_SPB - 1) / MLP_SPB, 2), dim3(MLP_BLOCK), 0,
-                       (hipStream_t)stream, P, m, idx, act, old_logp, adv, ret, log_std, ws, nbs, normalize, clip,
-                       vf_coef, partial);
+    static_assert(FM_TILES * FM_SPB == MLP_SPB, "the matrix-core backward keeps the partial-row count");
+    if (D2D_PPO_BWD_MFMA)
+        hipLaunchKernelGGL(mlp_backward_mfma_kernel, dim3((m + MLP_SPB - 1) / MLP_SPB), dim3(256), 0,
+                           (hipStream_t)stream, P, m, idx, act, old_logp, adv, ret, log_std, ws, nbs, normalize, clip,
+                           vf_coef, partial);
+    else
+        hipLaunchKernelGGL(mlp_backward_kernel, dim3((m + MLP_SPB - 1) / MLP_SPB, 2), dim3(MLP_BLOCK), 0,
+                           (hipStream_t)stream, P, m, idx, act, old_logp, adv, ret, log_std, ws, nbs, normalize, clip,
+                           vf_coef, partial);
     return rc(hipGetLastError());
 }
 
