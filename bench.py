@@ -124,9 +124,11 @@ def cpu_info() -> dict:
 def cpu_baseline(args, kwargs):
     """Time the C oracle on a bounded sample of the same workload (test infrastructure).
 
-    Threads: one per core of the affinity set (1 core and all cores), capped only
-    by a cgroup CPU quota when one is set (more threads than the quota would time-slice) and by
-    D2D_CPU_THREADS if given; ``cores`` is the thread count actually used."""
+    Threads: one per core of the affinity set (BASELINE.md / SURVEY 8(d): 1 core and all cores;
+    D2D_CPU_THREADS overrides); ``cores`` is the thread count actually used.  When a cgroup CPU
+    quota grants fewer CPUs than the affinity set holds, the same sample is also timed with one
+    thread per granted CPU (``quota_threads`` / ``quota_threads_value``): the all-cores threads then
+    time-slice inside the quota."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle
 
@@ -137,10 +139,11 @@ def cpu_baseline(args, kwargs):
     oracle.build()
     info = cpu_info()
     threads = info["affinity_cores"]
-    if info["cgroup_quota_cores"]:
-        threads = min(threads, info["cgroup_quota_cores"])
     if os.environ.get("D2D_CPU_THREADS"):
-        threads = min(threads, int(os.environ["D2D_CPU_THREADS"]))
+        threads = max(1, int(os.environ["D2D_CPU_THREADS"]))
+    threads = min(threads, 256)  # d2d_oracle.c's per-call thread bound
+    quota = info["cgroup_quota_cores"]
+    qthreads = quota if (quota and quota < threads) else None
     n = args.envs
     scn = [s.to_c() for s in build_scenarios(kwargs)]
     b = oracle.OracleBatch(make_cfg(dict(kwargs)), scn, n)
@@ -162,9 +165,15 @@ def cpu_baseline(args, kwargs):
         b.step(act, nthreads=1)
         steps1 += 1
     dt1 = time.perf_counter() - t1
+    extra = {}
+    if qthreads:
+        tq = time.perf_counter()
+        for _ in range(steps):
+            b.step(act, nthreads=qthreads)
+        extra = {"quota_threads": qthreads, "quota_threads_value": n * steps / (time.perf_counter() - tq)}
     b.close()
     return {"value": n * steps / dt, "unit": "env-steps/s", "cores": threads, "kind": "port",
-            "single_core_value": n * steps1 / dt1, **info,
+            "single_core_value": n * steps1 / dt1, **extra, **info,
             "sample": f"C oracle (oracle/d2d_oracle.c, scalar fp64 port of the reference step), "
                       f"{n} envs x {steps} steps of {args.scenario} with auto-reset, {threads} threads "
                       f"({info['affinity_cores']} cores in the affinity set, {info['cpu_model']}), "
