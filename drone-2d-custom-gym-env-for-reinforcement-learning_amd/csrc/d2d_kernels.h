@@ -43,18 +43,25 @@ constexpr int K1_THREADS = 256; // K1: 4 waves
 constexpr size_t K1_LDS_BUDGET = 40 * 1024;
 constexpr size_t K2_LDS_BUDGET = 64 * 1024;
 // Wave priorities per role (s_setprio, 0..3): the Brent waves win issue arbitration on their SIMD,
-// the physics waves come next (their 10-sweep joint chain must end before the search does).
+// the physics waves come next (their 10-sweep joint chain must end before the search does); once
+// its search is done the path wave drops to 0, since the physics wave is then the critical one.
+// A/B (tools/variants.py, µs per step at 65 536 envs, corridor / S_corridor / large / mixed):
+// W0..W3 = 2,0,3,2 29.46 / 37.97 / 35.73 / 40.11; 2,1,3,1 28.86 / 37.99 / 35.78 / 40.00; with W2 -> 0
+// after the search 28.55 / 37.61 / 35.78 / 40.11 (kept); all equal (0) 39.9, W0 = W2 = 3 35.2.
 #ifndef D2D_PRIO_W0
 #define D2D_PRIO_W0 2
 #endif
 #ifndef D2D_PRIO_W1
-#define D2D_PRIO_W1 0
+#define D2D_PRIO_W1 1
 #endif
 #ifndef D2D_PRIO_W2
 #define D2D_PRIO_W2 3
 #endif
 #ifndef D2D_PRIO_W3
-#define D2D_PRIO_W3 2
+#define D2D_PRIO_W3 1
+#endif
+#ifndef D2D_PRIO_W2_POST
+#define D2D_PRIO_W2_POST 0  // W2 once its search is done (the reward terms and waits)
 #endif
 #define D2D_SETPRIO(p)                                \
     do {                                              \
@@ -687,6 +694,7 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const Scn* scns, cons
             sh.pflags[lane] = f & D2D_FLAG_LA_LOCK;
         }
         STAMP(4);
+        if (D2D_PRIO_W2_POST != D2D_PRIO_W2) __builtin_amdgcn_s_setprio(D2D_PRIO_W2_POST);
         // the reward terms that do not need the joint sweep, while the physics wave finishes
         flag_wait(sh.f_done);
         flag_wait(sh.f_ca);
