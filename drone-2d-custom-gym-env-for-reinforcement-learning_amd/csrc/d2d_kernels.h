@@ -60,6 +60,12 @@ constexpr size_t K2_LDS_BUDGET = 64 * 1024;
 #ifndef D2D_PRIO_W3
 #define D2D_PRIO_W3 1
 #endif
+#ifndef D2D_PRIO_W1_POST
+#define D2D_PRIO_W1_POST D2D_PRIO_W1  // W1 once its sensing part is done
+#endif
+#ifndef D2D_PRIO_W3_TAB
+#define D2D_PRIO_W3_TAB D2D_PRIO_W2   // W3 while it re-checks its part of W2's table
+#endif
 #ifndef D2D_PRIO_W2_POST
 #define D2D_PRIO_W2_POST 0  // W2 once its search is done (the reward terms and waits)
 #endif
@@ -308,6 +314,9 @@ __device__ __forceinline__ void spawn_state(const StepArgs& a, const Scn& S, int
 // wave-uniform read of an LDS flag written by another wave of the workgroup
 // (explicit LDS address space: a generic volatile access would become a flat load)
 using LdsU32 = __attribute__((address_space(3))) uint32_t;
+#ifndef D2D_WAIT_SLEEP
+#define D2D_WAIT_SLEEP 1  // s_sleep units (64 cycles) between two polls of a hand-off flag
+#endif
 __device__ __forceinline__ bool flag_seen(const uint32_t& f) {
     return __builtin_amdgcn_readfirstlane(*(const volatile LdsU32*)&f) != 0u;
 }
@@ -364,7 +373,7 @@ __device__ __forceinline__ void flag_raise(uint32_t& f) {
     if ((threadIdx.x & 63) == 0) *(volatile LdsU32*)&f = 1u;
 }
 __device__ __forceinline__ void flag_wait(const uint32_t& f) {
-    while (!flag_seen(f)) __builtin_amdgcn_s_sleep(1);
+    while (!flag_seen(f)) __builtin_amdgcn_s_sleep(D2D_WAIT_SLEEP);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
@@ -654,6 +663,7 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const Scn* scns, cons
             }
         }
         STAMP(4);
+        if (D2D_PRIO_W1_POST != D2D_PRIO_W1) __builtin_amdgcn_s_setprio(D2D_PRIO_W1_POST);
         flag_wait(sh.f_gs);
         STAMP(5);
         if (valid) {
@@ -739,7 +749,7 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const Scn* scns, cons
         }
     } else {
         // ---------------------------------------------------------------- auto-reset observation
-        if (D2D_SPLIT) D2D_SETPRIO(D2D_PRIO_W2);  // the re-check below is on W2's critical path
+        if (D2D_SPLIT) D2D_SETPRIO(D2D_PRIO_W3_TAB);  // the re-check below is on W2's critical path
         double po[8];
         if (D2D_SPLIT && valid && !(D2D_ABL & 4) && !(D2D_ABLATE & 1) && a.brt) {
             // second half of W2's golden-march re-check (its first wave-priority work)
