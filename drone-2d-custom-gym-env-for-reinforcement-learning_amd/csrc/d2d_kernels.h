@@ -161,7 +161,8 @@ struct StepArgs {
 #define D2D_STRADDLE_LDS 1  // a grouped-layout workgroup straddling two scenarios stages both in LDS
 #endif
 #ifndef D2D_SPLIT3
-#define D2D_SPLIT3 0     // 1: W2, W1 and W3 re-check one third each of the golden-march table (needs D2D_SPLIT)
+#define D2D_SPLIT3 -1    // W2, W1 and W3 re-check one third each of the golden-march table (needs D2D_SPLIT):
+                         // 1 always, 0 never, -1 when K1 has at most one workgroup per CU (d2d_step)
 #endif
 #ifndef D2D_SPLIT
 #define D2D_SPLIT 1      // W3 re-checks the second half of W2's golden-march table (0: W2 alone)
@@ -407,7 +408,7 @@ __device__ __forceinline__ void k1_stage(const StepArgs& a, Scn* s_scn, int wg, 
 // tables indexed by global scenario id (LDS when staged: LDS / LTAB), s0 the group's scenario.
 // All 256 threads of the group call it once; the workgroup's barriers are block-wide, so every
 // wave of the block runs k1_body exactly once.
-template <bool LDS, bool LTAB, bool GRP, bool QSYNC = false>
+template <bool LDS, bool LTAB, bool GRP, bool QSYNC = false, bool S3 = false>
 __device__ __forceinline__ void k1_body(const StepArgs& a, const Scn* scns, const BtHot* hots, int s0, K1Shared& sh,
                                         int wg, int role, int qt) {
     const int wave = role;
@@ -426,7 +427,7 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const Scn* scns, cons
     if (wg == 0 && qt == 0 && a.clock)  // the step clock (fresh curriculum stage schedule)
         __hip_atomic_fetch_add(a.clock, (int64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (wave == 0) sh.scn[lane] = (valid && a.env_scn && a.n_scn > 1) ? a.env_scn[ie] : s0;
-    if (D2D_SPLIT3 && wave == 0) sh.pflags[lane] = 0x7fffffffu;  // W1 and W3 min their table parts in
+    if (S3 && wave == 0) sh.pflags[lane] = 0x7fffffffu;  // W1 and W3 min their table parts in
     // state loads issued before the staging barrier, so their HBM latency overlaps the staging:
     // W0 the whole state + action, the other roles the frame
     Body PB[3]{};
@@ -597,7 +598,7 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const Scn* scns, cons
         // ---------------------------------------------------------------- sensing
         float row[19];
         bool need = false;
-        if (D2D_SPLIT3) {
+        if (S3) {
             // the middle third of W2's golden-march re-check first, at W2's priority (its critical path)
             __builtin_amdgcn_s_setprio(D2D_PRIO_W2);
             if (valid && !(D2D_ABL & 4) && !(D2D_ABLATE & 1) && a.brt) {
@@ -691,9 +692,9 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const Scn* scns, cons
                 // golden-march re-check of steps [1, split); W3 checks [split, len) meanwhile
                 const BtHot* hot = LTAB ? hots + sh.scn[lane] : &T->hot;
                 BtLane L = bt_start<LTAB>(*T, hot, F.px, F.py);
-                bt_verify<LTAB>(hot, L, 1, D2D_SPLIT3 ? bt_third(*T, 1) : bt_split(*T), F.px, F.py);
+                bt_verify<LTAB>(hot, L, 1, S3 ? bt_third(*T, 1) : bt_split(*T), F.px, F.py);
                 flag_wait(sh.f_ver);
-                if (D2D_SPLIT3) flag_wait(sh.f_ver1);
+                if (S3) flag_wait(sh.f_ver1);
                 L.dev = min(L.dev, (int)sh.pflags[lane]);
                 int iu;
                 const double u = bt_finish<LTAB>(S, *T, hot, L.kind, L.dev, F.px, F.py, iu);
@@ -758,13 +759,13 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const Scn* scns, cons
             Body F = load_frame(a, i);
             advance_position(F);
             BtLane L = bt_start<LTAB>(T, hot, F.px, F.py);
-            const int k0 = D2D_SPLIT3 ? bt_third(T, 2) : bt_split(T);
+            const int k0 = S3 ? bt_third(T, 2) : bt_split(T);
             if (k0 < L.len) {
                 if (k0 >= 4) bt_window<LTAB>(hot, L, k0, F.px, F.py);
                 else bt_window_snap<LTAB>(T, hot, L, k0, F.px, F.py);
                 bt_verify<LTAB>(hot, L, k0, BT_K, F.px, F.py);
             }
-            if (D2D_SPLIT3) atomicMin(&sh.pflags[lane], (uint32_t)L.dev);
+            if (S3) atomicMin(&sh.pflags[lane], (uint32_t)L.dev);
             else sh.pflags[lane] = (uint32_t)L.dev;
         }
         flag_raise(sh.f_ver);
@@ -914,25 +915,27 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const Scn* scns, cons
     STAMP(6);
 }
 
-template <bool LDS, bool LTAB, bool GRP>
+template <bool LDS, bool LTAB, bool GRP, bool S3>
 __device__ __forceinline__ void k1_group(const StepArgs& a, Scn* s_scn, K1Shared& sh, int wg) {
     const Scn* scns;
     const BtHot* hots;
     int s0;
     k1_stage<LDS, LTAB, GRP>(a, s_scn, wg, scns, hots, s0);
-    k1_body<LDS, LTAB, GRP>(a, scns, hots, s0, sh, wg, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6),
-                            (int)threadIdx.x);
+    k1_body<LDS, LTAB, GRP, false, S3>(a, scns, hots, s0, sh, wg, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6),
+                                       (int)threadIdx.x);
 }
-template <bool LDS, bool LTAB>
+// S3: the three-way table re-check (D2D_SPLIT3), chosen at launch
+template <bool LDS, bool LTAB, bool S3>
 __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
     extern __shared__ __attribute__((aligned(16))) Scn s_scn[];
     __shared__ __attribute__((aligned(16))) K1Shared sh;
-    k1_group<LDS, LTAB, false>(a, s_scn, sh, blockIdx.x);
+    k1_group<LDS, LTAB, false, S3>(a, s_scn, sh, blockIdx.x);
 }
 // grouped slot layout: a pure group stages its scenario and probe table in LDS; a group that
 // straddles two scenarios (at most n_scn - 1 of them: the layout has no padding between scenarios)
 // stages both scenarios (2 x Scn fits in the Scn + BtHot allocation) and reads the probe tables
 // through L1/L2; a group of three or more scenarios reads everything through L1/L2
+template <bool S3>
 __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_grouped_kernel(StepArgs a) {
     extern __shared__ __attribute__((aligned(16))) Scn s_scn[];
     __shared__ __attribute__((aligned(16))) K1Shared sh;
@@ -940,11 +943,11 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_grouped_kernel(StepArg
     const int wg = xcd_group(blockIdx.x, gridDim.x);
     const int ws = a.wg_scn[wg];
     if (a.brt && ws >= 0)
-        k1_group<true, true, true>(a, s_scn, sh, wg);
+        k1_group<true, true, true, S3>(a, s_scn, sh, wg);
     else if (D2D_STRADDLE_LDS && ws <= -2)
-        k1_group<true, false, true>(a, s_scn, sh, wg);
+        k1_group<true, false, true, S3>(a, s_scn, sh, wg);
     else
-        k1_group<false, false, true>(a, s_scn, sh, wg);
+        k1_group<false, false, true, S3>(a, s_scn, sh, wg);
 }
 
 // Quad kernel: 16 waves = 4 groups x 4 roles; the QuadDesc tells each wave its quarter and role and
