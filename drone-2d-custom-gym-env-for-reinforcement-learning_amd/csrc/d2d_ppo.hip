@@ -849,6 +849,228 @@ __global__ __launch_bounds__(256) void mlp_backward_mfma_kernel(MlpPair P, int m
     }
 }
 
+
+// ---------------------------------------------------------------------------- fused minibatch gradient
+// One launch for what mlp_forward_mfma + mlp_backward + wgrad compute (D2D_PPO_FUSED, ABI v5): the
+// workgroup (x, net) walks the minibatch's 64-sample chunks x, x + gridDim.x, ... and keeps the
+// chunk's layer inputs, activations and output gradients in LDS, so nothing of the per-sample
+// state goes through HBM.  Wave w takes the 32 x 32 tile (samples 32 (w / 2) .., units 32 (w % 2) ..)
+// of both hidden layers and of g1 = g2 W2 on the matrix cores (W1 / W2 rows as register B operands
+// for the forward, W2's columns for g1), then the chunk's contribution to dW2 = g2^T h1 (one 32 x 32
+// tile per wave) and dW1 = g1^T x (waves 0, 1) accumulates on the matrix cores across chunks (the
+// sample is the contraction index); waves 2, 3 sum the bias and output-layer gradients on the VALU.
+// Each workgroup writes its sums into partial row x (the flat gradient's layout, its net's entries)
+// and its loss-head sums into head row x (policy) / gridDim.x + x (value); d2d_ppo_grad_reduce
+// finishes both.  Same formulas as the separate kernels, another summation order.
+struct FusedNet {
+    const float *w1, *b1, *w2, *b2, *w3, *b3;
+    int off[6];  // offsets in the flat gradient of W1, b1, W2, b2, W3, b3
+    int od;
+};
+struct FusedArgs {
+    FusedNet net[2];
+    int m;
+    const int64_t* idx;
+    const float *obs, *act, *old_logp, *adv, *ret, *log_std;
+    const double* ws;  // d2d_ppo_adv_stats' partials of the minibatch
+    int nbs, normalize;
+    float clip, vf_coef;
+    float* wpart;  // [gridDim.x][row_len]
+    int row_len;
+    float* hpart;  // [2 gridDim.x][5]
+};
+constexpr int FG_SPC = 64;
+__global__ __launch_bounds__(256, 2) void mlp_fused_grad_kernel(FusedArgs A) {
+    __shared__ float xs[FG_SPC][XS];
+    __shared__ float h1s[FG_SPC][HS], h2s[FG_SPC][HS], g1s[FG_SPC][HS], g2s[FG_SPC][HS];
+    __shared__ float gos[2][FG_SPC];
+    __shared__ float w3s[2][HID + 1];  // output rows, bias in column HID
+    __shared__ int64_t rows[FG_SPC];
+    __shared__ double red[5 * 4];
+    const int net = blockIdx.y;
+    const FusedNet& N = A.net[net];
+    const int od = N.od, m = A.m;
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, ci = lane & 31, h = lane >> 5;
+    const int st = w >> 1, u0 = (w & 1) * 32;  // this wave's sample tile and unit half
+    const int jw = (w & 1) * 32, kw = (w >> 1) * 32;  // its dW2 tile
+    // B operands, loaded once per workgroup
+    float w1r[(OBS + 1) / 2], w2r[HID / 2], w2b[HID / 2];
+#pragma unroll
+    for (int t = 0; t < (OBS + 1) / 2; ++t) w1r[t] = 2 * t + h < OBS ? N.w1[(u0 + ci) * OBS + 2 * t + h] : 0.0f;
+#pragma unroll
+    for (int t = 0; t < HID / 2; ++t) {
+        w2r[t] = N.w2[(u0 + ci) * HID + 2 * t + h];
+        w2b[t] = N.w2[(2 * t + h) * HID + u0 + ci];
+    }
+    const float b1v = N.b1[u0 + ci], b2v = N.b2[u0 + ci];
+    for (int e = tid; e < 2 * (HID + 1); e += 256) {
+        const int r = e / (HID + 1), j = e % (HID + 1);
+        w3s[r][j] = r < od ? (j < HID ? N.w3[r * HID + j] : N.b3[r]) : 0.0f;
+    }
+    float adv_mean = 0.0f, adv_inv = 1.0f;
+    if (net == 0 && A.normalize) {
+        double sm = 0.0, sq = 0.0;
+        for (int b = tid; b < A.nbs; b += 256) {
+            sm += A.ws[2 * b];
+            sq += A.ws[2 * b + 1];
+        }
+        double sv[2] = {sm, sq};
+        block_sum_n(sv, red);
+        const double mu = sv[0] / m, var = (sv[1] - sv[0] * mu) / (m > 1 ? m - 1 : 1);
+        adv_mean = (float)mu;
+        adv_inv = 1.0f / ((float)sqrt(var > 0.0 ? var : 0.0) + 1e-8f);
+    }
+    const float ls0 = A.log_std[0], ls1 = A.log_std[1], is0 = expf(-ls0), is1 = expf(-ls1);
+    f32x16 dw2 = {}, dw1 = {};
+    float db1 = 0.0f, db2 = 0.0f, dw3a = 0.0f, dw3b = 0.0f, db3a = 0.0f, db3b = 0.0f;
+    double q[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+    const int nch = (m + FG_SPC - 1) / FG_SPC;
+    for (int c = blockIdx.x; c < nch; c += gridDim.x) {
+        const int s0 = c * FG_SPC;
+        __syncthreads();  // the previous chunk's LDS reads are done
+        if (tid < FG_SPC) rows[tid] = s0 + tid < m ? A.idx[s0 + tid] : -1;
+        __syncthreads();
+        for (int e = tid; e < FG_SPC * XS; e += 256) {
+            const int i = e / XS, k = e % XS;
+            const int64_t r = rows[i];
+            xs[i][k] = (k < OBS && r >= 0) ? A.obs[r * OBS + k] : 0.0f;
+        }
+        __syncthreads();
+        f32x16 acc = {};
+#pragma unroll
+        for (int t = 0; t < (OBS + 1) / 2; ++t)
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(xs[st * 32 + ci][2 * t + h], w1r[t], acc, 0, 0, 0);
+#pragma unroll
+        for (int v = 0; v < 16; ++v) h1s[st * 32 + (v & 3) + 8 * (v >> 2) + 4 * h][u0 + ci] = ftanh(acc[v] + b1v);
+        __syncthreads();
+        acc = f32x16{};
+#pragma unroll
+        for (int t = 0; t < HID / 2; ++t)
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(h1s[st * 32 + ci][2 * t + h], w2r[t], acc, 0, 0, 0);
+#pragma unroll
+        for (int v = 0; v < 16; ++v) h2s[st * 32 + (v & 3) + 8 * (v >> 2) + 4 * h][u0 + ci] = ftanh(acc[v] + b2v);
+        __syncthreads();
+        if (tid < FG_SPC) {  // the outputs and the loss head, one sample per thread of wave 0
+            const int i = tid, s = s0 + i;
+            float o0 = w3s[0][HID], o1 = w3s[1][HID];
+#pragma unroll 16
+            for (int j = 0; j < HID; ++j) {
+                const float hv = h2s[i][j];
+                o0 += w3s[0][j] * hv;
+                o1 += w3s[1][j] * hv;
+            }
+            float g0 = 0.0f, g1v = 0.0f;
+            if (s < m) {
+                const int64_t j = rows[i];
+                if (net == 0) {
+                    const float z0 = (A.act[2 * j] - o0) * is0, z1 = (A.act[2 * j + 1] - o1) * is1;
+                    const float logp = (-0.5f * z0 * z0 - ls0 - HALF_LOG_2PI) + (-0.5f * z1 * z1 - ls1 - HALF_LOG_2PI);
+                    const float a = A.normalize ? (A.adv[j] - adv_mean) * adv_inv : A.adv[j];
+                    const float ratio = expf(logp - A.old_logp[j]);
+                    const float s1 = a * ratio, s2 = a * fminf(fmaxf(ratio, 1.0f - A.clip), 1.0f + A.clip);
+                    const float g_lp = (s1 <= s2) ? a * ratio * (-1.0f / m) : 0.0f;
+                    g0 = g_lp * z0 * is0;
+                    g1v = g_lp * z1 * is1;
+                    q[0] += fminf(s1, s2);
+                    q[2] += fabsf(ratio - 1.0f) > A.clip ? 1.0 : 0.0;
+                    q[3] += (double)g_lp * (z0 * z0 - 1.0f);
+                    q[4] += (double)g_lp * (z1 * z1 - 1.0f);
+                } else {
+                    const float err = A.ret[j] - o0;
+                    g0 = err * (-2.0f * A.vf_coef / m);
+                    q[1] += (double)err * err;
+                }
+            }
+            gos[0][i] = g0;
+            gos[1][i] = g1v;
+            db3a += g0;
+            db3b += g1v;
+        }
+        __syncthreads();
+        // g2 = (gout W3) (1 - h2^2)
+#pragma unroll 4
+        for (int it = 0; it < FG_SPC * HID / 256; ++it) {
+            const int e = it * 256 + tid, i = e >> 6, j = e & 63;
+            const float d = gos[0][i] * w3s[0][j] + gos[1][i] * w3s[1][j];
+            const float hv = h2s[i][j];
+            g2s[i][j] = d * (1.0f - hv * hv);
+        }
+        __syncthreads();
+        // g1 = (g2 W2) (1 - h1^2)
+        acc = f32x16{};
+#pragma unroll
+        for (int t = 0; t < HID / 2; ++t)
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(g2s[st * 32 + ci][2 * t + h], w2b[t], acc, 0, 0, 0);
+#pragma unroll
+        for (int v = 0; v < 16; ++v) {
+            const int i = st * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+            const float hv = h1s[i][u0 + ci];
+            g1s[i][u0 + ci] = acc[v] * (1.0f - hv * hv);
+        }
+        __syncthreads();
+        // this chunk's share of the weight gradients (padding samples carry zero gradients)
+#pragma unroll
+        for (int t = 0; t < FG_SPC / 2; ++t)
+            dw2 = __builtin_amdgcn_mfma_f32_32x32x2f32(g2s[2 * t + h][jw + ci], h1s[2 * t + h][kw + ci], dw2, 0, 0, 0);
+        if (w < 2) {
+#pragma unroll
+            for (int t = 0; t < FG_SPC / 2; ++t)
+                dw1 = __builtin_amdgcn_mfma_f32_32x32x2f32(g1s[2 * t + h][jw + ci], ci < OBS ? xs[2 * t + h][ci] : 0.0f,
+                                                           dw1, 0, 0, 0);
+        } else {
+            const int l = tid - 128, j = l & 63, hf = l >> 6;
+#pragma unroll 8
+            for (int k = 0; k < FG_SPC / 2; ++k) {
+                const int i = hf * (FG_SPC / 2) + k;
+                db1 += g1s[i][j];
+                db2 += g2s[i][j];
+                const float hv = h2s[i][j];
+                dw3a += gos[0][i] * hv;
+                dw3b += gos[1][i] * hv;
+            }
+        }
+    }
+    // this workgroup's partial row
+    float* P = A.wpart + (size_t)blockIdx.x * A.row_len;
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+        const int i = (v & 3) + 8 * (v >> 2) + 4 * h;
+        P[N.off[2] + (jw + i) * HID + kw + ci] = dw2[v];
+        if (w < 2 && ci < OBS) P[N.off[0] + (jw + i) * OBS + ci] = dw1[v];
+    }
+    __syncthreads();  // the chunk loop's LDS reads are done: g1s rows 0..3 become the half-sum scratch
+    if (w >= 2 && ((tid - 128) >> 6) == 1) {
+        const int j = (tid - 128) & 63;
+        g1s[0][j] = db1;
+        g1s[1][j] = db2;
+        g1s[2][j] = dw3a;
+        g1s[3][j] = dw3b;
+    }
+    __syncthreads();
+    if (w >= 2) {
+        const int l = tid - 128, j = l & 63, hf = l >> 6;
+        if (hf == 0) {
+            P[N.off[1] + j] = db1 + g1s[0][j];
+            P[N.off[3] + j] = db2 + g1s[1][j];
+            P[N.off[4] + j] = dw3a + g1s[2][j];
+            if (od == 2) P[N.off[4] + HID + j] = dw3b + g1s[3][j];
+        }
+    }
+    if (w == 0) {
+        const float a3 = wave_sum((double)db3a), b3 = wave_sum((double)db3b);
+        if (lane == 0) {
+            P[N.off[5]] = a3;
+            if (od == 2) P[N.off[5] + 1] = b3;
+        }
+    }
+    block_sum_n(q, red);
+    if (tid == 0) {
+        float* o = A.hpart + ((size_t)net * gridDim.x + blockIdx.x) * 5;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) o[k] = (float)q[k];
+    }
+}
+
 constexpr int ADAM_THREADS = 1024, ADAM_PER_THREAD = 16;  // n <= 16 384 parameters
 __global__ __launch_bounds__(ADAM_THREADS) void adam_kernel(int n, float* __restrict__ p, float* __restrict__ g,
                                                             float* __restrict__ m1, float* __restrict__ m2,
@@ -1386,6 +1608,78 @@ int32_t d2d_ppo_mlp_forward(int32_t m, const int64_t* idx, const float* obs, con
 }
 
 int32_t d2d_ppo_mlp_partial_rows(int32_t m) { return 2 * ((m + MLP_SPB - 1) / MLP_SPB); }
+
+static int n_cus() {
+    static int cached = 0;
+    if (cached == 0) {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+            n = 256;
+        cached = n;
+    }
+    return cached;
+}
+
+int32_t d2d_ppo_fused_rows(int32_t m) {
+    if (m <= 0) return 0;
+    const int nch = (m + FG_SPC - 1) / FG_SPC;
+    return nch < n_cus() ? nch : n_cus();
+}
+
+int32_t d2d_ppo_fused_grad(int32_t m, const int64_t* idx, const float* obs, const float* act, const float* old_logp,
+                           const float* adv, const float* ret, const float* log_std, const double* ws, int32_t normalize,
+                           float clip, float vf_coef, const float* const* weights, const int32_t* offsets,
+                           int32_t row_len, float* wpart, float* hpart, void* stream) {
+    if (m <= 0) return 0;
+    if (!idx || !obs || !act || !old_logp || !adv || !ret || !log_std || !weights || !offsets || !wpart || !hpart ||
+        (normalize && !ws))
+        return (int32_t)hipErrorInvalidValue;
+    FusedArgs A{};
+    for (int n = 0; n < 2; ++n) {
+        const float* const* W = weights + 6 * n;
+        A.net[n] = FusedNet{W[0], W[1], W[2], W[3], W[4], W[5], {0, 0, 0, 0, 0, 0}, n == 0 ? 2 : 1};
+        for (int k = 0; k < 6; ++k) {
+            const int o = offsets[6 * n + k];
+            const int len = k == 0 ? HID * OBS : (k == 2 ? HID * HID : (k == 4 ? A.net[n].od * HID : (k == 5 ? A.net[n].od : HID)));
+            if (o < 0 || o + len > row_len) return (int32_t)hipErrorInvalidValue;
+            A.net[n].off[k] = o;
+        }
+    }
+    A.m = m;
+    A.idx = idx;
+    A.obs = obs;
+    A.act = act;
+    A.old_logp = old_logp;
+    A.adv = adv;
+    A.ret = ret;
+    A.log_std = log_std;
+    A.ws = ws;
+    A.nbs = (m + D2D_PPO_HEAD_BLOCK - 1) / D2D_PPO_HEAD_BLOCK;
+    A.normalize = normalize;
+    A.clip = clip;
+    A.vf_coef = vf_coef;
+    A.wpart = wpart;
+    A.row_len = row_len;
+    A.hpart = hpart;
+    hipLaunchKernelGGL(mlp_fused_grad_kernel, dim3(d2d_ppo_fused_rows(m), 2), dim3(256), 0, (hipStream_t)stream, A);
+    return rc(hipGetLastError());
+}
+
+int32_t d2d_ppo_grad_reduce(int32_t n_rows, int32_t row_len, const float* partial, float* g, int32_t n_blocks,
+                            const float* head_partial, int32_t m, const float* log_std, float ent_coef,
+                            float* log_std_grad, float* acc_pl, float* acc_vl, float* acc_ent, float* acc_clip,
+                            void* stream) {
+    if (n_rows <= 0 || row_len <= 0) return 0;
+    if (!partial || !g || !head_partial || !log_std || !log_std_grad || log_std_grad < g ||
+        log_std_grad + 2 > g + row_len)
+        return (int32_t)hipErrorInvalidValue;
+    const HeadArgs H{m, n_blocks, head_partial, log_std, ent_coef, log_std_grad, acc_pl, acc_vl, acc_ent, acc_clip};
+    const AdamArgs Z{};
+    hipLaunchKernelGGL(wgrad_reduce_kernel<false>, dim3((row_len + 63) / 64 + 1), dim3(256), 0, (hipStream_t)stream,
+                       n_rows, row_len, partial, g, H, Z);
+    return rc(hipGetLastError());
+}
 
 int32_t d2d_ppo_permute(int64_t n, int32_t n_perm, uint64_t seed, uint64_t* counter, int64_t* out, void* stream) {
     if (n <= 0 || n_perm <= 0) return 0;

@@ -167,11 +167,14 @@ def ppo_native():
             "d2d_ppo_mlp_partial_rows": [i32],
             "d2d_ppo_permute": [i64, i32, C.c_uint64, vp, vp, vp],
             "d2d_ppo_rollout_step": [C.POINTER(D2DPPORollout), vp, vp],
+            "d2d_ppo_fused_rows": [i32],
+            "d2d_ppo_fused_grad": [i32, vp, vp, vp, vp, vp, vp, vp, vp, i32, f32, f32, vp, vp, i32, vp, vp, vp],
+            "d2d_ppo_grad_reduce": [i32, i32, vp, vp, i32, vp, i32, vp, f32, vp, vp, vp, vp, vp, vp],
         }
         for name, args in sig.items():
             fn = getattr(lib, name)
             fn.restype, fn.argtypes = C.c_int32, args
-        if lib.d2d_ppo_abi_version() != 4:
+        if lib.d2d_ppo_abi_version() != 5:
             raise RuntimeError("libd2d_ppo.so ABI mismatch")
         _PPO_LIB = lib
     return _PPO_LIB
@@ -233,6 +236,9 @@ class ManualStep:
         self._ticket = torch.zeros(1, dtype=torch.int32, device=device) if self.lib is not None else None
         # D2D_PPO_ADAM_SPREAD=1: the Adam step over ~11 workgroups (d2d_ppo_adam_spread) instead of one
         self.adam_spread = self.lib is not None and os.environ.get("D2D_PPO_ADAM_SPREAD", "0") == "1"
+        # D2D_PPO_FUSED=1 (default): forward + backward + weight gradients in one launch
+        # (d2d_ppo_fused_grad) + the reduce; 0: the separate kernels (forward, backward, wgrad + reduce)
+        self.fused = self.lib is not None and os.environ.get("D2D_PPO_FUSED", "1") == "1"
         o = 0
         for p in params:
             k = p.numel()
@@ -242,7 +248,7 @@ class ManualStep:
             o += k
 
     def step(self, idx, rollout, acc: dict, world: int = 1):
-        if self.fuse_adam and world == 1:
+        if self.fuse_adam and world == 1 and not self.fused:
             self._grad_hip(idx, rollout, acc, adam=True)  # gradient + clip + Adam, no exchange between
             return
         self.grad(idx, rollout, acc)
@@ -257,7 +263,10 @@ class ManualStep:
         W3p, W3v, ls = pol.action_net.weight, pol.value_net.weight, pol.log_std
         obs_all, act_all, ol_all, adv_all, ret_all = rollout
         if self.lib is not None:
-            self._grad_hip(idx, rollout, acc)
+            if self.fused:
+                self._grad_fused(idx, rollout, acc)
+            else:
+                self._grad_hip(idx, rollout, acc)
             return
         X = obs_all[idx]
         M, c = X.shape[0], cfg.clip_range
@@ -326,6 +335,45 @@ class ManualStep:
                 acc["policy_loss"].data_ptr(), acc["value_loss"].data_ptr(), acc["entropy"].data_ptr(),
                 acc["clip_fraction"].data_ptr())
         self._wgrad_hip(M, layers, hb["wpart"], head, adam)
+
+    def _grad_fused(self, idx, rollout, acc):
+        """libd2d_ppo.so, two launches (+ the advantage statistics): d2d_ppo_fused_grad (both MLPs
+        forward, the loss head, the backward and every weight / bias gradient, per-sample state on
+        chip) and d2d_ppo_grad_reduce (the workgroups' rows into G, log_std's gradient, statistics)."""
+        import ctypes as C
+
+        cfg, pol, lib, st = self.cfg, self.pol, self.lib, self._stream()
+        obs_all, act_all, ol_all, adv_all, ret_all = rollout
+        M, dev = idx.numel(), self.P.device
+        key = ("fused", M)
+        if key not in self._bufs:
+            rows = lib.d2d_ppo_fused_rows(M)
+            nb = (M + 63) // 64
+            self._bufs[key] = {"rows": rows, "wpart": torch.empty(rows * self.G.numel(), device=dev),
+                               "hpart": torch.empty(2 * rows * 5, device=dev),
+                               "ws": torch.zeros(nb, 2, dtype=torch.float64, device=dev)}
+        b = self._bufs[key]
+        pn, vn = pol.mlp_extractor.policy_net, pol.mlp_extractor.value_net
+        base = self.G.data_ptr()
+        layers = (pn[0], pn[2], pol.action_net, vn[0], vn[2], pol.value_net)
+        offs = []
+        for k in range(2):
+            for lin in layers[3 * k:3 * k + 3]:
+                offs += [(lin.weight.grad.data_ptr() - base) // 4, (lin.bias.grad.data_ptr() - base) // 4]
+        offsets = (C.c_int32 * 12)(*offs)
+        norm = int(cfg.normalize_advantage and M > 1)
+        if norm:
+            _ok(lib.d2d_ppo_adv_stats(M, idx.data_ptr(), adv_all.data_ptr(), b["ws"].data_ptr(), st), "d2d_ppo_adv_stats")
+        _ok(lib.d2d_ppo_fused_grad(M, idx.data_ptr(), obs_all.data_ptr(), act_all.data_ptr(), ol_all.data_ptr(),
+                                   adv_all.data_ptr(), ret_all.data_ptr(), pol.log_std.data_ptr(), b["ws"].data_ptr(),
+                                   norm, cfg.clip_range, cfg.vf_coef, self.weight_ptrs(), offsets, self.G.numel(),
+                                   b["wpart"].data_ptr(), b["hpart"].data_ptr(), st), "d2d_ppo_fused_grad")
+        ls = pol.log_std
+        _ok(lib.d2d_ppo_grad_reduce(b["rows"], self.G.numel(), b["wpart"].data_ptr(), base, 2 * b["rows"],
+                                    b["hpart"].data_ptr(), M, ls.data_ptr(), cfg.ent_coef, ls.grad.data_ptr(),
+                                    acc["policy_loss"].data_ptr(), acc["value_loss"].data_ptr(),
+                                    acc["entropy"].data_ptr(), acc["clip_fraction"].data_ptr(), st),
+            "d2d_ppo_grad_reduce")
 
     def weight_ptrs(self):
         """The 12 weight / bias device pointers of include/d2d_ppo.h (policy net, then value net);

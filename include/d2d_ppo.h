@@ -17,7 +17,7 @@
 extern "C" {
 #endif
 
-#define D2D_PPO_ABI_VERSION 4
+#define D2D_PPO_ABI_VERSION 5
 #define D2D_PPO_HEAD_BLOCK 64  /* v1: 256 */
 
 int32_t d2d_ppo_abi_version(void);
@@ -125,6 +125,24 @@ int32_t d2d_ppo_permute(int64_t n, int32_t n_perm, uint64_t seed, uint64_t* coun
  * RolloutBuffer.compute_returns_and_advantage (GAE(gamma, gae_lambda) with the episode starts, same
  * operation order as the torch restatement) into adv_buf / ret_buf.  Time-limit bootstrapping of
  * truncated episodes is not done here (the reference never truncates). */
+/* The minibatch gradient in one launch (ABI v5): what d2d_ppo_mlp_forward_adv + d2d_ppo_mlp_backward +
+ * d2d_ppo_wgrad compute, with every per-sample activation and gradient kept on chip.  Workgroup
+ * (x, net) handles the 64-sample chunks x, x + R, ... (R = d2d_ppo_fused_rows(m)) of rows idx[0..m) and
+ * writes its net's weight / bias gradient sums into row x of wpart ([R][row_len], at offsets[6 net
+ * + k] for W1, b1, W2, b2, W3, b3 of net 0 = policy, 1 = value) and its loss-head sums into row x
+ * (policy) / R + x (value) of hpart ([2 R][5], d2d_ppo_mlp_backward's partial-row meaning).  ws: the
+ * minibatch's d2d_ppo_adv_stats partials (normalize != 0).  d2d_ppo_grad_reduce then adds the rows
+ * into g and finishes the head (log_std gradient, statistics) as d2d_ppo_wgrad_head does. */
+int32_t d2d_ppo_fused_rows(int32_t m);
+int32_t d2d_ppo_fused_grad(int32_t m, const int64_t* idx, const float* obs, const float* act, const float* old_logp,
+                           const float* adv, const float* ret, const float* log_std, const double* ws, int32_t normalize,
+                           float clip, float vf_coef, const float* const* weights, const int32_t* offsets,
+                           int32_t row_len, float* wpart, float* hpart, void* stream);
+int32_t d2d_ppo_grad_reduce(int32_t n_rows, int32_t row_len, const float* partial, float* g, int32_t n_blocks,
+                            const float* head_partial, int32_t m, const float* log_std, float ent_coef,
+                            float* log_std_grad, float* acc_pl, float* acc_vl, float* acc_ent, float* acc_clip,
+                            void* stream);
+
 typedef struct d2d_ppo_rollout {
     int32_t n;            /* envs */
     int32_t t;            /* rollout step of obs: 0 .. T */

@@ -231,7 +231,7 @@ def test_ppo_library_exports_every_header_symbol(d2):
     for f in fns:
         assert hasattr(lib, f), f
         assert getattr(lib, f).argtypes is not None, f  # declared in ppo_native's signatures
-    assert lib.d2d_ppo_abi_version() == 4
+    assert lib.d2d_ppo_abi_version() == 5
     assert b"gfx950" in open(_build.PPO_OUT, "rb").read()
     # v4: the shuffles and the fused rollout step check their arguments before any launch
     assert lib.d2d_ppo_permute(0, 3, 1, None, None, None) == 0

@@ -192,7 +192,7 @@ def test_fused_adam_matches_separate_launch(d2):
         pol = ActorCritic()
         pol.load_state_dict(base.state_dict())
         step = ManualStep(pol.cuda(), cfg, "cuda")
-        step.fuse_adam = fuse
+        step.fuse_adam, step.fused = fuse, False  # the fused Adam rides on the separate gradient kernels
         acc = {k: torch.zeros((), device="cuda") for k in ("policy_loss", "value_loss", "entropy", "clip_fraction")}
         gi = torch.Generator().manual_seed(7)
         with torch.no_grad():
@@ -378,3 +378,42 @@ def test_rollout_step_matches_torch(d2, n):
     # where step T-1 ended the episode, the bootstrap value drops out: same bits as torch
     d = dones[T - 1]
     assert torch.equal(adv_buf[:, d], adv_ref[:, d]) and torch.equal(ret_buf[:, d], ret_ref[:, d])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M", [64, 1000, 32768, 40000])
+def test_fused_grad_matches_separate_kernels(d2, M):
+    """d2d_ppo_fused_grad + d2d_ppo_grad_reduce (forward, head, backward and weight gradients in one
+    launch, per-sample state on chip) against the separate forward / backward / wgrad kernels on
+    the same minibatch: every gradient and the loss statistics agree up to summation order."""
+    from drone2d_amd.ppo import ActorCritic, ManualStep, PPOConfig
+
+    torch.manual_seed(11)
+    base = ActorCritic()
+    with torch.no_grad():
+        base.log_std.copy_(torch.tensor([-0.3, 0.2]))
+        base.action_net.weight.mul_(30.0)
+    cfg = PPOConfig()
+    g = torch.Generator().manual_seed(12)
+    T = 50000
+    rollout = tuple(t.cuda() for t in (torch.randn(T, 27, generator=g) * 0.5, torch.randn(T, 2, generator=g),
+                                       torch.randn(T, generator=g) - 3.0, torch.randn(T, generator=g),
+                                       torch.randn(T, generator=g) * 3))
+    idx = torch.randperm(T, generator=g)[:M].cuda()
+    out = []
+    for fused in (False, True):
+        pol = ActorCritic()
+        pol.load_state_dict(base.state_dict())
+        step = ManualStep(pol.cuda(), cfg, "cuda")
+        step.fused = fused
+        acc = {k: torch.zeros((), device="cuda") for k in ("policy_loss", "value_loss", "entropy", "clip_fraction")}
+        with torch.no_grad():
+            step.grad(idx, rollout, acc)
+        torch.cuda.synchronize()
+        out.append((step.G.clone(), {k: v.clone() for k, v in acc.items()},
+                    [n for n, _ in pol.named_parameters()], [p.grad.numel() for p in pol.parameters()]))
+    (ga, aa, names, sizes), (gb, ab, _, _) = out
+    for name, a, b in zip(names, torch.split(ga, sizes), torch.split(gb, sizes)):
+        torch.testing.assert_close(b, a, rtol=2e-4, atol=1e-6, msg=name)
+    for k in aa:
+        torch.testing.assert_close(ab[k], aa[k], rtol=1e-5, atol=1e-6, msg=k)
