@@ -300,7 +300,8 @@ __device__ uint64_t* d2d_ppo_stamp_buf;
 #define PPO_STAMP(k)                                                                                  \
     do {                                                                                              \
         if (d2d_ppo_stamp_buf && (threadIdx.x & 63) == 0)                                             \
-            d2d_ppo_stamp_buf[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
+            d2d_ppo_stamp_buf[(((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 4 + (threadIdx.x >> 6)) * 8 + (k)] = \
+                __builtin_amdgcn_s_memtime();                                                         \
     } while (0)
 #else
 #define PPO_STAMP(k) \
@@ -893,14 +894,39 @@ __global__ __launch_bounds__(256, 2) void mlp_fused_grad_kernel(FusedArgs A) {
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, ci = lane & 31, h = lane >> 5;
     const int st = w >> 1, u0 = (w & 1) * 32;  // this wave's sample tile and unit half
     const int jw = (w & 1) * 32, kw = (w >> 1) * 32;  // its dW2 tile
-    // B operands, loaded once per workgroup
+    // B operands, once per workgroup: W1 and W2 staged through LDS with coalesced loads (xs and g2s
+    // as scratch: W1 rows in xs' stride, W2 rows in g2s' padded stride), then into registers (a
+    // direct gather of W's rows touches 32 cache lines per load instruction)
+    PPO_STAMP(0);
+    {
+        constexpr int NW1 = (HID * OBS + 255) / 256, NW2 = HID * HID / 256;
+        float v1[NW1], v2[NW2];
+#pragma unroll
+        for (int c = 0; c < NW1; ++c) {
+            const int e = c * 256 + tid;
+            v1[c] = e < HID * OBS ? N.w1[e] : 0.0f;
+        }
+#pragma unroll
+        for (int c = 0; c < NW2; ++c) v2[c] = N.w2[c * 256 + tid];
+#pragma unroll
+        for (int c = 0; c < NW1; ++c) {
+            const int e = c * 256 + tid;
+            if (e < HID * OBS) xs[e / OBS][e % OBS] = v1[c];
+        }
+#pragma unroll
+        for (int c = 0; c < NW2; ++c) {
+            const int e = c * 256 + tid;
+            g2s[e >> 6][e & 63] = v2[c];
+        }
+    }
+    __syncthreads();
     float w1r[(OBS + 1) / 2], w2r[HID / 2], w2b[HID / 2];
 #pragma unroll
-    for (int t = 0; t < (OBS + 1) / 2; ++t) w1r[t] = 2 * t + h < OBS ? N.w1[(u0 + ci) * OBS + 2 * t + h] : 0.0f;
+    for (int t = 0; t < (OBS + 1) / 2; ++t) w1r[t] = 2 * t + h < OBS ? xs[u0 + ci][2 * t + h] : 0.0f;
 #pragma unroll
     for (int t = 0; t < HID / 2; ++t) {
-        w2r[t] = N.w2[(u0 + ci) * HID + 2 * t + h];
-        w2b[t] = N.w2[(2 * t + h) * HID + u0 + ci];
+        w2r[t] = g2s[u0 + ci][2 * t + h];
+        w2b[t] = g2s[2 * t + h][u0 + ci];
     }
     const float b1v = N.b1[u0 + ci], b2v = N.b2[u0 + ci];
     for (int e = tid; e < 2 * (HID + 1); e += 256) {
@@ -925,17 +951,30 @@ __global__ __launch_bounds__(256, 2) void mlp_fused_grad_kernel(FusedArgs A) {
     float db1 = 0.0f, db2 = 0.0f, dw3a = 0.0f, dw3b = 0.0f, db3a = 0.0f, db3b = 0.0f;
     double q[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
     const int nch = (m + FG_SPC - 1) / FG_SPC;
+    PPO_STAMP(1);
     for (int c = blockIdx.x; c < nch; c += gridDim.x) {
         const int s0 = c * FG_SPC;
-        __syncthreads();  // the previous chunk's LDS reads are done
+        const bool first = c == (int)blockIdx.x;
+        __syncthreads();  // the previous chunk's (or the operand staging's) LDS reads are done
         if (tid < FG_SPC) rows[tid] = s0 + tid < m ? A.idx[s0 + tid] : -1;
         __syncthreads();
-        for (int e = tid; e < FG_SPC * XS; e += 256) {
-            const int i = e / XS, k = e % XS;
-            const int64_t r = rows[i];
-            xs[i][k] = (k < OBS && r >= 0) ? A.obs[r * OBS + k] : 0.0f;
+        {  // the chunk's observation rows: every load issued before the first LDS store
+            constexpr int NX = (FG_SPC * XS + 255) / 256;
+            float xv[NX];
+#pragma unroll
+            for (int q = 0; q < NX; ++q) {
+                const int e = q * 256 + tid, i = e / XS, k = e % XS;
+                const int64_t r = e < FG_SPC * XS ? rows[i] : -1;
+                xv[q] = (k < OBS && r >= 0) ? A.obs[r * OBS + k] : 0.0f;
+            }
+#pragma unroll
+            for (int q = 0; q < NX; ++q) {
+                const int e = q * 256 + tid;
+                if (e < FG_SPC * XS) xs[e / XS][e % XS] = xv[q];
+            }
         }
         __syncthreads();
+        if (first) PPO_STAMP(2);
         f32x16 acc = {};
 #pragma unroll
         for (int t = 0; t < (OBS + 1) / 2; ++t)
@@ -950,43 +989,55 @@ __global__ __launch_bounds__(256, 2) void mlp_fused_grad_kernel(FusedArgs A) {
 #pragma unroll
         for (int v = 0; v < 16; ++v) h2s[st * 32 + (v & 3) + 8 * (v >> 2) + 4 * h][u0 + ci] = ftanh(acc[v] + b2v);
         __syncthreads();
-        if (tid < FG_SPC) {  // the outputs and the loss head, one sample per thread of wave 0
-            const int i = tid, s = s0 + i;
-            float o0 = w3s[0][HID], o1 = w3s[1][HID];
-#pragma unroll 16
-            for (int j = 0; j < HID; ++j) {
+        if (first) PPO_STAMP(3);
+        {  // the outputs (four threads per sample, 16 units each) and the loss head (the first of the four)
+            const int i = tid >> 2, pq = tid & 3, s = s0 + i;
+            float o0 = 0.0f, o1 = 0.0f;
+#pragma unroll
+            for (int jj = 0; jj < HID / 4; ++jj) {
+                const int j = pq * (HID / 4) + jj;
                 const float hv = h2s[i][j];
                 o0 += w3s[0][j] * hv;
                 o1 += w3s[1][j] * hv;
             }
-            float g0 = 0.0f, g1v = 0.0f;
-            if (s < m) {
-                const int64_t j = rows[i];
-                if (net == 0) {
-                    const float z0 = (A.act[2 * j] - o0) * is0, z1 = (A.act[2 * j + 1] - o1) * is1;
-                    const float logp = (-0.5f * z0 * z0 - ls0 - HALF_LOG_2PI) + (-0.5f * z1 * z1 - ls1 - HALF_LOG_2PI);
-                    const float a = A.normalize ? (A.adv[j] - adv_mean) * adv_inv : A.adv[j];
-                    const float ratio = expf(logp - A.old_logp[j]);
-                    const float s1 = a * ratio, s2 = a * fminf(fmaxf(ratio, 1.0f - A.clip), 1.0f + A.clip);
-                    const float g_lp = (s1 <= s2) ? a * ratio * (-1.0f / m) : 0.0f;
-                    g0 = g_lp * z0 * is0;
-                    g1v = g_lp * z1 * is1;
-                    q[0] += fminf(s1, s2);
-                    q[2] += fabsf(ratio - 1.0f) > A.clip ? 1.0 : 0.0;
-                    q[3] += (double)g_lp * (z0 * z0 - 1.0f);
-                    q[4] += (double)g_lp * (z1 * z1 - 1.0f);
-                } else {
-                    const float err = A.ret[j] - o0;
-                    g0 = err * (-2.0f * A.vf_coef / m);
-                    q[1] += (double)err * err;
+            o0 += __shfl_xor(o0, 1, 64);
+            o1 += __shfl_xor(o1, 1, 64);
+            o0 += __shfl_xor(o0, 2, 64);
+            o1 += __shfl_xor(o1, 2, 64);
+            o0 += w3s[0][HID];
+            o1 += w3s[1][HID];
+            if (pq == 0) {
+                float g0 = 0.0f, g1v = 0.0f;
+                if (s < m) {
+                    const int64_t j = rows[i];
+                    if (net == 0) {
+                        const float z0 = (A.act[2 * j] - o0) * is0, z1 = (A.act[2 * j + 1] - o1) * is1;
+                        const float logp =
+                            (-0.5f * z0 * z0 - ls0 - HALF_LOG_2PI) + (-0.5f * z1 * z1 - ls1 - HALF_LOG_2PI);
+                        const float a = A.normalize ? (A.adv[j] - adv_mean) * adv_inv : A.adv[j];
+                        const float ratio = expf(logp - A.old_logp[j]);
+                        const float s1 = a * ratio, s2 = a * fminf(fmaxf(ratio, 1.0f - A.clip), 1.0f + A.clip);
+                        const float g_lp = (s1 <= s2) ? a * ratio * (-1.0f / m) : 0.0f;
+                        g0 = g_lp * z0 * is0;
+                        g1v = g_lp * z1 * is1;
+                        q[0] += fminf(s1, s2);
+                        q[2] += fabsf(ratio - 1.0f) > A.clip ? 1.0 : 0.0;
+                        q[3] += (double)g_lp * (z0 * z0 - 1.0f);
+                        q[4] += (double)g_lp * (z1 * z1 - 1.0f);
+                    } else {
+                        const float err = A.ret[j] - o0;
+                        g0 = err * (-2.0f * A.vf_coef / m);
+                        q[1] += (double)err * err;
+                    }
                 }
+                gos[0][i] = g0;
+                gos[1][i] = g1v;
+                db3a += g0;
+                db3b += g1v;
             }
-            gos[0][i] = g0;
-            gos[1][i] = g1v;
-            db3a += g0;
-            db3b += g1v;
         }
         __syncthreads();
+        if (first) PPO_STAMP(4);
         // g2 = (gout W3) (1 - h2^2)
 #pragma unroll 4
         for (int it = 0; it < FG_SPC * HID / 256; ++it) {
@@ -1008,6 +1059,7 @@ __global__ __launch_bounds__(256, 2) void mlp_fused_grad_kernel(FusedArgs A) {
             g1s[i][u0 + ci] = acc[v] * (1.0f - hv * hv);
         }
         __syncthreads();
+        if (first) PPO_STAMP(5);
         // this chunk's share of the weight gradients (padding samples carry zero gradients)
 #pragma unroll
         for (int t = 0; t < FG_SPC / 2; ++t)
@@ -1029,6 +1081,7 @@ __global__ __launch_bounds__(256, 2) void mlp_fused_grad_kernel(FusedArgs A) {
                 dw3b += gos[1][i] * hv;
             }
         }
+        if (first) PPO_STAMP(6);
     }
     // this workgroup's partial row
     float* P = A.wpart + (size_t)blockIdx.x * A.row_len;
@@ -1056,12 +1109,11 @@ __global__ __launch_bounds__(256, 2) void mlp_fused_grad_kernel(FusedArgs A) {
             if (od == 2) P[N.off[4] + HID + j] = dw3b + g1s[3][j];
         }
     }
-    if (w == 0) {
-        const float a3 = wave_sum((double)db3a), b3 = wave_sum((double)db3b);
-        if (lane == 0) {
-            P[N.off[5]] = a3;
-            if (od == 2) P[N.off[5] + 1] = b3;
-        }
+    double b3[2] = {(double)db3a, (double)db3b};  // the head threads' output-bias sums
+    block_sum_n(b3, red);
+    if (tid == 0) {
+        P[N.off[5]] = (float)b3[0];
+        if (od == 2) P[N.off[5] + 1] = (float)b3[1];
     }
     block_sum_n(q, red);
     if (tid == 0) {
@@ -1069,6 +1121,7 @@ __global__ __launch_bounds__(256, 2) void mlp_fused_grad_kernel(FusedArgs A) {
 #pragma unroll
         for (int k = 0; k < 5; ++k) o[k] = (float)q[k];
     }
+    PPO_STAMP(7);
 }
 
 constexpr int ADAM_THREADS = 1024, ADAM_PER_THREAD = 16;  // n <= 16 384 parameters

@@ -74,6 +74,27 @@ for n in (4096, 16384, 32768, 65536):
                           "p90_end": int(np.percentile(rel[:, :, 6], 90))}), flush=True)
     us = timed(lambda: lib.d2d_ppo_rollout_step(C.byref(r), wp, st))
     print(json.dumps({"kernel": "rollout_step", "n": n, "us": round(us, 2), "workgroups": (n + 63) // 64}), flush=True)
+    if STAMPS and n == 32768:  # the fused gradient kernel's phases
+        M = n
+        rollout = (torch.rand(M, 27, device="cuda"), torch.randn(M, 2, device="cuda"),
+                   torch.randn(M, device="cuda") - 3, torch.randn(M, device="cuda"), torch.randn(M, device="cuda"))
+        idx = torch.randperm(M, device="cuda")
+        acc = {k: torch.zeros((), device="cuda") for k in ("policy_loss", "value_loss", "entropy", "clip_fraction")}
+        man.fused = True
+        for _ in range(3):
+            man.grad(idx, rollout, acc)
+        rows = lib.d2d_ppo_fused_rows(M)
+        sbuf = torch.zeros(2 * rows * 4 * 8, dtype=torch.int64, device="cuda")
+        lib.d2d_ppo_debug_stamps(C.c_void_p(sbuf.data_ptr()))
+        man.grad(idx, rollout, acc)
+        torch.cuda.synchronize()
+        lib.d2d_ppo_debug_stamps(None)
+        a = sbuf.cpu().numpy().reshape(2 * rows, 4, 8).astype(np.int64)
+        rel = a - a[:, :, :1].min(1)[:, None, :]
+        print(json.dumps({"fused_stamps_m": M, "rows": rows,
+                          "phase_cycles_median_per_wave": np.median(rel, 0).astype(int).tolist(),
+                          "end_p90": int(np.percentile(rel[:, :, 7], 90)), "end_max": int(rel[:, :, 7].max())}),
+              flush=True)
     # the minibatch forward + backward on n rollout rows
     M = n
     rollout = (torch.rand(M, 27, device="cuda"), torch.randn(M, 2, device="cuda"), torch.randn(M, device="cuda") - 3,
