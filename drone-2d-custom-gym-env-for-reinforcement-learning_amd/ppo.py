@@ -247,14 +247,14 @@ class ManualStep:
             p.grad = self.G[o:o + k].view_as(p)
             o += k
 
-    def step(self, idx, rollout, acc: dict, world: int = 1):
+    def step(self, idx, rollout, acc: dict, world: int = 1, adv_ws=None):
         if self.fuse_adam and world == 1 and not self.fused:
             self._grad_hip(idx, rollout, acc, adam=True)  # gradient + clip + Adam, no exchange between
             return
-        self.grad(idx, rollout, acc)
+        self.grad(idx, rollout, acc, adv_ws)
         self.apply(world)
 
-    def grad(self, idx, rollout, acc: dict):
+    def grad(self, idx, rollout, acc: dict, adv_ws=None):
         """The loss gradient of minibatch ``idx`` of ``rollout`` = (obs, actions, old log-probs,
         advantages, returns) into ``G``; statistics added to ``acc``."""
         cfg, pol = self.cfg, self.pol
@@ -264,7 +264,7 @@ class ManualStep:
         obs_all, act_all, ol_all, adv_all, ret_all = rollout
         if self.lib is not None:
             if self.fused:
-                self._grad_fused(idx, rollout, acc)
+                self._grad_fused(idx, rollout, acc, adv_ws)
             else:
                 self._grad_hip(idx, rollout, acc)
             return
@@ -336,10 +336,11 @@ class ManualStep:
                 acc["clip_fraction"].data_ptr())
         self._wgrad_hip(M, layers, hb["wpart"], head, adam)
 
-    def _grad_fused(self, idx, rollout, acc):
-        """libd2d_ppo.so, two launches (+ the advantage statistics): d2d_ppo_fused_grad (both MLPs
-        forward, the loss head, the backward and every weight / bias gradient, per-sample state on
-        chip) and d2d_ppo_grad_reduce (the workgroups' rows into G, log_std's gradient, statistics)."""
+    def _grad_fused(self, idx, rollout, acc, adv_ws=None):
+        """libd2d_ppo.so, two launches (+ the advantage statistics unless ``adv_ws`` points at this
+        minibatch's precomputed d2d_ppo_adv_stats partials): d2d_ppo_fused_grad (both MLPs forward,
+        the loss head, the backward and every weight / bias gradient, per-sample state on chip) and
+        d2d_ppo_grad_reduce (the workgroups' rows into G, log_std's gradient, statistics)."""
         import ctypes as C
 
         cfg, pol, lib, st = self.cfg, self.pol, self.lib, self._stream()
@@ -362,10 +363,11 @@ class ManualStep:
                 offs += [(lin.weight.grad.data_ptr() - base) // 4, (lin.bias.grad.data_ptr() - base) // 4]
         offsets = (C.c_int32 * 12)(*offs)
         norm = int(cfg.normalize_advantage and M > 1)
-        if norm:
-            _ok(lib.d2d_ppo_adv_stats(M, idx.data_ptr(), adv_all.data_ptr(), b["ws"].data_ptr(), st), "d2d_ppo_adv_stats")
+        ws = adv_ws if adv_ws is not None else b["ws"].data_ptr()
+        if norm and adv_ws is None:
+            _ok(lib.d2d_ppo_adv_stats(M, idx.data_ptr(), adv_all.data_ptr(), ws, st), "d2d_ppo_adv_stats")
         _ok(lib.d2d_ppo_fused_grad(M, idx.data_ptr(), obs_all.data_ptr(), act_all.data_ptr(), ol_all.data_ptr(),
-                                   adv_all.data_ptr(), ret_all.data_ptr(), pol.log_std.data_ptr(), b["ws"].data_ptr(),
+                                   adv_all.data_ptr(), ret_all.data_ptr(), pol.log_std.data_ptr(), ws,
                                    norm, cfg.clip_range, cfg.vf_coef, self.weight_ptrs(), offsets, self.G.numel(),
                                    b["wpart"].data_ptr(), b["hpart"].data_ptr(), st), "d2d_ppo_fused_grad")
         ls = pol.log_std
@@ -549,6 +551,7 @@ class PPO:
         self._perm_ctr = torch.zeros(1, dtype=torch.int64, device=dev)
         self._perm_seed = (seed * 0x9E3779B97F4A7C15 + rank * 0xD1B54A32D192ED03 + 1) % (1 << 64)
         self._upd_warm = False
+        self._adv_ws = None      # every minibatch's advantage-statistics partials (_train_body_hip)
         self._fused = None       # decided at the first rollout (_alloc_rollout)
 
     # ------------------------------------------------------------------ rollout
@@ -697,12 +700,12 @@ class PPO:
         return {"episodes": f, "mean_return": r / f if f else float("nan")}
 
     # ------------------------------------------------------------------ update
-    def _minibatch(self, idx: torch.Tensor, zero_grad: bool = True):
+    def _minibatch(self, idx: torch.Tensor, zero_grad: bool = True, adv_ws=None):
         """One SB3 PPO gradient step on rollout samples ``idx`` (statistics accumulated on device)."""
         obs, act, old_logp, adv_all, ret = self._flat
         if self.manual is not None:
             with torch.no_grad():
-                self.manual.step(idx, self._flat, self._acc, self.world)
+                self.manual.step(idx, self._flat, self._acc, self.world, adv_ws)
             return
         c = self.cfg.clip_range
         params = list(self.policy.parameters())
@@ -758,11 +761,24 @@ class PPO:
         M, bs, E = self._flat[0].shape[0], self.cfg.batch_size, self.cfg.n_epochs
         for v in self._acc.values():
             v.zero_()
-        _ok(self.manual.lib.d2d_ppo_permute(M, E, self._perm_seed, self._perm_ctr.data_ptr(), self._perm.data_ptr(),
-                                            self.manual._stream()), "d2d_ppo_permute")
+        lib, st = self.manual.lib, self.manual._stream()
+        _ok(lib.d2d_ppo_permute(M, E, self._perm_seed, self._perm_ctr.data_ptr(), self._perm.data_ptr(), st),
+            "d2d_ppo_permute")
+        # the advantage statistics of every minibatch of the update in one launch: 64-row partials over
+        # the whole shuffle; minibatch boundaries fall on partial boundaries when M and bs are multiples
+        # of 64, so each minibatch reads its own slice (otherwise each minibatch computes its own)
+        ws = None
+        if self.manual.fused and self.cfg.normalize_advantage and M % 64 == 0 and bs % 64 == 0:
+            if self._adv_ws is None:
+                self._adv_ws = torch.zeros(E * M // 64, 2, dtype=torch.float64, device=self.device)
+            _ok(lib.d2d_ppo_adv_stats(E * M, self._perm.data_ptr(), self._flat[3].data_ptr(),
+                                      self._adv_ws.data_ptr(), st), "d2d_ppo_adv_stats")
+            ws = self._adv_ws
         for e in range(E):
             for s in range(0, M, bs):
-                self._minibatch(self._perm[e * M + s:e * M + min(s + bs, M)])
+                n = min(s + bs, M) - s
+                aw = ws[(e * M + s) // 64:].data_ptr() if (ws is not None and n > 1) else None
+                self._minibatch(self._perm[e * M + s:e * M + s + n], adv_ws=aw)
 
     def train(self) -> dict:
         M, bs = self._flat[0].shape[0], self.cfg.batch_size
