@@ -285,6 +285,9 @@ hipError_t rc_rebuild(d2d_t* h, hipStream_t stream) {
 // of three or more (everything through L1/L2).  Groups are then
 // ordered by their first env id, so groups whose envs interleave (e.g. scenario = id mod 7) get
 // consecutive numbers (xcd_group places consecutive numbers on one XCD).
+#ifndef D2D_STRADDLE_W
+#define D2D_STRADDLE_W 1.25  // balance_groups: a straddling group's cost over its heavier scenario's
+#endif
 // host copy of the kernels' block -> group numbering (d2d_kernels.h xcd_group)
 int xcd_group_host(int b, int nb) {
     const int per = nb / 8, rem = nb % 8, x = b % 8, k = b / 8;
@@ -306,7 +309,7 @@ void balance_groups(int n_cu, const double* cost, int n_cost, std::vector<int32_
     auto c = [&](int sc) { return (sc >= 0 && sc < n_cost) ? cost[sc] : cmax; };
     auto gcost = [&](int g) {
         const int w = ws[(size_t)g];
-        return w >= 0 ? c(w) : (w <= -2 ? 1.25 * std::max(c(-w - 2), c(-w - 1)) : 1.5 * cmax);
+        return w >= 0 ? c(w) : (w <= -2 ? D2D_STRADDLE_W * std::max(c(-w - 2), c(-w - 1)) : 1.5 * cmax);
     };
     std::vector<int32_t> block_of((size_t)ng);  // group number -> the block that runs it
     for (int b = 0; b < ng; ++b) block_of[(size_t)xcd_group_host(b, ng)] = b;
