@@ -167,6 +167,9 @@ struct StepArgs {
 #ifndef D2D_SPLIT
 #define D2D_SPLIT 1      // W3 re-checks the second half of W2's golden-march table (0: W2 alone)
 #endif
+#ifndef D2D_W0_TAIL
+#define D2D_W0_TAIL 0    // W0 stores its velocity observation after the reward hand-off (A/B knob)
+#endif
 #ifndef D2D_OBS_VEC
 #define D2D_OBS_VEC 1    // K1 stores its observation tile with 16-byte stores
 #endif
@@ -557,9 +560,9 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const Scn* scns, cons
         }
         flag_raise(sh.f_gs);
         STAMP(4);
-        // velocity part of the observation (obs 0-2, 17-18) into the tile / terminal obs
-        if (valid) {
-            sensor_vel(F0, sn[0], cs[0], ov);
+        // velocity part of the observation (obs 0-2, 17-18) into the tile / terminal obs (D2D_W0_TAIL:
+        // stored after the reward hand-off below, which W2 waits for)
+        const auto vel_obs_out = [&]() {
             if (!(done && auto_reset)) {
                 orow[0] = (float)ov[0];
                 orow[1] = (float)ov[1];
@@ -574,6 +577,10 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const Scn* scns, cons
                 trow[17] = (float)ov[17];
                 trow[18] = (float)ov[18];
             }
+        };
+        if (valid) {
+            sensor_vel(F0, sn[0], cs[0], ov);
+            if (!D2D_W0_TAIL) vel_obs_out();
         }
         // velocity part of the reward (speed, velocity angle, CA total), for W2
         flag_wait(sh.f_ca);
@@ -594,6 +601,7 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const Scn* scns, cons
             dclose = C.d;
         }
         flag_raise(sh.f_pre);
+        if (D2D_W0_TAIL && valid) vel_obs_out();
     } else if (wave == 1) {
         // ---------------------------------------------------------------- sensing
         float row[19];
