@@ -54,10 +54,27 @@ constexpr double VEL_MAX = 1330.0;            // drone_2d_env.py:635
 //   RN(1 / (us[n+1] - us[n])), and the blend threshold T: in interval n QPMI2D.__call__ blends the
 //   two quadratics exactly when u < T[n] (below).
 enum { REC_XB = 0, REC_XA = 6, REC_U0 = 12, REC_U1 = 13, REC_IDU = 14, REC_T = 15, REC_N = 16 };
+// Record layout.  D2D_REC_RM = 1: record-major with a one-double pad (interval n's 16 fields are
+// contiguous, 136 bytes apart): from LDS a wave whose lanes sit in different intervals still reads
+// 16 different banks per field (n x 34 dwords mod 64 is distinct for n < 16), and from global memory
+// (the fresh curriculum's per-lane scenarios) one QPMI2D evaluation touches 2-3 cache lines per lane
+// instead of 16.  The knots are the records' u0 column (us[k] = rec[k][REC_U0]; +inf past n_wps).
+// 0: field-major rec[f][n] plus a separate us[] (rounds 1-3).  Same size either way.  Measured
+// (profiles/r03/recrm/, parity green with either): 1 makes the fresh curriculum's step 1.70 x
+// faster (883 -> 521 us at 65 536 envs) but the LDS paths 0.7 % (corridor) to 3.7 % (mixed) slower,
+// so the BASELINE configs keep 0 until the global-memory instantiations get their own layout.
+#ifndef D2D_REC_RM
+#define D2D_REC_RM 0
+#endif
+constexpr int REC_W = REC_N + 1;
 struct Scn {
     int32_t n_wps, n_circles;
-    double us[D2D_MAX_WPS];
-    double rec[REC_N][D2D_MAX_WPS];
+#if D2D_REC_RM
+    double rec_[D2D_MAX_WPS][REC_W];
+#else
+    double us_[D2D_MAX_WPS];
+    double rec_[REC_N][D2D_MAX_WPS];
+#endif
     double cx[D2D_MAX_CIRCLES], cy[D2D_MAX_CIRCLES], cr[D2D_MAX_CIRCLES];
     double wp_last_x, wp_last_y;
     double spawn_xmin, spawn_xmax, spawn_ymin, spawn_ymax, spawn_amin, spawn_amax;
@@ -65,6 +82,14 @@ struct Scn {
                        // (also keeps sizeof(Scn) % 16 == 0: the probe tables staged after it stay aligned)
 };
 static_assert(sizeof(Scn) % 16 == 0, "Scn size");
+#if D2D_REC_RM
+#define SREC(s, f, n) ((s).rec_[(n)][(f)])
+#define SUS(s, k) ((s).rec_[(k)][REC_U0])
+#else
+#define SREC(s, f, n) ((s).rec_[(f)][(n)])
+#define SUS(s, k) ((s).us_[(k)])
+#endif
+
 // Returns false if the table is outside what the record form reproduces exactly: the last-segment
 // window us[nw-2] - 0.001 must not reach back past us[nw-3] (always true for real waypoints).
 __host__ __device__ inline bool scn_build(const d2d_scn& a, Scn& s) {
@@ -72,25 +97,31 @@ __host__ __device__ inline bool scn_build(const d2d_scn& a, Scn& s) {
     if (nw >= 4 && !(a.us[nw - 2] - 0.001 > a.us[nw - 3])) return false;
     s.n_wps = nw;
     s.n_circles = a.n_circles;
-    for (int k = 0; k < D2D_MAX_WPS; ++k) s.us[k] = (k < nw) ? a.us[k] : __builtin_inf();
+    double us[D2D_MAX_WPS];
+    for (int k = 0; k < D2D_MAX_WPS; ++k) us[k] = (k < nw) ? a.us[k] : __builtin_inf();
+#if !D2D_REC_RM
+    for (int k = 0; k < D2D_MAX_WPS; ++k) s.us_[k] = us[k];
+#else
+    for (int n = 0; n < D2D_MAX_WPS; ++n) s.rec_[n][REC_N] = 0.0;  // the pad
+#endif
     for (int n = 0; n < D2D_MAX_WPS; ++n) {
         const int b = (n < nseg - 1) ? n : nseg - 1;
         const int q = (n == 0) ? nseg - 1 : ((n - 1 < nseg - 1) ? n - 1 : nseg - 1);
         const double v[REC_N] = {a.xa[b], a.xb[b], a.xc[b], a.ya[b], a.yb[b], a.yc[b],
                                  a.xa[q], a.xb[q], a.xc[q], a.ya[q], a.yb[q], a.yc[q], 0.0, 0.0, 0.0};
-        for (int f = 0; f < REC_N; ++f) s.rec[f][n] = v[f];
+        for (int f = 0; f < REC_N; ++f) SREC(s, f, n) = v[f];
         const int n1 = (n + 1 < D2D_MAX_WPS) ? n + 1 : D2D_MAX_WPS - 1;
-        s.rec[REC_U0][n] = s.us[n];
-        s.rec[REC_U1][n] = s.us[n1];
-        s.rec[REC_IDU][n] = 1.0 / (s.us[n1] - s.us[n]);
+        SREC(s, REC_U0, n) = us[n];
+        SREC(s, REC_U1, n) = us[n1];
+        SREC(s, REC_IDU, n) = 1.0 / (us[n1] - us[n]);
         // predef_path.py:88-142 per interval n = u_index(u): "first" (u in [us[0], us[1]], B only),
         // "last" (u in [us[-2] - 0.001, us[-1]] or n == nw-1, B only), else the blend.  For n < nw-1
         // u <= us[n+1] <= L, so last <=> u >= last_lo; for n = 0, first <=> u >= us[0].  Hence blend
         // <=> u < T[n] with T[0] = min(us[0], last_lo), T[0 < n < nw-1] = last_lo, T[nw-1] = -inf
         // (also for NaN u, which u_index maps to nw-1).  scn_build's check above keeps last_lo
         // inside interval nw-3.
-        const double last_lo = s.us[nw - 2] - 0.001;
-        s.rec[REC_T][n] = (n == 0) ? (s.us[0] < last_lo ? s.us[0] : last_lo)
+        const double last_lo = us[nw - 2] - 0.001;
+        SREC(s, REC_T, n) = (n == 0) ? (us[0] < last_lo ? us[0] : last_lo)
                                    : (n < nw - 1 ? last_lo : -__builtin_inf());
     }
     for (int k = 0; k < D2D_MAX_CIRCLES; ++k) {
@@ -254,8 +285,8 @@ __device__ __forceinline__ int u_index(const Scn& s, double u) {
     uint32_t c = 0;
 #pragma unroll
     for (int k = 1; k < D2D_MAX_WPS; ++k) {
-        if (D2D_KNOT_CMP) c += !(u <= s.us[k]) ? 1u : 0u;
-        else c += (uint32_t)__double2hiint(s.us[k] - u) >> 31;
+        if (D2D_KNOT_CMP) c += !(u <= SUS(s, k)) ? 1u : 0u;
+        else c += (uint32_t)__double2hiint(SUS(s, k) - u) >> 31;
     }
     const int nw1 = s.n_wps - 1;
     return (u != u) ? nw1 : min((int)c, nw1);
@@ -267,7 +298,7 @@ struct PathK {
 };
 __device__ __forceinline__ PathK path_k(const Scn& s) {
     const int nw = s.n_wps;
-    return PathK{s.us[0], s.us[nw - 2] - 0.001, s.us[nw - 1], nw};
+    return PathK{SUS(s, 0), SUS(s, nw - 2) - 0.001, SUS(s, nw - 1), nw};
 }
 // QPMI2D.__call__ (predef_path.py:88-142), branch-free: both candidate quadratics are evaluated
 // and the reference's case analysis picks the result with selects (same arithmetic per case).
@@ -295,7 +326,7 @@ __device__ __forceinline__ void path_eval_n(const Scn& s, const PathK& K, double
                                             double& u1_out) {
     double r[REC_N];
 #pragma unroll
-    for (int f = 0; f < REC_N; ++f) r[f] = s.rec[f][n];
+    for (int f = 0; f < REC_N; ++f) r[f] = SREC(s, f, n);
     path_eval_rec(r, K, u, n, x, y, u1_out);
 }
 __device__ __forceinline__ void path_eval(const Scn& s, const PathK& K, double u, double& x, double& y) {
@@ -341,7 +372,7 @@ __device__ __forceinline__ void brent_init(const Scn& s, const PathK& K, double 
     B.e = 0.0;
     B.ia = u_index(s, B.a);
     B.ib = u_index(s, B.b);
-    B.ka = s.rec[REC_U1][B.ia];
+    B.ka = SREC(s, REC_U1, B.ia);
     B.ixf = u_index(s, B.xf);
     B.fx = path_dist_n(s, K, B.xf, B.ixf, px, py, B.kxf);
     B.num = 1;
@@ -374,9 +405,9 @@ __device__ __forceinline__ void brent_step(const Scn& s, const PathK& K, double 
     double rp[REC_N];
     if (D2D_RECPF) {
 #pragma unroll
-        for (int f = 0; f < REC_N; ++f) rp[f] = s.rec[f][B.ia];
+        for (int f = 0; f < REC_N; ++f) rp[f] = SREC(s, f, B.ia);
     }
-    const double ka = D2D_KTRACK ? B.ka : (D2D_RECPF ? rp[REC_U1] : s.rec[REC_U1][B.ia]);
+    const double ka = D2D_KTRACK ? B.ka : (D2D_RECPF ? rp[REC_U1] : SREC(s, REC_U1, B.ia));
     const double xm = 0.5 * (a + b);
     const double tol1 = BR_SQRT_EPS * fabs(xf) + BR_XATOL3;
     const double tol2 = 2.0 * tol1;
@@ -429,7 +460,7 @@ __device__ __forceinline__ void brent_step(const Scn& s, const PathK& K, double 
         double xq, yq;
         if (__ballot(ix != B.ia) != 0ull) {
 #pragma unroll
-            for (int f = 0; f < REC_N; ++f) rp[f] = (ix != B.ia) ? s.rec[f][ix] : rp[f];
+            for (int f = 0; f < REC_N; ++f) rp[f] = (ix != B.ia) ? SREC(s, f, ix) : rp[f];
         }
         path_eval_rec(rp, K, x, ix, xq, yq, kx);
         fu = norm2(xq - px, yq - py);
@@ -534,7 +565,7 @@ __device__ __forceinline__ void brtab_build(const Scn& s, int kind, BrTab& T) {
     B.e = 0.0;
     B.ia = u_index(s, B.a);
     B.ib = u_index(s, B.b);
-    B.ka = s.rec[REC_U1][B.ia];
+    B.ka = SREC(s, REC_U1, B.ia);
     B.ixf = u_index(s, B.xf);
     B.num = 1;
     B.fx = B.ffulc = B.fnfc = 0.0;
@@ -1215,7 +1246,7 @@ __device__ __forceinline__ void path_obs_u(const d2d_cfg& cfg, const Scn& s, dou
     const double W = cfg.screen_w, H = cfg.screen_h;
     double cpx, cpy, u1;
     path_eval_n(s, path_k(s), u, (iu >= 0) ? iu : u_index(s, u), cpx, cpy, u1);
-    const double L = s.us[s.n_wps - 1];
+    const double L = SUS(s, s.n_wps - 1);
     const double ula = (u + cfg.lookahead > L) ? L : u + cfg.lookahead;
     double lax, lay;
     path_eval(s, ula, lax, lay);
@@ -1246,7 +1277,7 @@ template <bool LT = false>
 __device__ __forceinline__ void path_obs(const d2d_cfg& cfg, const Scn& s, const BrTab* T, double x, double y,
                                          double al, uint32_t& flags, double o[8], const BtHot* hot = nullptr) {
     int iu = -1;
-    const double u = (D2D_ABLATE & 1) ? clipd(x - 100.0, -10.0, s.us[s.n_wps - 1])
+    const double u = (D2D_ABLATE & 1) ? clipd(x - 100.0, -10.0, SUS(s, s.n_wps - 1))
                      : (T ? (LT ? closest_u_tab<true>(s, *T, hot, x, y, iu)
                                 : closest_u_tab<false>(s, *T, &T->hot, x, y, iu))
                           : closest_u(s, x, y, iu));

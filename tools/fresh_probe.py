@@ -14,7 +14,8 @@ from drone2d_amd.config import ENV_TRAIN_CONFIG  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 400
-venv = d2.Drone2dVecEnv(n, seed=0, with_info=False,
+lib = sys.argv[3] if len(sys.argv) > 3 else None  # an alternative build (tools/variants.py)
+venv = d2.Drone2dVecEnv(n, seed=0, with_info=False, native_lib=lib,
                         **dict(ENV_TRAIN_CONFIG, mode="curriculum", scenario="curriculum", sim_num=0))
 venv.reset(seed=0)
 g = torch.Generator(device="cuda").manual_seed(0)
@@ -28,5 +29,5 @@ for k in range(steps):
     venv.step(acts[k % 16])
 b.record()
 torch.cuda.synchronize()
-print(f"fresh curriculum, {n} envs: {a.elapsed_time(b) * 1000 / steps:.1f} us per step "
+print(f"fresh curriculum{' (' + os.path.basename(lib) + ')' if lib else ''}, {n} envs: {a.elapsed_time(b) * 1000 / steps:.1f} us per step "
       f"({n * steps / (a.elapsed_time(b) / 1000) / 1e9:.3f} G env-steps/s, eager)", flush=True)
