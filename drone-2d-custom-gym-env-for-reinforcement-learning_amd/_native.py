@@ -14,6 +14,8 @@ from . import abi
 LIB_NAME = "libdrone2d_hip.so"
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
 LIB_PATH = os.path.join(LIB_DIR, LIB_NAME)
+# the record-major build of the same source (fresh curriculum: per-env scenarios in global memory)
+LIB_PATH_RM = os.path.join(LIB_DIR, "libdrone2d_hip_rm.so")
 
 # every entry point of include/drone2d.h: name -> (restype, argtypes)
 _VP = C.c_void_p
@@ -46,6 +48,7 @@ SIGNATURES = {
 }
 
 _lib = None
+_libs: dict = {}  # other builds, by path (one CDLL each)
 
 
 class NativeError(RuntimeError):
@@ -57,6 +60,8 @@ def load(path: str | None = None) -> C.CDLL:
     global _lib
     if _lib is not None and path is None:
         return _lib
+    if path is not None and path in _libs:
+        return _libs[path]
     p = path or LIB_PATH
     if not os.path.exists(p):
         raise NativeError(f"{p} not found: the HIP extension is not built "
@@ -75,10 +80,15 @@ def load(path: str | None = None) -> C.CDLL:
         raise NativeError(f"{p}: ABI version {v}, expected {abi.ABI_VERSION}")
     if path is None:
         _lib = lib
+    else:
+        _libs[path] = lib
     return lib
 
 
-def check(code: int, what: str) -> None:
+def check(code: int, what: str, lib: C.CDLL | None = None) -> None:
+    """Raise ``NativeError`` for a non-OK status; the message is ``lib``'s (default: the main build's)
+    thread-local ``d2d_last_error``."""
     if code != abi.E_OK:
-        msg = _lib.d2d_last_error().decode() if _lib is not None else ""
+        src = lib if lib is not None else _lib
+        msg = src.d2d_last_error().decode() if src is not None else ""
         raise NativeError(f"{what} failed (code {code}): {msg}")

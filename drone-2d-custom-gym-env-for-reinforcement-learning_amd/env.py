@@ -17,7 +17,7 @@ import numpy as np
 import torch
 
 from . import abi
-from ._native import check, load
+from ._native import LIB_PATH_RM, check, load
 from .config import CURRICULUM_STAGES, SCENARIO_STEP_COST, TEST_SCENARIOS, make_cfg
 from .scenarios import Scenario, create_test_scenario, free_flight
 
@@ -137,7 +137,11 @@ class Drone2dVecEnv:
                  timeup_truncates: bool = False, with_info: bool = True, env_id_offset: int = 0,
                  native_lib: str | None = None, envs_total: int | None = None, **kwargs):
         self.kwargs = dict(kwargs)
-        self._lib = load(native_lib)  # native_lib: alternative build (diagnostics only)
+        self.fresh = is_fresh_curriculum(self.kwargs)
+        # the fresh curriculum reads every env's own scenario from global memory: the record-major
+        # build of the same source (D2D_REC_RM=1, 1.7 x faster there); native_lib: an alternative
+        # build (diagnostics only)
+        self._lib = load(native_lib if native_lib is not None else (LIB_PATH_RM if self.fresh else None))
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device())
         self.device = torch.device(device)
@@ -149,7 +153,6 @@ class Drone2dVecEnv:
         self.cfg = make_cfg(self.kwargs, auto_reset=auto_reset, timeup_truncates=timeup_truncates,
                             env_id_base=env_id_offset)
         self.envs_total = int(envs_total) if envs_total is not None else self.num_envs
-        self.fresh = is_fresh_curriculum(self.kwargs)
         self.scenarios = [] if self.fresh else build_scenarios(self.kwargs)
         # curriculum: every reset draws a fresh device-generated scenario (2) or a pool entry (1)
         self.cfg.scn_pool = (2 if self.fresh else 1) if is_curriculum(self.kwargs) else 0
@@ -159,7 +162,7 @@ class Drone2dVecEnv:
         self.observation_space = _make_box(-np.ones(27), np.ones(27))
 
         h = C.c_void_p()
-        check(self._lib.d2d_create(C.byref(self.cfg), self.num_envs, self.device.index, C.byref(h)), "d2d_create")
+        self._check(self._lib.d2d_create(C.byref(self.cfg), self.num_envs, self.device.index, C.byref(h)), "d2d_create")
         self._h = h
         self._upload_scenarios(env_scenario)
 
@@ -176,11 +179,14 @@ class Drone2dVecEnv:
         self._stats = torch.zeros(abi.NSTATS, dtype=torch.float64, device=dev)
 
     # ------------------------------------------------------------------ plumbing
+    def _check(self, code: int, what: str) -> None:
+        check(code, what, self._lib)  # the error text of this handle's library
+
     def _upload_scenarios(self, env_scenario=None):
         if self.fresh:
             self.curriculum = make_curriculum(self.kwargs, self.envs_total)
             self.env_scenario = 2 * np.arange(self.num_envs, dtype=np.int32)
-            check(self._lib.d2d_set_curriculum(self._h, C.byref(self.curriculum)), "d2d_set_curriculum")
+            self._check(self._lib.d2d_set_curriculum(self._h, C.byref(self.curriculum)), "d2d_set_curriculum")
             return
         n_scn = len(self.scenarios)
         arr = (abi.D2DScn * n_scn)(*[s.to_c() for s in self.scenarios])
@@ -190,12 +196,12 @@ class Drone2dVecEnv:
         if es.shape != (self.num_envs,):
             raise ValueError("env_scenario must have shape [num_envs]")
         self.env_scenario = es  # in curriculum mode: the initial map only (resets redraw on device)
-        check(self._lib.d2d_set_scenarios(self._h, arr, n_scn, es.ctypes.data_as(C.POINTER(C.c_int32))),
+        self._check(self._lib.d2d_set_scenarios(self._h, arr, n_scn, es.ctypes.data_as(C.POINTER(C.c_int32))),
               "d2d_set_scenarios")
         if not self.cfg.scn_pool and n_scn > 1:  # step costs for the quad workgroups' heavy / light pairing
             cost = (C.c_double * n_scn)(*[SCENARIO_STEP_COST.get(s.name.removesuffix("_free"), 32.0)
                                           for s in self.scenarios])
-            check(self._lib.d2d_set_scenario_costs(self._h, cost, n_scn), "d2d_set_scenario_costs")
+            self._check(self._lib.d2d_set_scenario_costs(self._h, cost, n_scn), "d2d_set_scenario_costs")
 
     def set_curriculum(self, stage: str | None = None, sim_num: int | None = None, pool: int | None = None,
                        seed: int | None = None) -> torch.Tensor:
@@ -238,7 +244,7 @@ class Drone2dVecEnv:
         kw["curriculum_seed"] = int(seed) if seed is not None else int(kw.get("curriculum_seed", 0)) + 1
         scns = build_scenarios(kw)
         arr = (abi.D2DScn * len(scns))(*[s.to_c() for s in scns])
-        check(self._lib.d2d_refresh_pool(self._h, arr, len(scns)), "d2d_refresh_pool")
+        self._check(self._lib.d2d_refresh_pool(self._h, arr, len(scns)), "d2d_refresh_pool")
         self.kwargs, self.scenarios = kw, scns
 
     def _stream(self):
@@ -269,7 +275,7 @@ class Drone2dVecEnv:
         m = None
         if mask is not None:
             m = mask.to(device=self.device, dtype=torch.uint8).contiguous()
-        check(self._lib.d2d_reset(self._h, self._ptr(m), C.c_uint64(self.seed_value & (2 ** 64 - 1)),
+        self._check(self._lib.d2d_reset(self._h, self._ptr(m), C.c_uint64(self.seed_value & (2 ** 64 - 1)),
                                   self._ptr(b["obs"]), self._stream()), "d2d_reset")
         return b["obs"]
 
@@ -289,7 +295,7 @@ class Drone2dVecEnv:
         a = self._prep_actions(actions)
         self._k ^= 1
         b = self._bufs[self._k]
-        check(self._lib.d2d_step(self._h, self._ptr(a), self._ptr(b["obs"]), self._ptr(b["rew"]),
+        self._check(self._lib.d2d_step(self._h, self._ptr(a), self._ptr(b["obs"]), self._ptr(b["rew"]),
                                  self._ptr(b["term"]), self._ptr(b["trunc"]),
                                  self._ptr(b["info"]) if self.with_info else None,
                                  self._ptr(b["tobs"]), self._stream()), "d2d_step")
@@ -303,19 +309,19 @@ class Drone2dVecEnv:
     def get_state(self):
         st = torch.empty(abi.NSTATE, self.num_envs, dtype=torch.float64, device=self.device)
         ist = torch.empty(abi.NISTATE, self.num_envs, dtype=torch.int32, device=self.device)
-        check(self._lib.d2d_get_state(self._h, self._ptr(st), self._ptr(ist), self._stream()), "d2d_get_state")
+        self._check(self._lib.d2d_get_state(self._h, self._ptr(st), self._ptr(ist), self._stream()), "d2d_get_state")
         return st, ist
 
     def set_state(self, state: torch.Tensor | None, istate: torch.Tensor | None = None):
         st = None if state is None else state.to(self.device, torch.float64).contiguous()
         ist = None if istate is None else istate.to(self.device, torch.int32).contiguous()
-        check(self._lib.d2d_set_state(self._h, self._ptr(st), self._ptr(ist), self._stream()), "d2d_set_state")
+        self._check(self._lib.d2d_set_state(self._h, self._ptr(st), self._ptr(ist), self._stream()), "d2d_set_state")
         self._keep = (st, ist)
 
     def get_env_scenarios(self) -> torch.Tensor:
         """int32 [N]: each env's current scenario index (in curriculum pool mode every reset redraws it)."""
         es = torch.empty(self.num_envs, dtype=torch.int32, device=self.device)
-        check(self._lib.d2d_get_env_scenarios(self._h, self._ptr(es), self._stream()), "d2d_get_env_scenarios")
+        self._check(self._lib.d2d_get_env_scenarios(self._h, self._ptr(es), self._stream()), "d2d_get_env_scenarios")
         return es
 
     def set_env_scenarios(self, env_scn: torch.Tensor):
@@ -323,7 +329,7 @@ class Drone2dVecEnv:
         es = torch.as_tensor(env_scn).to(self.device, torch.int32).contiguous()
         if es.shape != (self.num_envs,):
             raise ValueError("env_scn must have shape [num_envs]")
-        check(self._lib.d2d_set_env_scenarios(self._h, self._ptr(es), self._stream()), "d2d_set_env_scenarios")
+        self._check(self._lib.d2d_set_env_scenarios(self._h, self._ptr(es), self._stream()), "d2d_set_env_scenarios")
 
     def group_layout(self):
         """The slot layout in use (include/drone2d.h d2d_get_group_layout): (slot_env [ns] int32,
@@ -333,7 +339,7 @@ class Drone2dVecEnv:
         gs = np.zeros(ng, np.int32)
         k = self._lib.d2d_get_group_layout(self._h, se.ctypes.data_as(C.c_void_p), gs.ctypes.data_as(C.c_void_p))
         if k < 0:
-            check(k, "d2d_get_group_layout")
+            self._check(k, "d2d_get_group_layout")
         return (se, gs) if k > 0 else None
 
     @property
@@ -348,7 +354,7 @@ class Drone2dVecEnv:
         total = 2 * self.num_envs if self.fresh else 2 * len(self.scenarios)
         count = total - first if count is None else count
         out = (abi.D2DScn * count)()
-        check(self._lib.d2d_get_scenario_table(self._h, first, count, out), "d2d_get_scenario_table")
+        self._check(self._lib.d2d_get_scenario_table(self._h, first, count, out), "d2d_get_scenario_table")
         return out
 
     def fresh_recipes(self):
@@ -357,7 +363,7 @@ class Drone2dVecEnv:
         k = np.zeros(2 * self.num_envs, np.int32)
         c = np.zeros(2 * self.num_envs, np.int64)
         t = C.c_int64()
-        check(self._lib.d2d_fresh_recipes(self._h, k.ctypes.data_as(C.c_void_p), c.ctypes.data_as(C.c_void_p),
+        self._check(self._lib.d2d_fresh_recipes(self._h, k.ctypes.data_as(C.c_void_p), c.ctypes.data_as(C.c_void_p),
                                           C.byref(t), 0), "d2d_fresh_recipes")
         return k, c, int(t.value)
 
@@ -370,7 +376,7 @@ class Drone2dVecEnv:
         sd = {"state": st, "istate": ist, "env_scn": self.get_env_scenarios(), "seed": self.seed_value}
         if self.cfg.scn_pool == 1:
             base, valid = C.c_int32(), C.c_int32()
-            check(self._lib.d2d_pool_state(self._h, C.byref(base), C.byref(valid)), "d2d_pool_state")
+            self._check(self._lib.d2d_pool_state(self._h, C.byref(base), C.byref(valid)), "d2d_pool_state")
             recs = self.scenario_table()
             sd["pool"] = {"records": np.frombuffer(bytes(recs), np.uint8).copy(), "active_base": int(base.value),
                           "valid_mask": int(valid.value), "size": len(self.scenarios)}
@@ -391,7 +397,7 @@ class Drone2dVecEnv:
             if int(pool["size"]) != len(self.scenarios):
                 raise ValueError("checkpoint pool size differs from this batch's curriculum_pool")
             recs = (abi.D2DScn * (2 * int(pool["size"]))).from_buffer_copy(np.asarray(pool["records"]).tobytes())
-            check(self._lib.d2d_restore_pool(self._h, recs, len(recs), int(pool["active_base"]),
+            self._check(self._lib.d2d_restore_pool(self._h, recs, len(recs), int(pool["active_base"]),
                                              int(pool["valid_mask"])), "d2d_restore_pool")
             self.set_env_scenarios(sd["env_scn"])
         elif self.cfg.scn_pool == 2:
@@ -401,7 +407,7 @@ class Drone2dVecEnv:
             if k.shape != (2 * self.num_envs,):
                 raise ValueError("checkpoint has a different number of envs")
             t = C.c_int64(int(f["clock"]))
-            check(self._lib.d2d_fresh_recipes(self._h, k.ctypes.data_as(C.c_void_p), c.ctypes.data_as(C.c_void_p),
+            self._check(self._lib.d2d_fresh_recipes(self._h, k.ctypes.data_as(C.c_void_p), c.ctypes.data_as(C.c_void_p),
                                               C.byref(t), 1), "d2d_fresh_recipes")
         elif not torch.equal(torch.as_tensor(sd["env_scn"]).cpu(), self.get_env_scenarios().cpu()):
             raise ValueError("checkpoint env -> scenario map differs from this batch's (static map)")
@@ -409,7 +415,7 @@ class Drone2dVecEnv:
 
     def episode_stats(self, clear: bool = True) -> torch.Tensor:
         """float64 [8]: (sum return, episodes, successes, fails, collisions, sum APE, sum len, 0)."""
-        check(self._lib.d2d_episode_stats(self._h, self._ptr(self._stats), 1 if clear else 0, self._stream()),
+        self._check(self._lib.d2d_episode_stats(self._h, self._ptr(self._stats), 1 if clear else 0, self._stream()),
               "d2d_episode_stats")
         return self._stats
 
