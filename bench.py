@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Benchmark: env-steps/s of the batched Drone2dEnv step at 65 536 envs per MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W]     (N > 1: starts its N ranks itself)
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
@@ -66,12 +66,49 @@ def parse():
     return p.parse_args()
 
 
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args) -> int:
+    """``--gpus N`` (N > 1) without a launcher: start the N ranks ourselves, one process per GPU,
+    as children under ``torch.distributed.run`` (rendezvous on 127.0.0.1) -- the reference's
+    process fan-out (main.py:183-190, SubprocVecEnv) -- and return the launcher's exit status.
+    Nothing here touches the GPU (``device_count`` does not initialise HIP on this image), so the
+    children start from a clean process; the parent never execs."""
+    import subprocess
+
+    backend = os.environ.get("D2D_BENCH_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    if backend == "nccl" and args.gpus > ndev:
+        print(f"bench.py: --gpus {args.gpus} but only {ndev} HIP device(s) are visible "
+              f"(RCCL needs one device per rank; D2D_BENCH_BACKEND=gloo rehearses on fewer)", file=sys.stderr)
+        return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__),
+           *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this pool (RCCL)
+    return subprocess.call(cmd, env=env)
+
+
 def setup_dist(args):
     from drone2d_amd import shard
 
     # RCCL ("nccl") between GPUs; D2D_BENCH_BACKEND=gloo rehearses the multi-rank path with every
     # rank on the one GPU of a single-GPU box (RCCL refuses two ranks on one device)
     backend = os.environ.get("D2D_BENCH_BACKEND", "nccl")
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env != args.gpus:
+        # refuse rather than report a world the run did not have (n_gpus is the world that stepped)
+        print(f"bench.py: launched with WORLD_SIZE={world_env} but --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
     rank, world, local = shard.init_process_group_from_env(backend)
     if world == 1 or backend != "nccl":
         torch.cuda.set_device(local % torch.cuda.device_count())
@@ -182,6 +219,11 @@ def cpu_baseline(args, kwargs):
 
 def main():
     args = parse()
+    if args.gpus < 1:
+        print("bench.py: --gpus must be >= 1", file=sys.stderr)
+        sys.exit(2)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     import drone2d_amd  # noqa: F401  (registers the package as drone2d_amd)
     from drone2d_amd import shard
     from drone2d_amd.config import ENV_TRAIN_CONFIG
@@ -263,12 +305,13 @@ def main():
     kern_ms = float(np.sum([s.elapsed_time(e) for s, e in zip(starts, ends)])) / n_timed
 
     wall_t = torch.tensor([wall], dtype=torch.float64, device=dev)
-    kern_ranks = [kern_ms]
+    kern_ranks, dev_ranks = [kern_ms], [dev.index]
     if world > 1:
         dist.all_reduce(wall_t, op=dist.ReduceOp.MAX)
-        kern_ranks = [None] * world
-        dist.all_gather_object(kern_ranks, kern_ms)
-        kern_ranks = [float(k) for k in kern_ranks]
+        parts = [None] * world
+        dist.all_gather_object(parts, (kern_ms, dev.index))
+        kern_ranks = [float(k) for k, _ in parts]
+        dev_ranks = [int(d) for _, d in parts]
     wall = float(wall_t.item())
     kern_ms = max(kern_ranks)
 
@@ -313,6 +356,8 @@ def main():
             # device time per step (the line's kernel_ms is their max)
             "ranks": world, "backend": (dist.get_backend() if world > 1 else None),
             "kernel_ms_per_rank": kern_ranks,
+            # HIP device of each rank (RCCL: one per rank; the gloo rehearsal shares one GPU)
+            "device_per_rank": dev_ranks,
         }
         vf = os.path.join(REPO, "profiles", f"valu_{tag}.json")
         if os.path.exists(vf):

@@ -1,6 +1,7 @@
 """Build the HIP extension in-tree (hipcc, gfx950) -- used by ``__graft_entry__.build()``."""
 from __future__ import annotations
 
+import glob
 import os
 import shutil
 import subprocess
@@ -8,8 +9,15 @@ import subprocess
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(PKG_DIR)
 SRC = os.path.join(PKG_DIR, "csrc", "d2d_hip.hip")
-HDRS = [os.path.join(PKG_DIR, "csrc", "d2d_device.h"), os.path.join(PKG_DIR, "csrc", "d2d_kernels.h"),
-        os.path.join(REPO, "include", "drone2d.h")]
+
+
+def env_headers() -> list:
+    """Every header the env library's source can include: all of csrc/*.h (globbed, so a new header
+    cannot be forgotten) and the public ABI header."""
+    return sorted(glob.glob(os.path.join(PKG_DIR, "csrc", "*.h"))) + [os.path.join(REPO, "include", "drone2d.h")]
+
+
+HDRS = env_headers()
 OUT = os.path.join(PKG_DIR, "_lib", "libdrone2d_hip.so")
 # the same source with record-major scenario records (D2D_REC_RM=1, d2d_device.h): the build the fresh
 # curriculum loads, whose per-env scenarios are read from global memory (1.7 x faster there, slower on
@@ -37,7 +45,7 @@ def needs_build(out: str = OUT, src: str = SRC, hdrs=None) -> bool:
     if not os.path.exists(out):
         return True
     t = os.path.getmtime(out)
-    return any(os.path.getmtime(p) > t for p in [src, *(HDRS if hdrs is None else hdrs)])
+    return any(os.path.getmtime(p) > t for p in [src, *(env_headers() if hdrs is None else hdrs)])
 
 
 # the PPO update is float32 training arithmetic with no reference rounding to follow: FMAs contracted

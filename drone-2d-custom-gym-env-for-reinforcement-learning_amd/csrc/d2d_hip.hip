@@ -712,11 +712,15 @@ int32_t d2d_reset(d2d_t* h, const uint8_t* mask_dev, uint64_t seed, float* obs_d
     if (!h) return fail(D2D_E_ARG, "d2d_reset: null handle");
     if (h->n_scn <= 0) return fail(D2D_E_STATE, "d2d_reset: call d2d_set_scenarios first");
     DeviceGuard g(h->device);
-    h->seed = seed;
     hipError_t e;
+    if (fresh_mode(h) && mask_dev && (!h->fresh_seeded || h->fresh_seed != seed))
+        return fail(D2D_E_ARG, "d2d_reset: fresh curriculum -- a masked reset must keep the seed of the "
+                               "previous full reset");
+    h->seed = seed;
     if (fresh_mode(h)) {
         // scenarios are keyed by the seed: a new seed drops every slot; then the slots of the
-        // episodes this reset starts
+        // episodes this reset starts.  (A masked reset cannot change the seed, checked above: the
+        // envs it leaves running would keep old-seed scenarios no recipe (key, clock) regenerates.)
         if (!h->fresh_seeded || h->fresh_seed != seed) {
             if ((e = hipMemsetAsync(h->scn_tag, 0xFF, sizeof(int32_t) * 2 * (size_t)h->n, (hipStream_t)stream)) !=
                 hipSuccess)
@@ -1024,7 +1028,10 @@ int32_t d2d_set_curriculum(d2d_t* h, const d2d_curriculum* c) {
             (e = hipMemset(h->gclk, 0, sizeof(int64_t) * S)) != hipSuccess)
             return hip_fail(e, "d2d_set_curriculum: hipMalloc");
     }
+    // the schedule restarts at c->sim_num0: sim_num = sim_num0 + clock * envs_total counts the steps
+    // taken on THIS curriculum, not those since the handle was created
     if ((e = hipMemset(h->scn_tag, 0xFF, sizeof(int32_t) * S)) != hipSuccess ||
+        (e = hipMemset(h->clock, 0, sizeof(int64_t))) != hipSuccess ||
         (e = hipDeviceSynchronize()) != hipSuccess)
         return hip_fail(e, "d2d_set_curriculum: slots");
     h->cur = *c;

@@ -207,9 +207,14 @@ class Drone2dVecEnv:
     def set_curriculum(self, stage: str | None = None, sim_num: int | None = None, pool: int | None = None,
                        seed: int | None = None) -> torch.Tensor:
         """Regenerate the curriculum pool (explicit ``stage`` or the reference's ``sim_num``
-        schedule), upload it and reset every env; returns the reset observations."""
+        schedule), upload it and reset every env; returns the reset observations.  Fresh
+        curriculum: the schedule restarts at ``sim_num`` (the device step clock is zeroed, so
+        sim_num = sim_num + steps taken from here x envs_total)."""
         if not self.cfg.scn_pool:
             raise ValueError("set_curriculum needs an env created in curriculum mode (mode='curriculum')")
+        if pool is not None and self.fresh:
+            raise ValueError("set_curriculum(pool=...) on a fresh-curriculum env: the library and its scenario "
+                             "slots are fixed at construction; build the env with curriculum_pool=P instead")
         if stage is not None:
             self.kwargs["scenario"] = stage
         elif sim_num is not None:

@@ -86,7 +86,8 @@ def _dist_world():
 
 def run_first_episodes(venv, policy: MlpActor, *, deterministic: bool = False, seed: int = 0,
                        max_steps: int | None = None, n_obstacles: int | None = None,
-                       flight_paths: bool = False, check_every: int = 16, gather: bool = True) -> dict:
+                       flight_paths: bool = False, check_every: int = 16, gather: bool = True,
+                       policy_device=None) -> dict:
     """Step ``venv`` (with info rows) under ``policy`` until every env has finished its first
     episode; per-episode records as the reference's test loop keeps them (main.py:273-281).
 
@@ -109,11 +110,16 @@ def run_first_episodes(venv, policy: MlpActor, *, deterministic: bool = False, s
     i at step t is entry i of one global N(0, 1) draw per step (the same generator on every rank),
     so the episodes are those of one unsharded batch; at the end rank 0 gathers every rank's
     records in global env order (``gather``) and the returned dict covers the whole batch (other
-    ranks get their own shard's).  Use a ``batch_invariant`` policy for bit-identical actions."""
+    ranks get their own shard's).  Use a ``batch_invariant`` policy for bit-identical actions.
+
+    ``policy_device``: where the policy and its noise run (default: the env's device).  The
+    parity tests pass "cpu" for the HIP batch and the CPU oracle alike, so both see the same
+    actions for the same observations (a GPU tanh or N(0, 1) stream is not the CPU one)."""
     dev = venv.device
+    pdev = torch.device(policy_device) if policy_device is not None else dev
     dist, rank, world = _dist_world()
-    gen = torch.Generator(device=dev).manual_seed(seed)
-    policy = policy.to(dev)
+    gen = torch.Generator(device=pdev).manual_seed(seed)
+    policy = policy.to(pdev)
     obs = venv.reset(seed=seed)
     n = venv.num_envs
     offset = int(getattr(venv.cfg, "env_id_base", 0)) if world > 1 else 0
@@ -130,8 +136,8 @@ def run_first_episodes(venv, policy: MlpActor, *, deterministic: bool = False, s
     for t in range(cap):
         noise = None
         if not deterministic:
-            noise = torch.randn((n_total, 2), device=dev, dtype=torch.float32, generator=gen)[offset:offset + n]
-        a = policy.act(obs, deterministic=deterministic, noise=noise)
+            noise = torch.randn((n_total, 2), device=pdev, dtype=torch.float32, generator=gen)[offset:offset + n]
+        a = policy.act(obs.to(pdev), deterministic=deterministic, noise=noise)
         obs, rew, term, trunc, info = venv.step(a)
         done = term | trunc
         new = done & ~finished

@@ -135,7 +135,8 @@ typedef struct d2d_curriculum {
     int32_t corner_lo, corner_hi;  /* spawn_corners: 1 DL, 2 DR, 3 UL, 4 UR                     */
     int32_t pad;
     double sim_num0;            /* schedule: sim_num = sim_num0 + clock * envs_total, clock = the  */
-    double envs_total;          /* number of d2d_step calls so far (all ranks' envs: envs_total)  */
+    double envs_total;          /* number of d2d_step calls since this d2d_set_curriculum (which   */
+                                /* zeroes it), all ranks' envs: envs_total                         */
 } d2d_curriculum;
 
 /* One scenario: a QPMI2D path + circle obstacles + spawn distribution.
@@ -180,7 +181,9 @@ int32_t d2d_set_scenario_costs(d2d_t* h, const double* cost, int32_t n_scn);
 /* Reset the envs whose mask byte is non-zero (mask_dev NULL = all envs) and write their
  * observation rows into obs_dev (float32 [n_envs][27]; NULL = do not write).  Spawn draws come
  * from a counter-based Philox4x32-10 stream keyed by (seed, env id, episode number), so results
- * do not depend on the batch size or the sharding.  The seed is kept for auto-resets.
+ * do not depend on the batch size or the sharding.  The seed is kept for auto-resets.  Fresh
+ * curriculum (cfg.scn_pool = 2): a masked reset must pass the seed of the previous full reset
+ * (D2D_E_ARG otherwise: the envs left running would keep scenarios no recipe regenerates).
  * (replaces Drone2dEnv.reset, :908-912) */
 int32_t d2d_reset(d2d_t* h, const uint8_t* mask_dev, uint64_t seed, float* obs_dev, void* stream);
 

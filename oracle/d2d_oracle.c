@@ -829,6 +829,7 @@ int32_t d2dcpu_set_curriculum(d2dcpu_t* h, const d2d_curriculum* c) {
     h->n_scn = S;
     h->pool_n = 0;
     h->cur = *c;
+    h->clock = 0;  /* the schedule restarts at c->sim_num0 (d2d_set_curriculum) */
     h->fresh_seeded = 0;
     return 0;
 }
@@ -896,6 +897,8 @@ static void o_reset_env(d2dcpu_t* h, int i, float* obs_out) {
 }
 
 int32_t d2dcpu_reset(d2dcpu_t* h, const uint8_t* mask, uint64_t seed, float* obs) {
+    if (h->cfg.scn_pool == 2 && mask && (!h->fresh_seeded || h->fresh_seed != seed))
+        return D2D_E_ARG; /* as d2d_reset: a masked fresh reset keeps the seed */
     h->seed = seed;
     if (h->cfg.scn_pool == 2) {
         if (!h->fresh_seeded || h->fresh_seed != seed)

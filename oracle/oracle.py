@@ -121,7 +121,9 @@ class OracleBatch:
 
     def reset(self, seed: int, mask=None):
         m = None if mask is None else np.ascontiguousarray(np.asarray(mask, dtype=np.uint8))
-        self.lib.d2dcpu_reset(self.h, _p(m), C.c_uint64(seed & (2 ** 64 - 1)), _p(self.obs))
+        rc = self.lib.d2dcpu_reset(self.h, _p(m), C.c_uint64(seed & (2 ** 64 - 1)), _p(self.obs))
+        if rc != 0:
+            raise RuntimeError(f"d2dcpu_reset: error {rc}")
         return self.obs.copy()
 
     def step(self, actions, nthreads: int = 1):

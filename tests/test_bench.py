@@ -56,3 +56,36 @@ def test_bench_two_ranks_match_one_process():
     # float sums: per-env accumulators are identical, the reduction order differs (two blocks)
     assert e2["mean_return"] == pytest.approx(e1["mean_return"], rel=1e-9)
     assert e2["sum_ape"] == pytest.approx(e1["sum_ape"], rel=1e-9)
+
+
+@pytest.mark.gpu
+def test_bench_gpus_flag_launches_its_ranks():
+    """``python bench.py --gpus 2`` with no launcher starts its two ranks itself:
+    the line reports the world that stepped, and the reduced episode statistics are one process's."""
+    env = dict(os.environ, D2D_BENCH_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    two = _run([sys.executable, "bench.py", "--gpus", "2", "--envs", "4096", *ARGS], env)
+    one = _run([sys.executable, "bench.py", "--envs", "8192", *ARGS], env)
+    assert two["n_gpus"] == two["ranks"] == 2 and two["backend"] == "gloo"
+    assert len(two["device_per_rank"]) == 2
+    assert two["config"]["total_envs"] == 8192
+    for k in ("finished", "success", "fails", "collisions", "sum_len"):
+        assert two["episodes"][k] == one["episodes"][k], k
+
+
+def test_bench_refuses_world_mismatch():
+    """Under a launcher whose world differs from --gpus the bench exits non-zero before any GPU work."""
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", *ARGS], cwd=REPO, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 2 and "WORLD_SIZE=1 but --gpus 2" in r.stderr
+
+
+def test_bench_refuses_more_gpus_than_devices():
+    """RCCL needs one device per rank: --gpus 4 on a host with fewer visible devices is refused."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "D2D_BENCH_BACKEND")}
+    env["HIP_VISIBLE_DEVICES"] = env["CUDA_VISIBLE_DEVICES"] = ""
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "4", *ARGS], cwd=REPO, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 2 and "HIP device" in r.stderr

@@ -137,3 +137,53 @@ def test_fresh_checkpoint_restore(d2):
         assert torch.equal(oa, ob) and torch.equal(ra, rb) and torch.equal(ta, tb)
     a.close()
     b.close()
+
+
+def test_set_curriculum_restarts_schedule(d2):
+    """set_curriculum(sim_num=X) on an env that has stepped starts the schedule at X
+    (the step clock is zeroed), so the next episodes are generated in X's stage."""
+    n = 1024
+    venv = d2.Drone2dVecEnv(n, seed=5, **_kw(sim_num=0))
+    venv.reset()
+    for _ in range(50):
+        venv.step(torch.rand(n, 2, device=venv.device) * 2 - 1)
+    assert venv.fresh_recipes()[2] == 50
+    venv.set_curriculum(sim_num=1_200_000)  # stage 3: one on-path obstacle, spawn at the first waypoint
+    keys, clocks, clock = venv.fresh_recipes()
+    assert clock == 0
+    tab = venv.scenario_table(0, 2 * n)
+    for s in np.flatnonzero(keys >= 0):
+        assert clocks[s] == 0
+        assert tab[s].n_circles <= 1 and tab[s].spawn_xmin == tab[s].spawn_xmax
+    for _ in range(7):
+        venv.step(torch.rand(n, 2, device=venv.device) * 2 - 1)
+    assert venv.fresh_recipes()[2] == 7
+    venv.set_curriculum(sim_num=800_000)  # stage 2: the random spawn box, no obstacles
+    keys, _, clock = venv.fresh_recipes()
+    assert clock == 0
+    tab = venv.scenario_table(0, 2 * n)
+    for s in np.flatnonzero(keys >= 0):
+        sc = tab[s]
+        assert sc.n_circles == 0 and (sc.spawn_xmin, sc.spawn_xmax) == (100.0, 1200.0)
+    venv.close()
+
+
+def test_masked_fresh_reset_keeps_seed(d2):
+    """a masked fresh reset with a new seed is refused (the envs it leaves running would
+    keep old-seed scenarios that no checkpoint recipe regenerates); with the same seed it works."""
+    n = 256
+    venv = d2.Drone2dVecEnv(n, seed=5, **_kw(sim_num=0))
+    venv.reset()
+    for _ in range(5):
+        venv.step(torch.rand(n, 2, device=venv.device) * 2 - 1)
+    mask = torch.zeros(n, dtype=torch.bool, device=venv.device)
+    mask[::3] = True
+    with pytest.raises(RuntimeError, match="masked reset"):
+        venv.reset(seed=99, mask=mask)
+    venv.seed_value = 5
+    venv.reset(mask=mask)
+    keys = venv.fresh_recipes()[0]
+    ep = venv.get_state()[1][2].cpu().numpy()
+    for i in range(n):  # every env's current slot stays tagged with its episode (checkpointable)
+        assert keys[2 * i + ((ep[i] - 1) & 1)] == ep[i] - 1, i
+    venv.close()

@@ -250,3 +250,106 @@ def test_batch_invariant_actor(d2):
     for a, b in ((0, 1), (5, 77), (100, 301)):
         assert torch.equal(pol.act(x[a:b], deterministic=True), full[a:b])
     np.testing.assert_allclose(full.numpy(), ref.act(x, deterministic=True).numpy(), atol=1e-5)
+
+
+# ---------------------------------------------------------------- the test loop on the HIP path vs the oracle
+PARITY_ENVS = 512
+
+
+def _records_equal(h, o):
+    """The per-episode records of main.py:273-281: counts and flight times identical, APE and the
+    total reward to rtol 1e-6 (float32 info rows from fp64 accumulators on both sides)."""
+    assert h["unfinished"] == o["unfinished"] == 0
+    assert (h["successes"], h["fails"]) == (o["successes"], o["fails"])
+    np.testing.assert_array_equal(h["collisions"], o["collisions"])
+    np.testing.assert_array_equal(h["time_spent"], o["time_spent"])
+    np.testing.assert_allclose(h["apes"], o["apes"], rtol=1e-6)
+    np.testing.assert_allclose(h["rewards"], o["rewards"], rtol=1e-6, atol=1e-6)
+    if "flight_xy" in h:
+        np.testing.assert_allclose(h["flight_xy"], o["flight_xy"], rtol=0, atol=2e-4)
+
+
+def _oracle_run(scn, n, seed):
+    from drone2d_amd import harness
+    from drone2d_amd.config import ENV_TEST_CONFIG
+
+    be = OracleVecBackend(n, seed=seed, **dict(ENV_TEST_CONFIG, scenario=scn))
+    pol = harness.MlpActor.from_npz(os.path.join(GOLD, "agent_17_90.npz"), batch_invariant=True)
+    m = harness.run_first_episodes(be, pol, seed=seed, flight_paths=True, policy_device="cpu")
+    be.close()
+    return m
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scn", ["corridor", "S_corridor"])
+def test_test_loop_hip_matches_oracle(d2, scn):
+    """the reference's test loop (main.py:258-327) run by ``run_first_episodes``
+    on the HIP batch and on the CPU oracle, same seed / scenario / env ids, the shipped agent 17_90
+    evaluated on the host for both (so both see one action stream): every record identical."""
+    from drone2d_amd import harness
+    from drone2d_amd.config import ENV_TEST_CONFIG
+
+    n, seed = PARITY_ENVS, 11
+    venv = d2.Drone2dVecEnv(n, device=torch.device("cuda", 0), seed=seed, **dict(ENV_TEST_CONFIG, scenario=scn))
+    pol = harness.MlpActor.from_npz(os.path.join(GOLD, "agent_17_90.npz"), batch_invariant=True)
+    h = harness.run_first_episodes(venv, pol, seed=seed, flight_paths=True, policy_device="cpu")
+    venv.close()
+    o = _oracle_run(scn, n, seed)
+    assert o["successes"] > 0 and o["fails"] > 0 or scn == "corridor"
+    _records_equal(h, o)
+    assert harness.summary(h) == pytest.approx(harness.summary(o), rel=1e-6)
+
+
+def _hip_parity_worker(rank, world, port, out_path, scn, n, seed):
+    import pickle
+    import sys
+
+    for p in (HERE, os.path.dirname(HERE), os.path.join(os.path.dirname(HERE), "oracle")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+
+    import drone2d_amd  # noqa: F401
+    from drone2d_amd import harness, shard
+    from drone2d_amd.config import ENV_TEST_CONFIG
+
+    shard.init_process_group_from_env("gloo")
+    be = shard.make_shard_venv(n, rank, world, device=torch.device("cuda", 0), seed=seed,
+                               **dict(ENV_TEST_CONFIG, scenario=scn))
+    pol = harness.MlpActor.from_npz(os.path.join(GOLD, "agent_17_90.npz"), batch_invariant=True)
+    m = harness.run_first_episodes(be, pol, seed=seed, flight_paths=True, policy_device="cpu")
+    if rank == 0:
+        with open(out_path, "wb") as f:
+            pickle.dump(m, f)  # written by this test's own worker, read back by the test
+    dist.barrier()
+    dist.destroy_process_group()
+    be.close()
+
+
+@pytest.mark.gpu
+def test_sharded_test_loop_hip_matches_oracle(d2, tmp_path):
+    """The same loop sharded over two ranks (each a HIP shard on the one GPU, gloo for the gather):
+    rank 0's gathered records equal the unsharded CPU oracle's."""
+    import pickle
+    import socket
+
+    import torch.multiprocessing as mp
+
+    scn, n, seed = "S_corridor", PARITY_ENVS - 1, 12  # odd: uneven shards
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = str(tmp_path / "m.pkl")
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_hip_parity_worker, args=(r, 2, port, out, scn, n, seed)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=600)
+        assert p.exitcode == 0
+    with open(out, "rb") as f:
+        h = pickle.load(f)
+    _records_equal(h, _oracle_run(scn, n, seed))
