@@ -42,6 +42,7 @@ SCENARIO = "corridor"
 BYTES_PER_ENV_STEP = 650   # DESIGN.md "Algorithmic bytes": 272 read + 378 written, info off
 INFO_BYTES = 48            # --info: the f32 [N, 12] info row per env-step
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec)
+FP64_PEAK_TFS = 78.6       # MI355X fp64 vector peak (the co-bound reported alongside)
 ACTION_BANK = 16
 # BASELINE.json configs[4]: env i gets scenario i mod 7 in this order
 MIXED = ["perpendicular", "parallel", "S_parallel", "corridor", "S_corridor", "large", "impossible"]
@@ -321,11 +322,14 @@ def main():
         bytes_env = BYTES_PER_ENV_STEP + (INFO_BYTES if args.info else 0)
         achieved = bytes_env * n / (kern_ms * 1e-3) / 1e9
         st = stats.cpu().numpy()
-        traffic = None
+        traffic = traffic_src = None
         tag = f"{args.scenario}_{n}" + ("_info" if args.info else "")
         tf = os.path.join(REPO, "profiles", f"traffic_{tag}.json")
         if os.path.exists(tf):
-            traffic = json.load(open(tf)).get("bytes_per_launch")
+            tj = json.load(open(tf))
+            traffic = tj.get("bytes_per_launch")
+            # PMC bytes come from a committed rocprofv3 pass, not from this run: say which
+            traffic_src = {"profile": os.path.relpath(tf, REPO), "pmc": tj.get("source"), "commit": tj.get("commit")}
         line = {
             "metric": METRIC,
             "value": value,
@@ -345,7 +349,7 @@ def main():
                        "outputs": "obs f32[N,27], reward f32, terminated/truncated u8, terminal obs"
                                   + (", info f32[N,12]" if args.info else " (info rows off)")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "d2d_step_kernel + d2d_fill_kernel/16 (per step)", "kernel_ms": kern_ms,
                          "bytes_per_env_step": bytes_env},
             "episodes": {"finished": float(st[1]), "mean_return": float(st[0] / max(st[1], 1)),
@@ -365,6 +369,22 @@ def main():
             v = json.load(open(vf))
             line["valu"] = {k: v[k] for k in ("valu_insts_per_simd", "valu_active_cycles_per_simd",
                                               "wave_lifetime_cycles", "valu_busy_frac", "source")}
+            line["valu"]["profile"] = os.path.relpath(vf, REPO)
+            line["valu"]["commit"] = v.get("commit")
+            if v.get("fp64_flops_per_env_step_issued"):
+                # the fp64 co-roofline: fp64 flops per env-step from the committed
+                # rocprofv3 VALU-mix pass x the env-steps this run's kernel did per second
+                fl = float(v["fp64_flops_per_env_step_issued"])
+                tfs = fl * n / (kern_ms * 1e-3) / 1e12
+                line["roofline"]["fp64"] = {
+                    "bound": "fp64 vector", "achieved": tfs, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
+                    "frac": tfs / FP64_PEAK_TFS, "flops_per_env_step": fl,
+                    "flops_per_env_step_counter": v.get("fp64_flops_per_env_step_counter"),
+                    "valu_issue_busy_frac": v["valu_busy_frac"], "mix_frac": v.get("mix_frac"),
+                    "source": v.get("mix_sources"), "commit": v.get("commit"),
+                    "note": "flops = (2 FMA + ADD + MUL) f64 wave-instructions x 64 lanes per env-step "
+                            "(issued lanes); the kernel is bound by VALU issue, of which fp64 arithmetic "
+                            "is the mix_frac share"}
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(args, kwargs)
         print(json.dumps(line), flush=True)

@@ -171,10 +171,8 @@ __device__ __forceinline__ double sqrt_nz(double x) {
     // +-0 and +inf return themselves (the refinement would give NaN for inf), NaN propagates
     return __builtin_amdgcn_class(x, 0x260) ? x : g;
 }
-#ifndef D2D_SQRT_NZ
-#define D2D_SQRT_NZ 1   // distances: range-limited sqrt (squared fp64 distances are 0 or >= 2^-767)
-#endif
-__device__ __forceinline__ double sqrt_dist(double x) { return D2D_SQRT_NZ ? sqrt_nz(x) : sqrt(x); }
+// distances: the range-limited sqrt (squared fp64 distances are 0 or >= 2^-767)
+__device__ __forceinline__ double sqrt_dist(double x) { return sqrt_nz(x); }
 // Correctly rounded a / b for normal operands with a normal quotient (no div_scale / div_fixup
 // range handling: results for zero / inf / NaN / extreme-exponent operands are unspecified).
 // Checked bitwise against '/' by d2d_selftest.
@@ -268,26 +266,12 @@ __device__ __forceinline__ void spawn_draw(const Scn& s, uint64_t seed, uint32_t
 // ------------------------------------------------------------------------------ QPMI2D path
 // get_u_index (predef_path.py:53-63): first n with u <= us[n+1]; for non-decreasing knots this is
 // the number of knots k >= 1 with !(u <= us[k]) (NaN -> n_wps-1, as the Python loop).
-// The knots are counted from the sign bit of (us[k] - u): that difference is negative exactly when
-// u > us[k] (equal values give +0), padded +inf knots give +inf (u finite) or NaN (u = +inf, sign
-// clear), and u = -inf gives +inf -- the Python loop's counts in every case; NaN u maps to
-// n_wps - 1 as the loop does.  No compare masks, so the 15 knot tests issue back to back.
-#ifndef D2D_SENSE_MINAXIS
-#define D2D_SENSE_MINAXIS 1  // circle distances / frame contact with min / max instead of selects
-#endif
-#ifndef D2D_SENSE_SQ
-#define D2D_SENSE_SQ 1   // uniform-radius obstacle sets: top-3 by squared distance, 4 square roots per env
-#endif
-#ifndef D2D_KNOT_CMP
-#define D2D_KNOT_CMP 1   // 1: compares (measured faster in the full kernel), 0: sign bits (faster alone)
-#endif
+// (Counting the sign bits of us[k] - u instead of compares gives the same counts and was measured
+// slower in the full kernel.)
 __device__ __forceinline__ int u_index(const Scn& s, double u) {
     uint32_t c = 0;
 #pragma unroll
-    for (int k = 1; k < D2D_MAX_WPS; ++k) {
-        if (D2D_KNOT_CMP) c += !(u <= SUS(s, k)) ? 1u : 0u;
-        else c += (uint32_t)__double2hiint(SUS(s, k) - u) >> 31;
-    }
+    for (int k = 1; k < D2D_MAX_WPS; ++k) c += !(u <= SUS(s, k)) ? 1u : 0u;
     const int nw1 = s.n_wps - 1;
     return (u != u) ? nw1 : min((int)c, nw1);
 }
@@ -385,29 +369,11 @@ __device__ __forceinline__ bool brent_active(const Brent& B) {
     const double tol2 = 2.0 * tol1;
     return (fabs(B.xf - xm) > (tol2 - 0.5 * (B.b - B.a))) & (B.num < 500);
 }
-#ifndef D2D_PAR_BALLOT
-#define D2D_PAR_BALLOT 1  // brent_step: the parabolic candidate only when some lane of the wave takes it
-#endif
-#ifndef D2D_RECPF
-#define D2D_RECPF 0  // brent_step reads the record of a's interval before the candidate is known
-#endif
-#ifndef D2D_COPYSIGN
-#define D2D_COPYSIGN 1  // the step's sign by copysign (bitfield insert) instead of compare + select
-#endif
-#ifndef D2D_KTRACK
-#define D2D_KTRACK 0  // 1: the state carries the knots us[ia + 1], us[ixf + 1]; 0: us[ia + 1] re-read from the table
-#endif
 __device__ __forceinline__ void brent_step(const Scn& s, const PathK& K, double px, double py, Brent& B) {
     const double a = B.a, b = B.b, xf = B.xf, fx = B.fx, nfc = B.nfc, fulc = B.fulc;
-    // the record of a's interval, read first: once the bracket lies in one knot interval (most of
-    // a continuation) the probe falls in it, and the LDS latency hides behind the candidate
-    // computation instead of following it.  Its upper knot serves the one-compare interval test.
-    double rp[REC_N];
-    if (D2D_RECPF) {
-#pragma unroll
-        for (int f = 0; f < REC_N; ++f) rp[f] = SREC(s, f, B.ia);
-    }
-    const double ka = D2D_KTRACK ? B.ka : (D2D_RECPF ? rp[REC_U1] : SREC(s, REC_U1, B.ia));
+    // the upper knot of a's interval, for the one-compare interval test.  (Carrying it in the state,
+    // or prefetching a's whole record before the candidate is known, measured no faster.)
+    const double ka = SREC(s, REC_U1, B.ia);
     const double xm = 0.5 * (a + b);
     const double tol1 = BR_SQRT_EPS * fabs(xf) + BR_XATOL3;
     const double tol2 = 2.0 * tol1;
@@ -422,7 +388,7 @@ __device__ __forceinline__ void brent_step(const Scn& s, const PathK& K, double 
     // only used when `par` holds: then q > 0 and |p / q| < |e| / 2, a normal quotient.  Skipped
     // when no lane of the wave takes the parabolic step (the golden tails of long searches)
     double rat_p = 0.0;
-    if (!D2D_PAR_BALLOT || __ballot(par) != 0ull) {
+    if (__ballot(par) != 0ull) {
         rat_p = div_normal(p + 0.0, q);
         const double xp = xf + rat_p;
         // tol1 * (np.sign(d) + (d == 0)) for d = xm - xf: a, b and xf are finite (the initial
@@ -442,7 +408,7 @@ __device__ __forceinline__ void brent_step(const Scn& s, const PathK& K, double 
     const double mx = fmax(fabs(rat), tol1);
     // (rat is never -0: e_g = a - xf or b - xf is +0 at worst, the parabolic step is p + 0.0 over
     // |q| or tol1 times a nonzero sign, so copysign gives the same -mx / +mx)
-    const double x = xf + (D2D_COPYSIGN ? copysign(mx, rat) : ((rat < 0.0) ? -mx : mx));
+    const double x = xf + copysign(mx, rat);
     // knot interval of x: one compare once the bracket spans <= 2 intervals (wave-uniform choice)
     const bool fast = (x >= a) & (x <= b) & (B.ib <= B.ia + 1);
     int ix;
@@ -455,18 +421,8 @@ __device__ __forceinline__ void brent_step(const Scn& s, const PathK& K, double 
         asm volatile("" : "+v"(sp));
         ix = u_index(*sp, x);
     }
-    double kx, fu;
-    if (D2D_RECPF) {
-        double xq, yq;
-        if (__ballot(ix != B.ia) != 0ull) {
-#pragma unroll
-            for (int f = 0; f < REC_N; ++f) rp[f] = (ix != B.ia) ? SREC(s, f, ix) : rp[f];
-        }
-        path_eval_rec(rp, K, x, ix, xq, yq, kx);
-        fu = norm2(xq - px, yq - py);
-    } else {
-        fu = path_dist_n(s, K, x, ix, px, py, kx);
-    }
+    double kx;
+    const double fu = path_dist_n(s, K, x, ix, px, py, kx);
     B.num += 1;
     const bool le = fu <= fx;
     const bool c1 = !le & ((fu <= B.fnfc) | (nfc == xf));
@@ -482,11 +438,6 @@ __device__ __forceinline__ void brent_step(const Scn& s, const PathK& K, double 
     B.ia = to_a ? ti : B.ia;
     B.ib = to_a ? B.ib : ti;
     B.ixf = le ? ix : B.ixf;
-    if (D2D_KTRACK) {
-        const double tk = le ? B.kxf : kx;
-        B.ka = to_a ? tk : B.ka;
-        B.kxf = le ? kx : B.kxf;
-    }
     const double nfulc = (le | c1) ? nfc : (c2 ? x : fulc);
     const double nffulc = (le | c1) ? B.fnfc : (c2 ? fu : B.ffulc);
     const double nnfc = le ? xf : (c1 ? x : nfc);
@@ -853,30 +804,24 @@ __device__ __forceinline__ void advance_position(Body& b) {
     b.py = b.py + (b.vy + 0.0) * DT;
     b.a = b.a + (b.w + 0.0) * DT;
 }
-#ifndef D2D_COLL_CULL
-#define D2D_COLL_CULL 1  // skip a circle for the whole wave when it is out of reach of every lane's frame
-#endif
 __device__ __forceinline__ bool frame_hits(const Scn& s, const Body& F, double cs, double sn) {
     bool hit = false;
     for (int k = 0; k < ((D2D_ABLATE & 8) ? 0 : s.n_circles); ++k) {
         const double dx = s.cx[k] - F.px, dy = s.cy[k] - F.py;
-        if (D2D_COLL_CULL) {
-            // every point of the box is within sqrt(50^2 + 5^2) = 50.25 of its center, so a center
-            // offset of at least r + 51.25 on either axis puts the circle beyond r of the box: the
-            // exact test below would say "no contact" for this lane.  Steady state: ~8 % of the
-            // (wave, circle) pairs of corridor, ~5 % of S_corridor's, have a lane in reach.
+        {
+            // skip the circle for the whole wave when it is out of every lane's reach: every point of
+            // the box is within sqrt(50^2 + 5^2) = 50.25 of its center, so a center offset of at
+            // least r + 51.25 on either axis puts the circle beyond r of the box: the exact test
+            // below would say "no contact" for this lane.  Steady state: ~8 % of the (wave, circle)
+            // pairs of corridor, ~5 % of S_corridor's, have a lane in reach.
             const double reach = s.cr[k] + 51.25;
             const bool near = (fabs(dx) < reach) & (fabs(dy) < reach);
             if (__ballot(near) == 0ull) continue;
         }
         const double lx = dx * cs + dy * sn;
         const double ly = -dx * sn + dy * cs;
-#if D2D_SENSE_MINAXIS
         // clamp by max / min: equal to clipd for every input (a NaN lx or ly gives a NaN e: no hit)
         const double ex = lx - fmin(fmax(lx, -FRAME_HX), FRAME_HX), ey = ly - fmin(fmax(ly, -FRAME_HY), FRAME_HY);
-#else
-        const double ex = lx - clipd(lx, -FRAME_HX, FRAME_HX), ey = ly - clipd(ly, -FRAME_HY, FRAME_HY);
-#endif
         const double r = s.cr[k];
         hit |= (ex * ex + ey * ey <= r * r);
     }
@@ -947,12 +892,6 @@ __device__ __forceinline__ Arms make_arms(const double cs[3], const double sn[3]
 
 // stage 2.  pos = {frame px, py, left px, py, right px, py} (post position update); vel[9] =
 // (vx, vy, w) of frame, left, right; j[12] the accumulated pivot impulses.
-#ifndef D2D_ZERO_ARM
-#define D2D_ZERO_ARM 1  // joint sweep: skip the signed-zero terms of the motor-centre pivots
-#endif
-#ifndef D2D_SWEEP_UNROLL
-#define D2D_SWEEP_UNROLL 1  // unroll factor of the 10-sweep loop (2: no loop-carried register moves)
-#endif
 constexpr int JB_PER_JOINT = 5;  // K^-1 (a, b = c, d) + bias (x, y)
 template <bool JBUF>
 __device__ __forceinline__ void phys_velocities(const Arms& A, const double pos[6], double damping_dt, double fx,
@@ -1013,7 +952,7 @@ __device__ __forceinline__ void phys_velocities(const Arms& A, const double pos[
         vel[2] += II_F * (r2x * jy - r2y * jx);
     }
     // 10 sequential-impulse sweeps (Space.iterations default)
-#pragma unroll D2D_SWEEP_UNROLL
+#pragma unroll 1  // (unrolled twice: 28 B of spills, no gain)
     for (int it = 0; it < ((D2D_ABLATE & 4) ? 0 : 10); ++it) {
 #pragma unroll
         for (int k = 0; k < 6; ++k) {
@@ -1039,8 +978,8 @@ __device__ __forceinline__ void phys_velocities(const Arms& A, const double pos[
             // perp(r1) * w terms and its angular impulse are signed zeros.  Adding a signed zero
             // leaves a velocity unchanged unless it is -0, and velocities are never -0 here (the
             // gravity / force update adds +0 or a nonzero term, sums of nonzero terms round to +0,
-            // never -0); they are dropped for finite states (ZERO_ARM)
-            const bool za = D2D_ZERO_ARM && (k % 3 == 1);
+            // never -0); they are dropped for finite states
+            const bool za = (k % 3 == 1);
             const double v1x = za ? vel[3 * m + 0] : vel[3 * m + 0] + (-r1y) * vel[3 * m + 2];
             const double v1y = za ? vel[3 * m + 1] : vel[3 * m + 1] + r1x * vel[3 * m + 2];
             const double v2x = vel[0] + (-r2y) * vel[2], v2y = vel[1] + r2x * vel[2];
@@ -1135,7 +1074,7 @@ __device__ __forceinline__ void sensor_pos(const d2d_cfg& cfg, const Scn& s, dou
     int bi0 = -1, bi1 = -1, bi2 = -1;
     const int nc = (D2D_ABLATE & 2) ? 0 : s.n_circles;
     bool full = true;
-    if (D2D_SENSE_SQ && s.r_uniform == s.r_uniform) {
+    if (s.r_uniform == s.r_uniform) {
         // every circle has radius r: d = sqrt(q) - r is non-decreasing in the squared distance q,
         // so the stable top-3 by d is the stable top-3 by q unless two of the candidates round to
         // the same d (then the reference's index order among them can differ from q's order).
@@ -1181,21 +1120,11 @@ __device__ __forceinline__ void sensor_pos(const d2d_cfg& cfg, const Scn& s, dou
         const double cx = s.cx[i], cy = s.cy[i];
         const double ax = (50.0 + x) - cx, bxx = (-50.0 + x) - cx;
         const double ay = (-5.0 + y) - cy, byy = (5.0 + y) - cy;
-#if D2D_SENSE_MINAXIS
         // min over the vertices (±50, ±5) of RN(dx² + dy²) == RN(min dx² + min dy²): squaring and
         // rounding are monotone, so the x and y parts minimise independently (bit-identical to
         // the four sums; NaN coordinates give NaN either way)
         const double mx = fmin(fabs(ax), fabs(bxx)), my = fmin(fabs(ay), fabs(byy));
         const double q = mx * mx + my * my;
-#else
-        const double ax2 = ax * ax, bx2 = bxx * bxx, ay2 = ay * ay, by2 = byy * byy;
-        // vertex order (50,-5), (50,5), (-50,5), (-50,-5)
-        const double q0 = ax2 + ay2, q1 = ax2 + by2, q2 = bx2 + by2, q3 = bx2 + ay2;
-        double q = q0;
-        q = (q1 < q) ? q1 : q;
-        q = (q2 < q) ? q2 : q;
-        q = (q3 < q) ? q3 : q;
-#endif
         const double d = sqrt_dist(q) - s.cr[i];
         // stable ascending insertion into the top-3 (equal keys keep index order)
         const bool l0 = (bi0 < 0) || d < bd0, l1 = (bi1 < 0) || d < bd1, l2 = (bi2 < 0) || d < bd2;

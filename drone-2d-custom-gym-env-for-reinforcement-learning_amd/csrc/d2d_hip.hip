@@ -17,12 +17,6 @@
 
 using namespace d2dk;
 
-#ifndef D2D_GROUP
-#define D2D_GROUP 1  // 0: no scenario-grouped lane map (diagnostic A/B builds only)
-#endif
-#ifndef D2D_BRTAB
-#define D2D_BRTAB 1  // 0: searches without the golden-march tables (diagnostic A/B builds only)
-#endif
 
 namespace {
 thread_local std::string g_err;
@@ -78,13 +72,8 @@ struct d2d_handle {
     uint64_t fresh_seed = 0;
     bool fresh_seeded = false;
     int32_t generation = 0;      // bumped whenever captured graphs' pointers go stale
-    // quad workgroups (d2d_step_quad_kernel): one per QuadDesc
-    QuadDesc* quad = nullptr;
-    int n_quads = 0;
     int n_cu = 0;                      // compute units of the device
     std::vector<double> scn_cost;      // relative step cost per scenario (d2d_set_scenario_costs)
-    int quad_mode = 0;                 // D2D_QUAD: 0 off (default: measured slower), 1 on,
-                                       // -1 when there is at least one quad per CU
 };
 
 namespace {
@@ -98,12 +87,12 @@ StepArgs make_args(const d2d_t* h) {
     a.ist = h->ist;
     a.acc = h->acc;
     a.scn = h->scn;
-    a.brt = D2D_BRTAB ? h->brt : nullptr;
+    a.brt = h->brt;
     a.env_scn = h->env_scn;
     a.pool_base = h->pool_dev;
     a.pool_n = h->pool_n;
     a.fill_ctl = h->fill_ctl;
-    a.fill_every = D2D_FILL_EVERY;
+    a.fill_every = FILL_EVERY;
     a.fill_force = 0;
     a.cfg = h->cfg;
     a.damping_dt = std::pow(h->cfg.damping, 1.0 / 60.0);
@@ -116,117 +105,7 @@ StepArgs make_args(const d2d_t* h) {
     a.wg_scn = h->wg_scn;
     a.scn_tag = h->scn_tag;
     a.clock = h->clock;
-    a.quad = h->quad;
     return a;
-}
-
-// Quad workgroups for the current layout (identity with one scenario, or the scenario-grouped
-// layout; pool / fresh curriculum keep the 256-thread kernels).  Groups are dealt by step cost:
-// sorted heaviest first, quad j takes the heavy pair 2j, 2j + 1 as quarters 0 and 2 and the light
-// pair from the other end as quarters 1 and 3; wave 4 r + c (SIMD class c) runs role r of quarter
-// (c + r) % 4, so every SIMD runs one wave of each role and, of its path (role 2) and sensing (role
-// 1) waves, one belongs to a heavy quarter and one to a light one.  Each quad stages up to four
-// scenarios (+ probe tables) once; a quarter whose scenarios do not fit reads them from global memory.
-hipError_t make_quads(d2d_t* h) {
-    if (h->quad) (void)hipFree(h->quad);
-    h->quad = nullptr;
-    h->n_quads = 0;
-    const bool grouped = h->lane_env != nullptr;
-    if (h->cfg.scn_pool || !h->brt || (!grouped && h->n_scn != 1)) return hipSuccess;
-    const int ng = (h->ns + EPB - 1) / EPB;
-    const int nq = (ng + 3) / 4;
-    if (h->quad_mode == 0 || (h->quad_mode < 0 && nq < h->n_cu)) return hipSuccess;
-    std::vector<int32_t> ws((size_t)ng, 0);
-    if (grouped) {
-        hipError_t e = hipMemcpy(ws.data(), h->wg_scn, sizeof(int32_t) * (size_t)ng, hipMemcpyDeviceToHost);
-        if (e != hipSuccess) return e;
-    }
-    auto cost = [&](int g) {
-        if (g < 0) return -1.0;
-        const int w = ws[(size_t)g];
-        auto c = [&](int s) { return (s >= 0 && s < (int)h->scn_cost.size()) ? h->scn_cost[(size_t)s] : 1.0; };
-        return w >= 0 ? c(w) : (w <= -2 ? std::max(c(-w - 2), c(-w - 1)) : 2.0);
-    };
-    // quads in XCD chunks (xcd_group: XCD x runs quad numbers [first_x, first_x + cnt_x)); a chunk's
-    // quads take the groups of one contiguous range of group numbers (= of env ids: make_groups
-    // numbers groups by their first env), so the env-ordered output rows one XCD writes stay together
-    // in its L2, and inside the chunk the groups are dealt by cost
-    std::vector<int32_t> order((size_t)(4 * nq), -1);
-    {
-        const int per = nq / 8, rem = nq % 8;
-        int qfirst = 0;
-        for (int x = 0; x < 8; ++x) {
-            const int cnt = per + (x < rem ? 1 : 0);
-            const int g0 = std::min(ng, 4 * qfirst), g1 = std::min(ng, 4 * (qfirst + cnt));
-            std::vector<int32_t> ch;
-            for (int g = g0; g < g1; ++g) ch.push_back(g);
-            while ((int)ch.size() < 4 * cnt) ch.push_back(-1);
-            if (grouped)  // heaviest first (ties: group order); empty quarters last
-                std::stable_sort(ch.begin(), ch.end(), [&](int32_t u, int32_t v) { return cost(u) > cost(v); });
-            for (int k = 0; k < 4 * cnt; ++k) order[(size_t)(4 * qfirst + k)] = ch[(size_t)k];
-            qfirst += cnt;
-        }
-    }
-    std::vector<QuadDesc> Q((size_t)nq);
-    for (int j = 0; j < nq; ++j) {
-        QuadDesc& D = Q[(size_t)j];
-        std::memset(&D, 0, sizeof D);
-        if (grouped) {
-            // chunk c of this quad: its groups are order[4 f, 4 f + 4 m) sorted by cost; quad f + i takes
-            // the heavy pair 2 i, 2 i + 1 and the light pair from the chunk's other end
-            const int per = nq / 8, rem = nq % 8;
-            int f = 0, m = 0;
-            for (int x = 0, first = 0; x < 8; ++x) {
-                const int cnt = per + (x < rem ? 1 : 0);
-                if (j >= first && j < first + cnt) {
-                    f = first;
-                    m = cnt;
-                }
-                first += cnt;
-            }
-            const int i = j - f;
-            const size_t base = (size_t)(4 * f), last = base + (size_t)(4 * m) - 1;
-            D.group[0] = order[base + (size_t)(2 * i)];
-            D.group[2] = order[base + (size_t)(2 * i + 1)];
-            D.group[1] = order[last - (size_t)(2 * i)];
-            D.group[3] = order[last - (size_t)(2 * i + 1)];
-        } else {
-            for (int q = 0; q < 4; ++q) D.group[q] = (4 * j + q < ng) ? 4 * j + q : -1;
-        }
-        for (int k = 0; k < 4; ++k) D.stage[k] = -1;
-        int used = 0;
-        for (int q = 0; q < 4; ++q) {
-            const int g = D.group[q];
-            const int w = (g >= 0 && grouped) ? ws[(size_t)g] : 0;
-            const int lo = w >= 0 ? w : -w - 2, cnt = w >= 0 ? 1 : (w <= -2 ? 2 : 0);
-            D.s0[q] = lo;
-            D.qslot[q] = -1;
-            if (cnt == 0) continue;  // three or more scenarios in the group: global memory
-            int at = -1;
-            for (int k = 0; k + cnt <= used && at < 0; ++k)
-                if (D.stage[k] == lo && (cnt == 1 || D.stage[k + 1] == lo + 1)) at = k;
-            if (at < 0 && used + cnt <= 4) {
-                at = used;
-                for (int k = 0; k < cnt; ++k) D.stage[used++] = lo + k;
-            }
-            D.qslot[q] = at;
-        }
-        uint64_t roles = 0;
-        for (int w = 0; w < 16; ++w) {
-            const int r = w / 4, c = w % 4, q = (c + r) % 4;
-            roles |= (uint64_t)((q << 2) | r) << (4 * w);
-        }
-        D.roles = roles;
-    }
-    hipError_t e = hipMalloc(&h->quad, sizeof(QuadDesc) * (size_t)nq);
-    if (e == hipSuccess) e = hipMemcpy(h->quad, Q.data(), sizeof(QuadDesc) * (size_t)nq, hipMemcpyHostToDevice);
-    if (e != hipSuccess) {
-        if (h->quad) (void)hipFree(h->quad);
-        h->quad = nullptr;
-        return e;
-    }
-    h->n_quads = nq;
-    return hipSuccess;
 }
 
 // K5: the fresh curriculum's scenario slots (restore: every slot from its recipe), on `stream`
@@ -257,10 +136,9 @@ bool fresh_mode(const d2d_t* h) { return h->cfg.scn_pool == 2; }
 hipError_t rc_fill(d2d_t* h, hipStream_t stream, bool force = false) {
     StepArgs a = make_args(h);
     a.fill_force = force ? 1 : 0;
-    const int spb = (D2D_FILL_SPLIT && D2D_FILL_COMPACT) ? FILL_SPB : BLOCK;
-    const dim3 grid((h->ns + spb - 1) / spb);
-    // (D2D_FILL_RESIDENT: dynamic LDS padded to K1's per-workgroup LDS, so K4 is resident 4 per CU as K1)
-    const size_t pad = D2D_FILL_RESIDENT ? sizeof(d2d::Scn) + sizeof(d2d::BtHot) + sizeof(K1Shared) - 2048 : 0;
+    const dim3 grid((h->ns + FILL_SPB - 1) / FILL_SPB);
+    // dynamic LDS padded to K1's per-workgroup LDS, so K4 is resident 4 per CU as K1 (d2d_fill_kernel)
+    const size_t pad = sizeof(d2d::Scn) + sizeof(d2d::BtHot) + sizeof(K1Shared) - 2048;
     if (sizeof(d2d::Scn) * (size_t)h->n_scn <= K2_LDS_BUDGET)
         hipLaunchKernelGGL(d2d_fill_kernel<true>, grid, dim3(BLOCK), std::max(sizeof(d2d::Scn) * h->n_scn, pad), stream, a);
     else
@@ -269,8 +147,8 @@ hipError_t rc_fill(d2d_t* h, hipStream_t stream, bool force = false) {
 }
 // drop every entry (new seed, counters or scenarios) and refill, ordered on `stream`
 hipError_t rc_rebuild(d2d_t* h, hipStream_t stream) {
-    hipError_t e = hipMemsetAsync(h->rc_tag, 0xFF, sizeof(int32_t) * D2D_RC_SLOTS * (size_t)h->ns, stream);
-    if (e == hipSuccess && D2D_FILL_PERIOD > 0) e = rc_fill(h, stream, true);
+    hipError_t e = hipMemsetAsync(h->rc_tag, 0xFF, sizeof(int32_t) * RC_SLOTS * (size_t)h->ns, stream);
+    if (e == hipSuccess) e = rc_fill(h, stream, true);
     if (e == hipSuccess) h->rc_dirty = false;
     return e;
 }
@@ -285,9 +163,7 @@ hipError_t rc_rebuild(d2d_t* h, hipStream_t stream) {
 // of three or more (everything through L1/L2).  Groups are then
 // ordered by their first env id, so groups whose envs interleave (e.g. scenario = id mod 7) get
 // consecutive numbers (xcd_group places consecutive numbers on one XCD).
-#ifndef D2D_STRADDLE_W
-#define D2D_STRADDLE_W 1.25  // balance_groups: a straddling group's cost over its heavier scenario's
-#endif
+constexpr double STRADDLE_W = 1.25;  // balance_groups: a straddling group's cost over its heavier scenario's
 // host copy of the kernels' block -> group numbering (d2d_kernels.h xcd_group)
 int xcd_group_host(int b, int nb) {
     const int per = nb / 8, rem = nb % 8, x = b % 8, k = b / 8;
@@ -309,7 +185,7 @@ void balance_groups(int n_cu, const double* cost, int n_cost, std::vector<int32_
     auto c = [&](int sc) { return (sc >= 0 && sc < n_cost) ? cost[sc] : cmax; };
     auto gcost = [&](int g) {
         const int w = ws[(size_t)g];
-        return w >= 0 ? c(w) : (w <= -2 ? D2D_STRADDLE_W * std::max(c(-w - 2), c(-w - 1)) : 1.5 * cmax);
+        return w >= 0 ? c(w) : (w <= -2 ? STRADDLE_W * std::max(c(-w - 2), c(-w - 1)) : 1.5 * cmax);
     };
     std::vector<int32_t> block_of((size_t)ng);  // group number -> the block that runs it
     for (int b = 0; b < ng; ++b) block_of[(size_t)xcd_group_host(b, ng)] = b;
@@ -408,13 +284,13 @@ hipError_t alloc_layout(Layout& L, int n, const std::vector<int32_t>& lanes, con
     if ((e = hipMalloc(&L.st, sizeof(double) * D2D_NSTATE * ns)) != hipSuccess ||
         (e = hipMalloc(&L.ist, sizeof(int32_t) * D2D_NISTATE * ns)) != hipSuccess ||
         (e = hipMalloc(&L.acc, sizeof(double) * D2D_NSTATS * ns)) != hipSuccess ||
-        (e = hipMalloc(&L.rc_obs, sizeof(float) * D2D_OBS_DIM * D2D_RC_SLOTS * ns)) != hipSuccess ||
-        (e = hipMalloc(&L.rc_rfl, sizeof(int32_t) * D2D_RC_SLOTS * ns)) != hipSuccess ||
-        (e = hipMalloc(&L.rc_tag, sizeof(int32_t) * D2D_RC_SLOTS * ns)) != hipSuccess ||
+        (e = hipMalloc(&L.rc_obs, sizeof(float) * D2D_OBS_DIM * RC_SLOTS * ns)) != hipSuccess ||
+        (e = hipMalloc(&L.rc_rfl, sizeof(int32_t) * RC_SLOTS * ns)) != hipSuccess ||
+        (e = hipMalloc(&L.rc_tag, sizeof(int32_t) * RC_SLOTS * ns)) != hipSuccess ||
         (e = hipMemset(L.st, 0, sizeof(double) * D2D_NSTATE * ns)) != hipSuccess ||
         (e = hipMemset(L.ist, 0, sizeof(int32_t) * D2D_NISTATE * ns)) != hipSuccess ||
         (e = hipMemset(L.acc, 0, sizeof(double) * D2D_NSTATS * ns)) != hipSuccess ||
-        (e = hipMemset(L.rc_tag, 0xFF, sizeof(int32_t) * D2D_RC_SLOTS * ns)) != hipSuccess) {
+        (e = hipMemset(L.rc_tag, 0xFF, sizeof(int32_t) * RC_SLOTS * ns)) != hipSuccess) {
         free_layout(L);
         return e;
     }
@@ -510,7 +386,6 @@ int32_t d2d_create(const d2d_cfg* cfg, int32_t n_envs, int32_t device, d2d_t** o
     h->n = n_envs;
     h->device = device;
     if (hipDeviceGetAttribute(&h->n_cu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) h->n_cu = 256;
-    if (const char* qm = std::getenv("D2D_QUAD")) h->quad_mode = std::atoi(qm);  // A/B switch (diagnostics)
     const size_t n = (size_t)n_envs;
     Layout L;
     if ((e = hipMalloc(&h->env_scn, sizeof(int32_t) * n)) != hipSuccess ||
@@ -545,7 +420,6 @@ void d2d_destroy(d2d_t* h) {
     if (h->pool_dev) (void)hipFree(h->pool_dev);
     if (h->fill_ctl) (void)hipFree(h->fill_ctl);
     if (h->clock) (void)hipFree(h->clock);
-    if (h->quad) (void)hipFree(h->quad);
     if (h->abi) (void)hipFree(h->abi);
     if (h->scn_tag) (void)hipFree(h->scn_tag);
     if (h->gclk) (void)hipFree(h->gclk);
@@ -617,7 +491,7 @@ int32_t d2d_set_scenarios(d2d_t* h, const d2d_scn* scns, int32_t n_scn, const in
     // slot layout: grouped for a static mixed map (pool mode redraws scenarios at every reset);
     // the current state moves into the new layout
     std::vector<int32_t> lanes, ws;
-    if (D2D_GROUP && env_scn_host && n_scn > 1 && !h->cfg.scn_pool) {
+    if (env_scn_host && n_scn > 1 && !h->cfg.scn_pool) {
         make_groups(h->n, env_scn_host, n_scn, lanes, ws);
         if ((int)h->scn_cost.size() == n_scn) balance_groups(h->n_cu, h->scn_cost.data(), n_scn, lanes, ws);
     }
@@ -657,7 +531,6 @@ int32_t d2d_set_scenarios(d2d_t* h, const d2d_scn* scns, int32_t n_scn, const in
         h->reset_done = false;
         return hip_fail(e, "d2d_set_scenarios: env_scn upload");
     }
-    if ((e = make_quads(h)) != hipSuccess) return hip_fail(e, "d2d_set_scenarios: quad workgroups");
     return D2D_OK;
 }
 
@@ -670,7 +543,7 @@ int32_t d2d_set_scenario_costs(d2d_t* h, const double* cost, int32_t n_scn) {
     hipError_t e;
     if ((e = hipDeviceSynchronize()) != hipSuccess) return hip_fail(e, "d2d_set_scenario_costs: sync");
     h->scn_cost.assign(cost, cost + n_scn);
-    if (h->lane_env && !h->quad_mode) {
+    if (h->lane_env) {
         // grouped layout: deal the groups over the CUs by the new costs (balance_groups); the state
         // moves into the renumbered layout, the reset cache refills
         std::vector<int32_t> es((size_t)h->n);
@@ -691,7 +564,6 @@ int32_t d2d_set_scenario_costs(d2d_t* h, const double* cost, int32_t n_scn) {
         h->generation += 1;  // captured graphs hold the old layout's buffers
         h->rc_dirty = true;
     }
-    if ((e = make_quads(h)) != hipSuccess) return hip_fail(e, "d2d_set_scenario_costs: quad workgroups");
     return D2D_OK;
 }
 
@@ -769,14 +641,7 @@ int32_t d2d_step(d2d_t* h, const float* act_dev, float* obs_dev, float* rew_dev,
     const dim3 grid((h->n + EPB - 1) / EPB);
     const size_t lds_scn = sizeof(d2d::Scn) * (size_t)h->n_scn, lds_hot = sizeof(d2d::BtHot) * (size_t)h->n_scn;
     static_assert(sizeof(d2d::Scn) + sizeof(d2d::BtHot) + sizeof(K1Shared) <= K1_LDS_BUDGET, "grouped K1 LDS");
-    static_assert(4 * (sizeof(d2d::Scn) + sizeof(d2d::BtHot) + sizeof(K1Shared)) <= 160 * 1024, "quad K1 LDS");
-    if (h->quad) {
-        const size_t dyn = 4 * (sizeof(d2d::Scn) + sizeof(d2d::BtHot));
-        if (h->lane_env)
-            hipLaunchKernelGGL(d2d_step_quad_kernel<true>, dim3(h->n_quads), dim3(QUAD_THREADS), dyn, (hipStream_t)stream, a);
-        else
-            hipLaunchKernelGGL(d2d_step_quad_kernel<false>, dim3(h->n_quads), dim3(QUAD_THREADS), dyn, (hipStream_t)stream, a);
-    } else {
+    {
         // the three-way table re-check pays when the SIMDs have idle issue slots (at most one K1
         // workgroup per CU: 4 096 / 16 384 envs -4 %), not at full load (65 536 envs +3.6 %)
         const int nwg = h->lane_env ? h->n_groups : (int)grid.x;
@@ -803,7 +668,7 @@ int32_t d2d_step(d2d_t* h, const float* act_dev, float* obs_dev, float* rew_dev,
     if (e != hipSuccess) return hip_fail(e, "d2d_step launch");
     if (fresh_mode(h) && (e = fresh_regen(h, (hipStream_t)stream)) != hipSuccess)
         return hip_fail(e, "d2d_step: fresh scenarios");
-    if (D2D_FILL_PERIOD > 0 && h->cfg.auto_reset && ++h->n_steps % D2D_FILL_PERIOD == 0 &&
+    if (h->cfg.auto_reset && ++h->n_steps % FILL_PERIOD == 0 &&
         (e = rc_fill(h, (hipStream_t)stream)) != hipSuccess)
         return hip_fail(e, "d2d_step: cache fill");
     return D2D_OK;

@@ -13,7 +13,7 @@
 //   W2  path role: Brent closest point through the golden-march tables (steps [1, bt_split) of the
 //       table re-check), obs 19..26, the position / path terms of the reward while the physics wave
 //       finishes, then the sum
-//   W3  steps [bt_split, len) of W2's table re-check (D2D_SPLIT); then, for envs that end, the
+//   W3  steps [bt_split, len) of W2's table re-check; then, for envs that end, the
 //       spawn state and the spawn-state path part
 //   (W1 and W3 take the spawn-state parts from the auto-reset observation cache when it is ready)
 //   epilogue (after the one barrier): the 64x27 f32 obs tile is stored as one contiguous span;
@@ -48,47 +48,11 @@ constexpr size_t K2_LDS_BUDGET = 64 * 1024;
 // A/B (tools/variants.py, µs per step at 65 536 envs, corridor / S_corridor / large / mixed):
 // W0..W3 = 2,0,3,2 29.46 / 37.97 / 35.73 / 40.11; 2,1,3,1 28.86 / 37.99 / 35.78 / 40.00; with W2 -> 0
 // after the search 28.55 / 37.61 / 35.78 / 40.11 (kept); all equal (0) 39.9, W0 = W2 = 3 35.2.
-#ifndef D2D_PRIO_W0
-#define D2D_PRIO_W0 2
-#endif
-#ifndef D2D_PRIO_W1
-#define D2D_PRIO_W1 1
-#endif
-#ifndef D2D_PRIO_W2
-#define D2D_PRIO_W2 3
-#endif
-#ifndef D2D_PRIO_W3
-#define D2D_PRIO_W3 1
-#endif
-#ifndef D2D_PRIO_W1_POST
-#define D2D_PRIO_W1_POST D2D_PRIO_W1  // W1 once its sensing part is done
-#endif
-#ifndef D2D_PRIO_W3_TAB
-#define D2D_PRIO_W3_TAB D2D_PRIO_W2   // W3 while it re-checks its part of W2's table
-#endif
-#ifndef D2D_PRIO_W2_POST
-#define D2D_PRIO_W2_POST 0  // W2 once its search is done (the reward terms and waits)
-#endif
-#define D2D_SETPRIO(p)                                \
-    do {                                              \
-        if ((p) != 0) __builtin_amdgcn_s_setprio(p);  \
-    } while (0)
-
-// Quad workgroup (d2d_step_quad_kernel): four 64-env groups in one 1 024-thread workgroup.  Waves w
-// and w + 4 k share a SIMD (wave w lands on SIMD cycle[(start + w) % 4] whatever the start), so the
-// host decides which (quarter, role) each SIMD runs -- one wave of every role per SIMD, heavy and
-// light scenarios' path and sensing waves paired (d2d_hip.hip, make_quads) -- instead of relying on
-// how the dispatcher rotates the wave placement of co-resident 256-thread workgroups.
-struct QuadDesc {
-    int32_t group[4];   // quarter q's 64-env group (slots [64 g, 64 g + 64)); -1: empty quarter
-    int32_t stage[4];   // scenario staged in LDS slot j (scenario + probe table); -1: unused
-    int32_t qslot[4];   // LDS slot of quarter q's scenario s0 (a straddling pair: s0 + 1 in qslot + 1);
-                        // -1: the quarter reads its scenarios from global memory
-    int32_t s0[4];      // quarter q's (first) scenario
-    uint64_t roles;     // wave w -> bits [4w, 4w + 4): quarter << 2 | role
-    uint64_t pad;
-};
-static_assert(sizeof(QuadDesc) == 80, "QuadDesc size");
+// W3 re-checks its part of W2's golden-march table at W2's priority, then drops to PRIO_W3; W2 drops
+// to PRIO_W2_POST once its search is done (the reward terms and waits).
+constexpr int PRIO_W0 = 2, PRIO_W1 = 1, PRIO_W2 = 3, PRIO_W3 = 1, PRIO_W2_POST = 0;
+// (A four-group 1 024-thread "quad" workgroup with host-chosen role -> SIMD placement was measured
+// 2-13 % slower than four 256-thread workgroups and removed in round 4: DESIGN.md.)
 
 struct StepArgs {
     int n;                   // envs
@@ -120,9 +84,9 @@ struct StepArgs {
     const uint8_t* mask;     // reset kernel only
     uint64_t* stamps;        // diagnostic builds only (D2D_STAMPS): [waves][8] s_memtime stamps
     // auto-reset observation cache (handle-internal; see "Auto-reset observation cache" below)
-    float* rc_obs;           // [D2D_RC_SLOTS][n][27] reset observations (rc_entry: the slot of a key)
-    int32_t* rc_rfl;         // [D2D_RC_SLOTS][n] their flags (LA lock)
-    int32_t* rc_tag;         // [D2D_RC_SLOTS][n] episode counter an entry belongs to (-1: none)
+    float* rc_obs;           // [RC_SLOTS][n][27] reset observations (rc_entry: the slot of a key)
+    int32_t* rc_rfl;         // [RC_SLOTS][n] their flags (LA lock)
+    int32_t* rc_tag;         // [RC_SLOTS][n] episode counter an entry belongs to (-1: none)
     // Scenario-grouped slot layout (null unless the env -> scenario map is static and mixed).
     // Internal state lives in slots: slot s holds env lane_env[s] (-1: padding), and slots
     // [64 g, 64 g + 64) all hold envs of scenario wg_scn[g], so K1 workgroup g (after the XCD-aware
@@ -135,12 +99,11 @@ struct StepArgs {
     // reset observation only once its scenario exists) and the step clock K1 advances
     const int32_t* scn_tag;   // [2 n]
     int64_t* clock;           // [1]
-    const QuadDesc* quad;     // quad workgroups (d2d_step_quad_kernel), or null
 };
 
 // Auto-reset observation cache.  The observation an env gets when it auto-resets depends only on
 // (seed, env id, episode counter, scenario), so it is computed ahead of time, while the env is still
-// running, by the fill kernel K4 that d2d_step launches after every D2D_FILL_PERIOD-th step (and
+// running, by the fill kernel K4 that d2d_step launches after every FILL_PERIOD-th step (and
 // d2d_reset / d2d_set_state after theirs): one lane per env, every env whose entry is not tagged
 // with its current episode counter computes the spawn-state observation of its next episode.  K1
 // takes an entry only when its tag matches; otherwise (an episode shorter than the fill period) it
@@ -150,51 +113,19 @@ struct StepArgs {
 #define D2D_ABL 0        // diagnostic builds only: bit r skips role r's compute, bit 4 = perfect
                          // reset cache (no fills, every entry taken as ready): timing ablations
 #endif
-#ifndef D2D_PREFETCH
-#define D2D_PREFETCH 2   // K1 issues its state loads before the staging barrier (bit 0: W0 all, bit 2: W0 without
-                         // the joint impulses, bit 1: the frame for W1/W2)
-#endif
-#ifndef D2D_GLDS
-#define D2D_GLDS 1       // K1 stages its scenario (+ probe table) with LDS-DMA
-#endif
-#ifndef D2D_STRADDLE_LDS
-#define D2D_STRADDLE_LDS 1  // a grouped-layout workgroup straddling two scenarios stages both in LDS
-#endif
 #ifndef D2D_SPLIT3
-#define D2D_SPLIT3 -1    // W2, W1 and W3 re-check one third each of the golden-march table (needs D2D_SPLIT):
-                         // 1 always, 0 never, -1 when K1 has at most one workgroup per CU (d2d_step)
+#define D2D_SPLIT3 -1    // W2, W1 and W3 re-check one third each of the golden-march table: 1 always,
+                         // 0 never, -1 when K1 has at most one workgroup per CU (chosen in d2d_step)
 #endif
-#ifndef D2D_SPLIT
-#define D2D_SPLIT 1      // W3 re-checks the second half of W2's golden-march table (0: W2 alone)
-#endif
-#ifndef D2D_W0_TAIL
-#define D2D_W0_TAIL 0    // W0 stores its velocity observation after the reward hand-off (A/B knob)
-#endif
-#ifndef D2D_OBS_VEC
-#define D2D_OBS_VEC 1    // K1 stores its observation tile with 16-byte stores
-#endif
-#ifndef D2D_FILL_COMPACT
-#define D2D_FILL_COMPACT 1  // K4 compacts the envs that need a fill into the leading lanes
-#endif
-#ifndef D2D_RC_SLOTS
-#define D2D_RC_SLOTS 2  // reset-cache entries per env: the next reset's observation and the one after
-#endif
-#ifndef D2D_FILL_PERIOD
-#define D2D_FILL_PERIOD 16  // K4 launched after every this many steps (0: never; graphs of 16 steps)
-#endif
-#ifndef D2D_FILL_EVERY
-#define D2D_FILL_EVERY (D2D_RC_SLOTS == 2 ? 3 : 1)  // of those launches every this many fill (a device tick)
-#endif
-static_assert(D2D_RC_SLOTS == 1 || D2D_RC_SLOTS == 2, "one or two reset-cache slots");
-// K4 split path: slots per block -- about one 64-item round per block between fills (one slot:
-// ~26 fills per 16 steps of 128 slots; two slots: ~35 per 48 steps of 64 slots)
-constexpr int FILL_SPB = (D2D_RC_SLOTS == 2) ? 64 : 128;
-#ifndef D2D_FILL_SPLIT
-#define D2D_FILL_SPLIT 1  // K4: the block's four waves share each round of 64 envs (fill_split)
-#endif
-#ifndef D2D_FILL_SENSE_LATE
-#define D2D_FILL_SENSE_LATE 1  // K4 split: wave 0's sensor part after the first barrier
-#endif
+// Reset-cache entries per env: the next reset's observation and the one after (slot = episode
+// counter mod 2), so K4 may fill every 48 steps instead of 16 without more envs falling back to the
+// synchronous reset.  K4 is launched after every FILL_PERIOD steps (a captured 16-step graph holds one
+// launch) and every FILL_EVERY-th launch fills (a device tick).
+constexpr int RC_SLOTS = 2;
+constexpr int FILL_PERIOD = 16;
+constexpr int FILL_EVERY = 3;
+// K4: slots per block -- about one 64-item round per block between fills (~35 per 48 steps of 64 slots)
+constexpr int FILL_SPB = 64;
 
 
 // Diagnostic phase stamps (separate timing-only build, never in the product): lane 0 of each wave
@@ -230,9 +161,9 @@ constexpr int FILL_SPB = (D2D_RC_SLOTS == 2) ? 64 : 128;
 
 __device__ __forceinline__ const BrTab* brtab(const StepArgs& a, int si) { return a.brt ? a.brt + si : nullptr; }
 // the reset-cache entry of slot i for key ep (the observation of the reset that ends episode ep):
-// slot ep % D2D_RC_SLOTS, so the entries of two consecutive episodes coexist
+// slot ep % RC_SLOTS, so the entries of two consecutive episodes coexist
 __device__ __forceinline__ size_t rc_entry(const StepArgs& a, int i, uint32_t ep) {
-    return (size_t)(D2D_RC_SLOTS == 2 ? (ep & 1u) : 0u) * (size_t)a.ns + (size_t)i;
+    return (size_t)(ep & 1u) * (size_t)a.ns + (size_t)i;
 }
 
 // Scenarios [first, first + count) into LDS; the returned table is indexed by the global scenario
@@ -318,9 +249,6 @@ __device__ __forceinline__ void spawn_state(const StepArgs& a, const Scn& S, int
 // wave-uniform read of an LDS flag written by another wave of the workgroup
 // (explicit LDS address space: a generic volatile access would become a flat load)
 using LdsU32 = __attribute__((address_space(3))) uint32_t;
-#ifndef D2D_WAIT_SLEEP
-#define D2D_WAIT_SLEEP 1  // s_sleep units (64 cycles) between two polls of a hand-off flag
-#endif
 __device__ __forceinline__ bool flag_seen(const uint32_t& f) {
     return __builtin_amdgcn_readfirstlane(*(const volatile LdsU32*)&f) != 0u;
 }
@@ -357,7 +285,6 @@ struct K1Shared {
     uint32_t ep[EPB];         // W0 -> W1, W3: episode counter (the state's copy changes at a reset)
     double sina[EPB];         // W0 -> W2: sin of the post-step frame angle (AA reward)
     uint32_t f_done, f_ca, f_gs, f_pre, f_ver, f_ver1;
-    uint32_t f_end;           // quad workgroups: the group's roles that reached the epilogue
     double pe[2][EPB];        // W3 -> W0: path_err, total_reward (prefetched for the epilogue)
     union {
         struct {
@@ -377,7 +304,7 @@ __device__ __forceinline__ void flag_raise(uint32_t& f) {
     if ((threadIdx.x & 63) == 0) *(volatile LdsU32*)&f = 1u;
 }
 __device__ __forceinline__ void flag_wait(const uint32_t& f) {
-    while (!flag_seen(f)) __builtin_amdgcn_s_sleep(D2D_WAIT_SLEEP);
+    while (!flag_seen(f)) __builtin_amdgcn_s_sleep(1)  /* 64 cycles between polls */;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
@@ -393,7 +320,7 @@ __device__ __forceinline__ void k1_stage(const StepArgs& a, Scn* s_scn, int wg, 
     s0 = ws >= 0 ? ws : -ws - 2;          // a straddling group: its two scenarios s0, s0 + 1
     const int ncopy = (GRP && LDS) ? (ws >= 0 ? 1 : 2) : a.n_scn;
     hots = nullptr;
-    if (D2D_GLDS && LDS && (ncopy == 1 || !LTAB)) {
+    if (LDS && (ncopy == 1 || !LTAB)) {
         // one scenario (+ its probe table) or scenarios only: contiguous sources, LDS-DMA
         glds_copy<K1_THREADS / 64>(s_scn, a.scn + s0, (int)sizeof(Scn) * ncopy);
         if (LTAB) glds_copy<K1_THREADS / 64>(s_scn + 1, &a.brt[s0].hot, (int)sizeof(BtHot));
@@ -405,13 +332,12 @@ __device__ __forceinline__ void k1_stage(const StepArgs& a, Scn* s_scn, int wg, 
     }
 }
 
-// One env step for the 64 envs of group wg (slots [64 wg, 64 wg + 64); wg < 0: an empty quarter of a
-// quad workgroup, every lane invalid) by the calling wave in role `role` (0..3, wave-uniform); qt =
+// One env step for the 64 envs of group wg (slots [64 wg, 64 wg + 64)) by the calling wave in role `role` (0..3, wave-uniform); qt =
 // 64 role + lane, the thread's index among the group's 256.  scns / hots: the scenario and probe
 // tables indexed by global scenario id (LDS when staged: LDS / LTAB), s0 the group's scenario.
 // All 256 threads of the group call it once; the workgroup's barriers are block-wide, so every
 // wave of the block runs k1_body exactly once.
-template <bool LDS, bool LTAB, bool GRP, bool QSYNC = false, bool S3 = false>
+template <bool LDS, bool LTAB, bool GRP, bool S3 = false>
 __device__ __forceinline__ void k1_body(const StepArgs& a, const Scn* scns, const BtHot* hots, int s0, K1Shared& sh,
                                         int wg, int role, int qt) {
     const int wave = role;
@@ -424,42 +350,18 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const Scn* scns, cons
     const int n = a.ns;
     const bool auto_reset = a.cfg.auto_reset != 0;
     STAMP(0);
-    if (D2D_FILL_EVERY > 1 && wg == 0 && qt == 0 && a.fill_ctl)  // K4's tick: publish its next value
+    if (wg == 0 && qt == 0 && a.fill_ctl)  // K4's tick: publish its next value
         __hip_atomic_store(&a.fill_ctl[0], __hip_atomic_load(&a.fill_ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (wg == 0 && qt == 0 && a.clock)  // the step clock (fresh curriculum stage schedule)
         __hip_atomic_fetch_add(a.clock, (int64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (wave == 0) sh.scn[lane] = (valid && a.env_scn && a.n_scn > 1) ? a.env_scn[ie] : s0;
     if (S3 && wave == 0) sh.pflags[lane] = 0x7fffffffu;  // W1 and W3 min their table parts in
-    // state loads issued before the staging barrier, so their HBM latency overlaps the staging:
-    // W0 the whole state + action, the other roles the frame
-    Body PB[3]{};
-    double PJ[12];
-    int Pt = 0;
-    uint32_t Pfl = 0;
-    float2 Pact = make_float2(0.0f, 0.0f);
-    if (D2D_PREFETCH && valid) {
-        if (wave == 0 && (D2D_PREFETCH & 5)) {
-#pragma unroll
-            for (int b = 0; b < 3; ++b) {
-                PB[b].px = fld(a.st, 6 * b + 0, n, i);
-                PB[b].py = fld(a.st, 6 * b + 1, n, i);
-                PB[b].a = fld(a.st, 6 * b + 2, n, i);
-                PB[b].vx = fld(a.st, 6 * b + 3, n, i);
-                PB[b].vy = fld(a.st, 6 * b + 4, n, i);
-                PB[b].w = fld(a.st, 6 * b + 5, n, i);
-            }
-            if (D2D_PREFETCH & 1) {
-#pragma unroll
-                for (int k = 0; k < 12; ++k) PJ[k] = fld(a.st, D2D_S_J + k, n, i);
-            }
-            Pt = fld(a.ist, D2D_I_T, n, i);
-            Pfl = (uint32_t)fld(a.ist, D2D_I_FLAGS, n, i);
-            Pact = reinterpret_cast<const float2*>(a.act)[ie];
-        } else if (wave != 0 && (D2D_PREFETCH & 2)) {
-            PB[0] = load_frame(a, i);
-        }
-    }
+    // W1..W3 load the pre-step frame before the staging barrier, so its HBM latency overlaps the
+    // staging (and every read precedes W0's stores of the new positions).  W0 loads its state after
+    // the barrier: issuing those ~30 loads earlier spilled registers (42 vs 32 us).
+    Body PF{};
+    if (valid && wave != 0) PF = load_frame(a, i);
     if (qt == 0) {
         sh.f_done = 0u;
         sh.f_ca = 0u;
@@ -467,7 +369,6 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const Scn* scns, cons
         sh.f_pre = 0u;
         sh.f_ver = 0u;
         sh.f_ver1 = 0u;
-        sh.f_end = 0u;
     }
     __syncthreads();
     STAMP(1);
@@ -485,35 +386,26 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const Scn* scns, cons
     bool done = false;
     if (wave == 0) {
         // ---------------------------------------------------------------- physics
-        D2D_SETPRIO(D2D_PRIO_W0);
+        __builtin_amdgcn_s_setprio(PRIO_W0);
         double ov[19];
         Body B[3];
         double j[12], cs[3], sn[3], fx = 0.0, fy = 0.0, tq = 0.0;
         if (valid && !(D2D_ABL & 1)) {
-            if (D2D_PREFETCH & 5) {
 #pragma unroll
-                for (int b = 0; b < 3; ++b) B[b] = PB[b];
-#pragma unroll
-                for (int k = 0; k < 12; ++k) j[k] = (D2D_PREFETCH & 1) ? PJ[k] : fld(a.st, D2D_S_J + k, n, i);
-                t = Pt;
-                flags = Pfl;
-            } else {
-#pragma unroll
-                for (int b = 0; b < 3; ++b) {
-                    B[b].px = fld(a.st, 6 * b + 0, n, i);
-                    B[b].py = fld(a.st, 6 * b + 1, n, i);
-                    B[b].a = fld(a.st, 6 * b + 2, n, i);
-                    B[b].vx = fld(a.st, 6 * b + 3, n, i);
-                    B[b].vy = fld(a.st, 6 * b + 4, n, i);
-                    B[b].w = fld(a.st, 6 * b + 5, n, i);
-                }
-#pragma unroll
-                for (int k = 0; k < 12; ++k) j[k] = fld(a.st, D2D_S_J + k, n, i);
-                t = fld(a.ist, D2D_I_T, n, i);
-                flags = (uint32_t)fld(a.ist, D2D_I_FLAGS, n, i);
+            for (int b = 0; b < 3; ++b) {
+                B[b].px = fld(a.st, 6 * b + 0, n, i);
+                B[b].py = fld(a.st, 6 * b + 1, n, i);
+                B[b].a = fld(a.st, 6 * b + 2, n, i);
+                B[b].vx = fld(a.st, 6 * b + 3, n, i);
+                B[b].vy = fld(a.st, 6 * b + 4, n, i);
+                B[b].w = fld(a.st, 6 * b + 5, n, i);
             }
+#pragma unroll
+            for (int k = 0; k < 12; ++k) j[k] = fld(a.st, D2D_S_J + k, n, i);
+            t = fld(a.ist, D2D_I_T, n, i);
+            flags = (uint32_t)fld(a.ist, D2D_I_FLAGS, n, i);
             // thrust in float32 exactly as SB3's float32 action hits drone_2d_env.py:400-401
-            const float2 act = (D2D_PREFETCH & 5) ? Pact : reinterpret_cast<const float2*>(a.act)[ie];
+            const float2 act = reinterpret_cast<const float2*>(a.act)[ie];
             const float fs = (float)a.cfg.force_scale;
             const float lf = __fmul_rn(__fadd_rn(act.x / 2.0f, 0.5f), fs);
             const float rf = __fmul_rn(__fadd_rn(act.y / 2.0f, 0.5f), fs);
@@ -560,9 +452,9 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const Scn* scns, cons
         }
         flag_raise(sh.f_gs);
         STAMP(4);
-        // velocity part of the observation (obs 0-2, 17-18) into the tile / terminal obs (D2D_W0_TAIL:
-        // stored after the reward hand-off below, which W2 waits for)
-        const auto vel_obs_out = [&]() {
+        // velocity part of the observation (obs 0-2, 17-18) into the tile / terminal obs
+        if (valid) {
+            sensor_vel(F0, sn[0], cs[0], ov);
             if (!(done && auto_reset)) {
                 orow[0] = (float)ov[0];
                 orow[1] = (float)ov[1];
@@ -577,10 +469,6 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const Scn* scns, cons
                 trow[17] = (float)ov[17];
                 trow[18] = (float)ov[18];
             }
-        };
-        if (valid) {
-            sensor_vel(F0, sn[0], cs[0], ov);
-            if (!D2D_W0_TAIL) vel_obs_out();
         }
         // velocity part of the reward (speed, velocity angle, CA total), for W2
         flag_wait(sh.f_ca);
@@ -601,18 +489,17 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const Scn* scns, cons
             dclose = C.d;
         }
         flag_raise(sh.f_pre);
-        if (D2D_W0_TAIL && valid) vel_obs_out();
     } else if (wave == 1) {
         // ---------------------------------------------------------------- sensing
         float row[19];
         bool need = false;
         if (S3) {
             // the middle third of W2's golden-march re-check first, at W2's priority (its critical path)
-            __builtin_amdgcn_s_setprio(D2D_PRIO_W2);
+            __builtin_amdgcn_s_setprio(PRIO_W2);
             if (valid && !(D2D_ABL & 4) && !(D2D_ABLATE & 1) && a.brt) {
                 const BrTab& T = a.brt[sh.scn[lane]];
                 const BtHot* hot = LTAB ? hots + sh.scn[lane] : &T.hot;
-                Body F = (D2D_PREFETCH & 2) ? PB[0] : load_frame(a, i);
+                Body F = PF;
                 advance_position(F);
                 BtLane L = bt_start<LTAB>(T, hot, F.px, F.py);
                 const int k0 = bt_third(T, 1), k1 = bt_third(T, 2);
@@ -624,12 +511,10 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const Scn* scns, cons
                 atomicMin(&sh.pflags[lane], (uint32_t)L.dev);
             }
             flag_raise(sh.f_ver1);
-            __builtin_amdgcn_s_setprio(D2D_PRIO_W1);
-        } else {
-            D2D_SETPRIO(D2D_PRIO_W1);
         }
+        __builtin_amdgcn_s_setprio(PRIO_W1);
         if (valid && !(D2D_ABL & 2)) {
-            Body F = (D2D_PREFETCH & 2) ? PB[0] : load_frame(a, i);
+            Body F = PF;
             advance_position(F);
             double so[19];
             sensor_pos(a.cfg, S, F.px, F.py, F.a, so);
@@ -672,7 +557,6 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const Scn* scns, cons
             }
         }
         STAMP(4);
-        if (D2D_PRIO_W1_POST != D2D_PRIO_W1) __builtin_amdgcn_s_setprio(D2D_PRIO_W1_POST);
         flag_wait(sh.f_gs);
         STAMP(5);
         if (valid) {
@@ -688,15 +572,15 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const Scn* scns, cons
     } else if (wave == 2) {
         // ---------------------------------------------------------------- path search (critical)
         // the critical path, so it wins issue arbitration on its SIMD
-        D2D_SETPRIO(D2D_PRIO_W2);
+        __builtin_amdgcn_s_setprio(PRIO_W2);
         double po[8];
         Body F{};
         if (valid && !(D2D_ABL & 4)) {
-            F = (D2D_PREFETCH & 2) ? PB[0] : load_frame(a, i);
+            F = PF;
             advance_position(F);
             uint32_t f = (uint32_t)fld(a.ist, D2D_I_FLAGS, n, i);
             const BrTab* T = brtab(a, sh.scn[lane]);
-            if (D2D_SPLIT && T && !(D2D_ABLATE & 1)) {
+            if (T && !(D2D_ABLATE & 1)) {
                 // golden-march re-check of steps [1, split); W3 checks [split, len) meanwhile
                 const BtHot* hot = LTAB ? hots + sh.scn[lane] : &T->hot;
                 BtLane L = bt_start<LTAB>(*T, hot, F.px, F.py);
@@ -713,7 +597,7 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const Scn* scns, cons
             sh.pflags[lane] = f & D2D_FLAG_LA_LOCK;
         }
         STAMP(4);
-        if (D2D_PRIO_W2_POST != D2D_PRIO_W2) __builtin_amdgcn_s_setprio(D2D_PRIO_W2_POST);
+        __builtin_amdgcn_s_setprio(PRIO_W2_POST);
         // the reward terms that do not need the joint sweep, while the physics wave finishes
         flag_wait(sh.f_done);
         flag_wait(sh.f_ca);
@@ -758,13 +642,13 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const Scn* scns, cons
         }
     } else {
         // ---------------------------------------------------------------- auto-reset observation
-        if (D2D_SPLIT) D2D_SETPRIO(D2D_PRIO_W3_TAB);  // the re-check below is on W2's critical path
+        __builtin_amdgcn_s_setprio(PRIO_W2);  // the re-check below is on W2's critical path
         double po[8];
-        if (D2D_SPLIT && valid && !(D2D_ABL & 4) && !(D2D_ABLATE & 1) && a.brt) {
+        if (valid && !(D2D_ABL & 4) && !(D2D_ABLATE & 1) && a.brt) {
             // second half of W2's golden-march re-check (its first wave-priority work)
             const BrTab& T = a.brt[sh.scn[lane]];
             const BtHot* hot = LTAB ? hots + sh.scn[lane] : &T.hot;
-            Body F = load_frame(a, i);
+            Body F = PF;
             advance_position(F);
             BtLane L = bt_start<LTAB>(T, hot, F.px, F.py);
             const int k0 = S3 ? bt_third(T, 2) : bt_split(T);
@@ -777,8 +661,7 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const Scn* scns, cons
             else sh.pflags[lane] = (uint32_t)L.dev;
         }
         flag_raise(sh.f_ver);
-        if (D2D_SPLIT) __builtin_amdgcn_s_setprio(D2D_PRIO_W3);
-        else D2D_SETPRIO(D2D_PRIO_W3);
+        __builtin_amdgcn_s_setprio(PRIO_W3);
         if (valid) {
             // running path error / return for W0's epilogue
             sh.pe[0][lane] = fld(a.st, D2D_S_PATH_ERR, n, i);
@@ -832,16 +715,7 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const Scn* scns, cons
         }
     }
     STAMP(2);
-    if (QSYNC) {
-        // quad workgroup: only the group's own four waves meet before its epilogue (the other
-        // groups of the workgroup finish on their own time); an LDS count instead of the barrier
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        if (lane == 0) __hip_atomic_fetch_add(&sh.f_end, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        while (__builtin_amdgcn_readfirstlane(*(const volatile LdsU32*)&sh.f_end) < 4u) __builtin_amdgcn_s_sleep(1);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    } else {
-        __syncthreads();
-    }
+    __syncthreads();
     STAMP(3);
 
     // ---------------------------------------------------------------- epilogue
@@ -860,7 +734,7 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const Scn* scns, cons
         // a full tile is 64 x 27 floats = 432 float4 at a 16-B aligned offset (e0 * 108 B, e0 % 64
         // == 0; the caller's obs buffer is a torch allocation): 16-byte stores
         int k0 = 0;
-        if (D2D_OBS_VEC && rows == EPB && ((uintptr_t)a.obs & 15u) == 0) {
+        if (rows == EPB && ((uintptr_t)a.obs & 15u) == 0) {
             float4* d4 = reinterpret_cast<float4*>(dst);
             const float4* s4 = reinterpret_cast<const float4*>(sh.u.p.obs);
             for (int k = qt; k < words / 4; k += K1_THREADS) d4[k] = s4[k];
@@ -929,7 +803,7 @@ __device__ __forceinline__ void k1_group(const StepArgs& a, Scn* s_scn, K1Shared
     const BtHot* hots;
     int s0;
     k1_stage<LDS, LTAB, GRP>(a, s_scn, wg, scns, hots, s0);
-    k1_body<LDS, LTAB, GRP, false, S3>(a, scns, hots, s0, sh, wg, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6),
+    k1_body<LDS, LTAB, GRP, S3>(a, scns, hots, s0, sh, wg, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6),
                                        (int)threadIdx.x);
 }
 // S3: the three-way table re-check (D2D_SPLIT3), chosen at launch
@@ -952,41 +826,10 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_grouped_kernel(StepArg
     const int ws = a.wg_scn[wg];
     if (a.brt && ws >= 0)
         k1_group<true, true, true, S3>(a, s_scn, sh, wg);
-    else if (D2D_STRADDLE_LDS && ws <= -2)
+    else if (ws <= -2)
         k1_group<true, false, true, S3>(a, s_scn, sh, wg);
     else
         k1_group<false, false, true, S3>(a, s_scn, sh, wg);
-}
-
-// Quad kernel: 16 waves = 4 groups x 4 roles; the QuadDesc tells each wave its quarter and role and
-// which scenarios (+ probe tables) the workgroup stages once for its four groups.  Static LDS 4 x
-// K1Shared + dynamic 4 x (Scn + BtHot): 163 776 of the CU's 163 840 bytes (one workgroup per CU).
-constexpr int QUAD_THREADS = 4 * K1_THREADS;
-template <bool GRP>
-__global__ __launch_bounds__(QUAD_THREADS, 1) void d2d_step_quad_kernel(StepArgs a) {
-    extern __shared__ __attribute__((aligned(16))) Scn q_scn[];  // [4] Scn, then [4] BtHot
-    __shared__ __attribute__((aligned(16))) K1Shared shq[4];
-    const int qi = GRP ? xcd_group(blockIdx.x, gridDim.x) : (int)blockIdx.x;
-    const QuadDesc& D = a.quad[qi];
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const uint32_t code = (uint32_t)(D.roles >> (4 * w)) & 15u;
-    const int q = __builtin_amdgcn_readfirstlane((int)(code >> 2)), role = __builtin_amdgcn_readfirstlane((int)(code & 3u));
-    Scn* stS = q_scn;
-    BtHot* stH = reinterpret_cast<BtHot*>(q_scn + 4);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int sj = D.stage[j];
-        if (sj >= 0) {
-            glds_copy<QUAD_THREADS / 64>(stS + j, a.scn + sj, (int)sizeof(Scn));
-            glds_copy<QUAD_THREADS / 64>(stH + j, &a.brt[sj].hot, (int)sizeof(BtHot));
-        }
-    }
-    const int g = D.group[q], sl = D.qslot[q], s0 = D.s0[q];
-    const int qt = role * 64 + lane;
-    if (sl >= 0)  // the quarter's scenarios staged at slots sl (, sl + 1): indexed by global scenario id
-        k1_body<true, true, GRP, true>(a, stS + sl - s0, stH + sl - s0, s0, shq[q], g, role, qt);
-    else
-        k1_body<false, false, GRP, true>(a, a.scn, nullptr, s0, shq[q], g, role, qt);
 }
 
 // ------------------------------------------------------------------------------------------ K2
@@ -1065,14 +908,7 @@ __device__ __forceinline__ void fill_split(const StepArgs& a, const Scn* scns, c
         spawn_state(a, S, ie, (uint32_t)ep, sp);
         if (r0 == 0) FSTAMP(2);
         float* c = a.rc_obs + ce * D2D_OBS_DIM;
-        if (wave == 0 && !D2D_FILL_SENSE_LATE) {
-            double so[19];
-            sensor_obs(a.cfg, S, Body{sp[0], sp[1], sp[2], 0.0, 0.0, 0.0}, so);
-            if (act) {
-#pragma unroll
-                for (int k = 0; k < 19; ++k) c[k] = (float)so[k];
-            }
-        } else if (wave != 0 && T) {
+        if (wave != 0 && T) {
             const int w = wave - 1;
             BtLane L = bt_start<false>(*T, &T->hot, sp[0], sp[1]);
             // steps [1, b1), [b1, b2), [b2, BT_K)
@@ -1096,7 +932,7 @@ __device__ __forceinline__ void fill_split(const StepArgs& a, const Scn* scns, c
         if (r0 == 0) FSTAMP(3);
         __syncthreads();
         if (r0 == 0) FSTAMP(4);
-        if (wave == 0 && D2D_FILL_SENSE_LATE) {
+        if (wave == 0) {
             // the sensor part is independent of the path search: off the barrier's critical path
             double so[19];
             sensor_obs(a.cfg, S, Body{sp[0], sp[1], sp[2], 0.0, 0.0, 0.0}, so);
@@ -1143,31 +979,22 @@ __device__ __forceinline__ void fill_work(const StepArgs& a) {
     FSTAMP(0);
     const Scn* scns = stage_scenarios<LDS, BLOCK>(a, s_scn);
     const int n = a.ns;
-    // slots per block: BLOCK, or FILL_SPB with the split path (about one 64-env round per block)
-    const int spb = (D2D_FILL_SPLIT && D2D_FILL_COMPACT) ? FILL_SPB : BLOCK;
-    // work items: (slot, which) -- the entry for the env's current episode counter (which = 0) and,
-    // with two slots, for the next one (which = 1); thread t takes slot t % spb, which t / spb
-    static_assert(D2D_RC_SLOTS == 1 || (D2D_FILL_SPLIT && D2D_FILL_COMPACT && 2 * FILL_SPB <= BLOCK),
-                  "two reset-cache slots need the split, compacting fill with 2 items per slot");
-    const int which = (D2D_RC_SLOTS == 2) ? (int)threadIdx.x / spb : 0;
-    const int i0 = blockIdx.x * spb + ((D2D_RC_SLOTS == 2) ? (int)threadIdx.x % spb : (int)threadIdx.x);  // slot
-    const bool need = ((int)threadIdx.x < D2D_RC_SLOTS * spb) && (i0 < n) &&
-                      (!a.lane_env || a.lane_env[i0] >= 0) && [&] {
-                          const int32_t key = fld(a.ist, D2D_I_EPISODE, n, i0) + which;
-                          // fresh curriculum: only once the scenario of that episode exists
-                          return a.rc_tag[rc_entry(a, i0, (uint32_t)key)] != key &&
-                                 (a.cfg.scn_pool != 2 || a.scn_tag[fresh_slot(i0, (uint32_t)key)] == key);
-                      }();
-    int i = i0, total = 0;
-    if (!D2D_FILL_COMPACT) {
-        __syncthreads();
-        if (!need) return;
-    } else {
+    // work items: (slot, which) -- the entry for the env's current episode counter (which = 0) and
+    // for the next one (which = 1); thread t takes slot t % FILL_SPB, which t / FILL_SPB
+    static_assert(RC_SLOTS == 2 && 2 * FILL_SPB <= BLOCK, "two items per slot");
+    const int which = (int)threadIdx.x / FILL_SPB;
+    const int i0 = blockIdx.x * FILL_SPB + (int)threadIdx.x % FILL_SPB;  // slot
+    const bool need = ((int)threadIdx.x < RC_SLOTS * FILL_SPB) && (i0 < n) && (!a.lane_env || a.lane_env[i0] >= 0) && [&] {
+        const int32_t key = fld(a.ist, D2D_I_EPISODE, n, i0) + which;
+        // fresh curriculum: only once the scenario of that episode exists
+        return a.rc_tag[rc_entry(a, i0, (uint32_t)key)] != key &&
+               (a.cfg.scn_pool != 2 || a.scn_tag[fresh_slot(i0, (uint32_t)key)] == key);
+    }();
     const uint64_t m = __ballot(need);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     if (lane == 0) cnt[wave] = __popcll(m);
     __syncthreads();
-    int off = 0;
+    int off = 0, total = 0;
 #pragma unroll
     for (int w = 0; w < BLOCK / 64; ++w) {
         off += (w < wave) ? cnt[w] : 0;
@@ -1175,56 +1002,27 @@ __device__ __forceinline__ void fill_work(const StepArgs& a) {
     }
     if (need) list[off + __popcll(m & ((1ull << lane) - 1ull))] = 2 * i0 + which;
     __syncthreads();
-    if (D2D_FILL_SPLIT) {
-        if (total == 0) return;  // block-uniform
-    } else {
-        if ((int)threadIdx.x >= total) return;
-        i = list[threadIdx.x] >> 1;
-    }
-    }
-    if (D2D_FILL_SPLIT && D2D_FILL_COMPACT) {
-        FSTAMP(1);
-        fill_split(a, scns, list, total);
-        FSTAMP(7);
+    if (total == 0) return;  // block-uniform
+    FSTAMP(1);
+    fill_split(a, scns, list, total);
+    FSTAMP(7);
 #ifdef D2D_STAMPS
-        if (a.stamps && threadIdx.x == 0)  // the block's number of fills after the stamps
-            a.stamps[D2D_FSTAMP_BASE + (size_t)gridDim.x * 32 + blockIdx.x] = (uint64_t)total;
+    if (a.stamps && threadIdx.x == 0)  // the block's number of fills after the stamps
+        a.stamps[D2D_FSTAMP_BASE + (size_t)gridDim.x * 32 + blockIdx.x] = (uint64_t)total;
 #endif
-        return;
-    }
-    const int32_t ep = fld(a.ist, D2D_I_EPISODE, n, i);
-    const int ie = a.lane_env ? a.lane_env[i] : i;  // env of slot i
-    const int si = next_scenario(a, ie, (uint32_t)ep);
-    const Scn& S = scns[si];
-    double sp[7], so[19], o[8];
-    spawn_state(a, S, ie, (uint32_t)ep, sp);
-    uint32_t f = 0;
-    sensor_obs(a.cfg, S, Body{sp[0], sp[1], sp[2], 0.0, 0.0, 0.0}, so);
-    path_obs(a.cfg, S, brtab(a, si), sp[0], sp[1], sp[2], f, o);
-    const size_t ce = rc_entry(a, i, (uint32_t)ep);  // (one slot: this path is not built with two)
-    float* c = a.rc_obs + ce * D2D_OBS_DIM;
-#pragma unroll
-    for (int k = 0; k < 19; ++k) c[k] = (float)so[k];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) c[19 + k] = (float)o[k];
-    a.rc_rfl[ce] = (int32_t)f;
-    a.rc_tag[ce] = ep;
 }
 
-// The launch cadence is fixed on the host (every D2D_FILL_PERIOD steps, so a captured graph of 16
-// steps holds one launch); with two cache slots only every D2D_FILL_EVERY-th launch fills, decided
+// The launch cadence is fixed on the host (every FILL_PERIOD steps, so a captured graph of 16
+// steps holds one launch); only every FILL_EVERY-th launch fills, decided
 // by a device tick (so a replayed graph alternates too): every workgroup reads ctl[0], workgroup 0
 // writes the next value to ctl[1], and the next K1 launch copies it to ctl[0] -- no workgroup
 // writes what another may still read, and no atomics contend on one address.
-// D2D_FILL_RESIDENT: K4 with K1's residency (4 waves per SIMD, K1's LDS per workgroup: exactly 4
-// workgroups per CU, one round).  K4 (1 024 workgroups at 65 536 envs) otherwise ran 3 per CU and
-// left the CUs' wave-placement rotation uneven, and the next K1 then put two path waves of one CU
-// on one SIMD on a few CUs (+7 us on that step, tools/ubench_after_stamps.py).
-#ifndef D2D_FILL_RESIDENT
-#define D2D_FILL_RESIDENT 1
-#endif
+// K4 runs with K1's residency (4 waves per SIMD, K1's LDS per workgroup: exactly 4 workgroups per
+// CU, one round).  K4 (1 024 workgroups at 65 536 envs) otherwise ran 3 per CU and left the CUs'
+// wave-placement rotation uneven, and the next K1 then put two path waves of one CU on one SIMD on
+// a few CUs (+7 us on that step, tools/ubench_after_stamps.py).
 template <bool LDS>
-__global__ __launch_bounds__(BLOCK, D2D_FILL_RESIDENT ? 4 : 1) void d2d_fill_kernel(StepArgs a) {
+__global__ __launch_bounds__(BLOCK, 4) void d2d_fill_kernel(StepArgs a) {
     const bool ticked = !a.fill_force && a.fill_every > 1;
     bool run = true;
     if (ticked) {

@@ -131,123 +131,14 @@ struct MlpPair {
     MlpNet net[2];
 };
 constexpr int MLP_BLOCK = 256, OBS = 27, HID = 64;
-// the weights through the constant address space: wave-uniform loads become scalar loads (SGPR
-// operands of the FMAs) instead of one vector load per weight
-using CW = const __attribute__((address_space(4))) float*;
-__device__ __forceinline__ CW cw(const float* p) { return (CW)p; }
 
 // TPS threads per (sample, net): thread t of a workgroup serves sample t / TPS of the workgroup's
 // MLP_SPB and owns output units [UNITS (t % TPS), UNITS (t % TPS + 1)) of every layer; the layer
 // inputs of a sample (x, h1; g2 in the backward pass) are an LDS column all its threads read.
-#ifndef D2D_PPO_TPS
-#define D2D_PPO_TPS 4  // threads per (sample, net)
-#endif
-constexpr int TPS = D2D_PPO_TPS, MLP_SPB = MLP_BLOCK / TPS, UNITS = HID / TPS;
-constexpr int WT_NET = OBS * HID + HID * HID;
+constexpr int TPS = 4, MLP_SPB = MLP_BLOCK / TPS, UNITS = HID / TPS;
 
-// W1^T [27][64] and W2^T [64][64] of the workgroup's net staged in LDS: input unit k outermost (a
-// rolled loop), 32 independent accumulators, the weight row of k read as LDS broadcasts
-__global__ __launch_bounds__(MLP_BLOCK) void mlp_forward_kernel(MlpPair P, int m, const int64_t* __restrict__ idx,
-                                                                const float* __restrict__ obs,
-                                                                float* __restrict__ xg) {
-    __shared__ __attribute__((aligned(16))) float wt[WT_NET];
-    __shared__ float col[HID][MLP_SPB];  // the layer input of every sample (x: rows 0..26, then h1)
-    const MlpNet& N = P.net[blockIdx.y];
-    for (int e = threadIdx.x; e < WT_NET; e += MLP_BLOCK) {
-        if (e < OBS * HID) {
-            const int k = e / HID, j = e % HID;
-            wt[e] = N.w1[j * OBS + k];
-        } else {
-            const int f = e - OBS * HID, k = f / HID, j = f % HID;
-            wt[e] = N.w2[j * HID + k];
-        }
-    }
-    const int i0 = blockIdx.x * MLP_SPB;
-    for (int e = threadIdx.x; e < OBS * MLP_SPB; e += MLP_BLOCK) {
-        const int k = e / MLP_SPB, sl = e % MLP_SPB, i = i0 + sl;
-        const float v = i < m ? obs[idx[i] * OBS + k] : 0.0f;
-        col[k][sl] = v;
-        if (blockIdx.y == 0 && i < m) xg[(size_t)i * OBS + k] = v;  // the gathered minibatch observations
-    }
-    __syncthreads();
-    const int sl = threadIdx.x / TPS, u0 = (threadIdx.x % TPS) * UNITS;
-    const int i = i0 + sl;
-    const CW b1 = cw(N.b1), b2 = cw(N.b2), w3 = cw(N.w3), b3 = cw(N.b3);
-    float acc[UNITS];
-    // layer 1: h1[j] = tanh(b1[j] + sum_k W1[j][k] x[k])
-#pragma unroll
-    for (int j = 0; j < UNITS; ++j) acc[j] = N.b1[u0 + j];
-#pragma unroll 1
-    for (int k = 0; k < OBS; ++k) {
-        const float xv = col[k][sl];
-        const float4* w = reinterpret_cast<const float4*>(wt + k * HID + u0);
-#pragma unroll
-        for (int j4 = 0; j4 < UNITS / 4; ++j4) {
-            const float4 wv = w[j4];
-            acc[4 * j4] += wv.x * xv;
-            acc[4 * j4 + 1] += wv.y * xv;
-            acc[4 * j4 + 2] += wv.z * xv;
-            acc[4 * j4 + 3] += wv.w * xv;
-        }
-    }
-    __syncthreads();  // every x column has been read before h1 overwrites rows 0..26
-#pragma unroll
-    for (int j = 0; j < UNITS; ++j) {
-        acc[j] = tanhf(acc[j]);
-        col[u0 + j][sl] = acc[j];
-    }
-    if (i < m) {
-#pragma unroll
-        for (int j = 0; j < UNITS; j += 4)
-            *reinterpret_cast<float4*>(N.h1 + (size_t)i * HID + u0 + j) =
-                make_float4(acc[j], acc[j + 1], acc[j + 2], acc[j + 3]);
-    }
-    __syncthreads();  // both halves of h1 are in the column
-    // layer 2 and the output layer
-#pragma unroll
-    for (int j = 0; j < UNITS; ++j) acc[j] = N.b2[u0 + j];
-#pragma unroll 1
-    for (int k = 0; k < HID; ++k) {
-        const float hv = col[k][sl];
-        const float4* w = reinterpret_cast<const float4*>(wt + OBS * HID + k * HID + u0);
-#pragma unroll
-        for (int j4 = 0; j4 < UNITS / 4; ++j4) {
-            const float4 wv = w[j4];
-            acc[4 * j4] += wv.x * hv;
-            acc[4 * j4 + 1] += wv.y * hv;
-            acc[4 * j4 + 2] += wv.z * hv;
-            acc[4 * j4 + 3] += wv.w * hv;
-        }
-    }
-    float o0 = 0.0f, o1 = 0.0f;
-#pragma unroll
-    for (int j = 0; j < UNITS; ++j) {
-        acc[j] = tanhf(acc[j]);
-        o0 += N.w3[u0 + j] * acc[j];
-        if (N.od == 2) o1 += N.w3[HID + u0 + j] * acc[j];
-    }
-#pragma unroll
-    for (int o = 1; o < TPS; o <<= 1) {  // the sample's other threads (adjacent lanes)
-        o0 += __shfl_xor(o0, o, 64);
-        o1 += __shfl_xor(o1, o, 64);
-    }
-    if (i >= m) return;
-#pragma unroll
-    for (int j = 0; j < UNITS; j += 4)
-        *reinterpret_cast<float4*>(N.h2 + (size_t)i * HID + u0 + j) =
-            make_float4(acc[j], acc[j + 1], acc[j + 2], acc[j + 3]);
-    if (u0 == 0) {
-        if (N.od == 2) {
-            N.out[2 * i] = o0 + b3[0];
-            N.out[2 * i + 1] = o1 + b3[1];
-        } else {
-            N.out[i] = o0 + b3[0];
-        }
-    }
-    (void)b1;
-    (void)b2;
-    (void)w3;
-}
+// (A VALU forward, one thread per (sample, net) quarter with the weights staged in LDS, ran 42.5 us
+// per 32 768-sample minibatch against 25 us for the matrix-core kernel below; removed in round 4.)
 
 // The forward pass on the matrix cores (v_mfma_f32_32x32x2_f32): a workgroup takes FM_TILES = 2
 // tiles of FM_SPB = 32 samples and both nets; wave w computes the 32 (samples) x 32 (units) tile
@@ -257,20 +148,13 @@ __global__ __launch_bounds__(MLP_BLOCK) void mlp_forward_kernel(MlpPair P, int m
 // 16 samples, so h1 goes through LDS (as the next layer's A operand, and to global memory as row
 // stores) and so does h2 (the output layers are 64-term dot products per (output row, sample), one
 // thread each, weights in LDS).  Measured per 32768-sample minibatch (rocprofv3): 1 tile per
-// workgroup 29.8 us, 2 tiles 25.4 us, 4 tiles 35.0 us (one workgroup per CU); the VALU kernel 42.5 us.
-#ifndef D2D_PPO_FWD_MFMA
-#define D2D_PPO_FWD_MFMA 1
-#endif
+// workgroup 29.8 us, 2 tiles 25.4 us, 4 tiles 35.0 us (one workgroup per CU).
 constexpr int FM_SPB = 32, FM_TILES = 2, XS = OBS + 2, HS = HID + 1;  // LDS row strides: bank spread
-// tanh for the matrix-core forward (D2D_PPO_FTANH=1): |x| < 0.25 an odd Taylor polynomial (next term
+// tanh for the matrix-core forward: |x| < 0.25 an odd Taylor polynomial (next term
 // < 3e-8 relative), else (1 - t) / (1 + t) with t = exp(-2 |x|) from v_exp_f32 and v_rcp_f32 (no
 // cancellation: 1 - t >= 0.39): a few ulp, 15 instructions instead of the library's ~60, which made
 // the hidden layers' activations the longest part of a forward workgroup.
-#ifndef D2D_PPO_FTANH
-#define D2D_PPO_FTANH 1
-#endif
 __device__ __forceinline__ float ftanh(float x) {
-    if (!D2D_PPO_FTANH) return tanhf(x);
     const float ax = fabsf(x), x2 = x * x;
     const float p = x * (1.0f + x2 * (-0.333333333f + x2 * (0.133333333f + x2 * (-0.0539682540f + x2 * 0.0218694885f))));
     const float t = __builtin_amdgcn_exp2f(ax * -2.88539008f);  // exp(-2 |x|)
@@ -709,147 +593,9 @@ __global__ __launch_bounds__(MLP_BLOCK) void mlp_backward_kernel(MlpPair P, int 
     }
 }
 
-// The same loss head and backward pass with g1 = g2 W2 on the matrix cores (D2D_PPO_BWD_MFMA=1): a
-// workgroup takes 64 samples and both nets.  Threads 0-63 compute the policy head of one sample
-// each, 64-127 the value head; then g2 = (gout W3) (1 - h2^2) for every (sample, net, unit) into
-// global memory (the weight gradients read it) and into LDS as the A operand; wave w computes the
-// 32 (samples) x 32 (units) tiles [net w / 2, units 32 (w % 2) ..] of g1 = g2 W2 for both 32-sample
-// halves with v_mfma_f32_32x32x2_f32, its B operands (W2's rows, 128-byte coalesced) held in
-// registers.  Partial rows: row b holds all five sums, row nb + b zeros (head_finish adds all rows).
-#ifndef D2D_PPO_BWD_MFMA
-#define D2D_PPO_BWD_MFMA 0
-#endif
-__global__ __launch_bounds__(256) void mlp_backward_mfma_kernel(MlpPair P, int m, const int64_t* __restrict__ idx,
-                                                                const float* __restrict__ act,
-                                                                const float* __restrict__ old_logp,
-                                                                const float* __restrict__ adv,
-                                                                const float* __restrict__ ret,
-                                                                const float* __restrict__ log_std,
-                                                                const double* __restrict__ ws, int nbs,
-                                                                int normalize, float clip, float vf_coef,
-                                                                float* __restrict__ partial) {
-    constexpr int SPB = FM_TILES * FM_SPB;  // 64 samples per workgroup
-    __shared__ double red[5 * 4];
-    __shared__ float g2s[2][SPB][HS];       // g2 of both nets, one sample per row (A operands)
-    __shared__ float gos[3][SPB];           // d loss / d (mean0, mean1, value)
-    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, ci = lane & 31, h = lane >> 5;
-    const int sb = blockIdx.x * SPB, net = w >> 1, k0 = (w & 1) * 32;
-    // this wave's B operands: W2[net][2 t + h][k0 + ci], issued first (consumed after the head)
-    float w2r[HID / 2];
-    {
-        const float* W2 = P.net[net].w2 + k0 + ci;
-#pragma unroll
-        for (int t = 0; t < HID / 2; ++t) w2r[t] = W2[(2 * t + h) * HID];
-    }
-    float adv_mean = 0.0f, adv_inv = 1.0f;
-    if (normalize) {
-        double sm = 0.0, sq = 0.0;
-        for (int b = tid; b < nbs; b += 256) {
-            sm += ws[2 * b];
-            sq += ws[2 * b + 1];
-        }
-        double sv[2] = {sm, sq};
-        block_sum_n(sv, red);
-        const double mu = sv[0] / m, var = (sv[1] - sv[0] * mu) / (m > 1 ? m - 1 : 1);
-        adv_mean = (float)mu;
-        adv_inv = 1.0f / ((float)sqrt(var > 0.0 ? var : 0.0) + 1e-8f);
-    }
-    double q[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
-    if (tid < 2 * SPB) {
-        const int sl = tid & (SPB - 1), i = sb + sl;
-        float g0 = 0.0f, g1v = 0.0f;
-        if (i < m) {
-            const int64_t j = idx[i];
-            if (tid < SPB) {  // the policy head (mlp_backward_kernel's arithmetic)
-                const MlpNet& N = P.net[0];
-                const float ls0 = log_std[0], ls1 = log_std[1];
-                const float is0 = expf(-ls0), is1 = expf(-ls1);
-                const float z0 = (act[2 * j] - N.out[2 * i]) * is0, z1 = (act[2 * j + 1] - N.out[2 * i + 1]) * is1;
-                const float logp = (-0.5f * z0 * z0 - ls0 - HALF_LOG_2PI) + (-0.5f * z1 * z1 - ls1 - HALF_LOG_2PI);
-                const float a = normalize ? (adv[j] - adv_mean) * adv_inv : adv[j];
-                const float ratio = expf(logp - old_logp[j]);
-                const float s1 = a * ratio, s2 = a * fminf(fmaxf(ratio, 1.0f - clip), 1.0f + clip);
-                const float g_lp = (s1 <= s2) ? a * ratio * (-1.0f / m) : 0.0f;
-                g0 = g_lp * z0 * is0;
-                g1v = g_lp * z1 * is1;
-                N.gout[2 * i] = g0;
-                N.gout[2 * i + 1] = g1v;
-                q[0] = fminf(s1, s2);
-                q[2] = fabsf(ratio - 1.0f) > clip ? 1.0 : 0.0;
-                q[3] = (double)g_lp * (z0 * z0 - 1.0f);
-                q[4] = (double)g_lp * (z1 * z1 - 1.0f);
-            } else {  // the value head
-                const MlpNet& N = P.net[1];
-                const float err = ret[j] - N.out[i];
-                g0 = err * (-2.0f * vf_coef / m);
-                N.gout[i] = g0;
-                q[1] = (double)err * err;
-            }
-        }
-        if (tid < SPB) {
-            gos[0][sl] = g0;
-            gos[1][sl] = g1v;
-        } else {
-            gos[2][sl] = g0;
-        }
-    }
-    block_sum_n(q, red);  // (its barriers also publish gos)
-    if (tid == 0) {
-        float* o = partial + (size_t)blockIdx.x * 5;
-        float* z = partial + ((size_t)gridDim.x + blockIdx.x) * 5;
-#pragma unroll
-        for (int k = 0; k < 5; ++k) {
-            o[k] = (float)q[k];
-            z[k] = 0.0f;
-        }
-    }
-    // g2 = (gout W3) (1 - h2^2), as float4s in row order: element e = it 256 + tid is float4 e % 16 of
-    // row (e / 16) % 64 of net e / 1024, so a wave reads / writes four whole 256-byte rows
-#pragma unroll
-    for (int it = 0; it < 2 * SPB * HID / 4 / 256; ++it) {
-        const int e = it * 256 + tid, gn = e >> 10, sl = (e >> 4) & (SPB - 1), u = (e & 15) * 4, i = sb + sl;
-        float g[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-        if (i < m) {
-            const MlpNet& Nn = P.net[gn];
-            const float go0 = gn ? gos[2][sl] : gos[0][sl], go1 = gn ? 0.0f : gos[1][sl];
-            const float4 hv = *reinterpret_cast<const float4*>(Nn.h2 + (size_t)i * HID + u);
-            const float4 wa = *reinterpret_cast<const float4*>(Nn.w3 + u);
-            float4 wb = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            if (gn == 0) wb = *reinterpret_cast<const float4*>(Nn.w3 + HID + u);
-            const float hh[4] = {hv.x, hv.y, hv.z, hv.w}, a4[4] = {wa.x, wa.y, wa.z, wa.w},
-                        b4[4] = {wb.x, wb.y, wb.z, wb.w};
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                float d = go0 * a4[k];
-                if (gn == 0) d += go1 * b4[k];
-                g[k] = d * (1.0f - hh[k] * hh[k]);
-            }
-            *reinterpret_cast<float4*>(Nn.g2 + (size_t)i * HID + u) = make_float4(g[0], g[1], g[2], g[3]);
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) g2s[gn][sl][u + k] = g[k];
-    }
-    __syncthreads();
-    // g1 = (g2 W2) (1 - h1^2) on the matrix cores
-    const MlpNet& N = P.net[net];
-#pragma unroll
-    for (int tile = 0; tile < FM_TILES; ++tile) {
-        f32x16 acc = {};
-#pragma unroll
-        for (int t = 0; t < HID / 2; ++t)
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(g2s[net][tile * FM_SPB + ci][2 * t + h], w2r[t], acc, 0, 0, 0);
-#pragma unroll
-        for (int v = 0; v < 16; ++v) {
-            const int i = sb + tile * FM_SPB + (v & 3) + 8 * (v >> 2) + 4 * h;  // the C/D map
-            if (i < m) {
-                const size_t o = (size_t)i * HID + k0 + ci;
-                const float hv = N.h1[o];
-                N.g1[o] = acc[v] * (1.0f - hv * hv);
-            }
-        }
-    }
-}
-
+// (g1 = g2 W2 on the matrix cores was bit-identical -- an f32 MFMA is an exact fmaf chain -- and
+// measured 33.5 us against 23.4 us for this kernel: the 32 x 32 x 2 f32 MFMA runs at the f32 VALU rate
+// and only adds tile hand-offs.  Removed in round 4.)
 
 // ---------------------------------------------------------------------------- fused minibatch gradient
 // One launch for what mlp_forward_mfma + mlp_backward + wgrad compute (D2D_PPO_FUSED, ABI v5): the
@@ -1169,136 +915,8 @@ __global__ __launch_bounds__(ADAM_THREADS) void adam_kernel(int n, float* __rest
     if (threadIdx.x == 0) t[0] = step;
 }
 
-// adam_kernel's step run by one 256-thread workgroup (the gradient reduce's last one to finish):
-// thread t stands in for adam_kernel's threads t + 256 j (j < 4), with the same per-thread and
-// per-wave summation order of the norm, so the result is bit-identical to adam_kernel's.
-struct AdamArgs {
-    int n;
-    float *p, *m1, *m2, *t;  // p == nullptr: no Adam step in the reduce launch
-    float lr, b1, b2, eps, max_norm;
-    int* ticket;  // workgroups done; the last one resets it to 0
-};
-constexpr int ADAM_VT = ADAM_THREADS / 256;  // virtual adam_kernel threads per thread
-__device__ __forceinline__ void adam_body_256(const AdamArgs& A, float* __restrict__ g) {
-    __shared__ double red[ADAM_THREADS / 64];
-    const int n = A.n, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    float gv[ADAM_VT][ADAM_PER_THREAD];
-    double q[ADAM_VT];
-#pragma unroll
-    for (int j = 0; j < ADAM_VT; ++j) {
-        q[j] = 0.0;
-#pragma unroll
-        for (int k = 0; k < ADAM_PER_THREAD; ++k) {
-            const int i = threadIdx.x + 256 * j + k * ADAM_THREADS;
-            gv[j][k] = i < n ? g[i] : 0.0f;
-        }
-#pragma unroll
-        for (int k = 0; k < ADAM_PER_THREAD; ++k) q[j] += (double)gv[j][k] * gv[j][k];
-    }
-#pragma unroll
-    for (int j = 0; j < ADAM_VT; ++j) q[j] = wave_sum(q[j]);
-    if (lane == 0) {
-#pragma unroll
-        for (int j = 0; j < ADAM_VT; ++j) red[w + 4 * j] = q[j];  // adam_kernel's wave w + 4 j
-    }
-    __syncthreads();
-    double tot = 0.0;
-    for (int k = 0; k < ADAM_THREADS / 64; ++k) tot += red[k];
-    const double norm = sqrt(tot);
-    const float coef = fminf((float)(A.max_norm / (norm + 1e-6)), 1.0f);
-    const float step = A.t[0] + 1.0f;
-    const float b1 = A.b1, b2 = A.b2;
-    const float bc1 = 1.0f - powf(b1, step), bc2s = sqrtf(1.0f - powf(b2, step));
-    const float lr_t = A.lr / bc1;
-#pragma unroll
-    for (int j = 0; j < ADAM_VT; ++j) {
-#pragma unroll
-        for (int k = 0; k < ADAM_PER_THREAD; ++k) {
-            const int i = threadIdx.x + 256 * j + k * ADAM_THREADS;
-            if (i < n) {
-                const float gi = gv[j][k] * coef;
-                g[i] = gi;
-                const float a0 = A.m1[i], v0 = A.m2[i];
-                const float a = a0 + (1.0f - b1) * (gi - a0);
-                const float v = v0 * b2 + (1.0f - b2) * gi * gi;
-                A.m1[i] = a;
-                A.m2[i] = v;
-                A.p[i] -= a * lr_t / (sqrtf(v) / bc2s + A.eps);
-            }
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) A.t[0] = step;
-}
-
-// The same step spread over ceil(n / 1024) workgroups (4 parameters per thread): every workgroup
-// computes the full gradient norm itself (n floats from L2, eight loads in flight per thread, one
-// summation order, so every workgroup gets the same clip coefficient) and updates its slice.  The
-// step counter is read by all of them, so adam_tick_kernel increments it afterwards, and the
-// clipped gradient is not written back (another workgroup may still be reading g for its norm).
-// Off by default: measured 8.1 us + 3.9 us for the one-thread tick launch (a launch costs ~4 us
-// whatever it does) against 10.8 us for the one-workgroup kernel.
-#ifndef D2D_PPO_ADAM_SPREAD
-#define D2D_PPO_ADAM_SPREAD 0
-#endif
-constexpr int ADAM_WG = 256, ADAM_SLICE = 4 * ADAM_WG;
-__global__ __launch_bounds__(ADAM_WG) void adam_spread_kernel(int n, float* __restrict__ p,
-                                                              const float* __restrict__ g, float* __restrict__ m1,
-                                                              float* __restrict__ m2, float* __restrict__ t,
-                                                              float lr, float b1, float b2, float eps,
-                                                              float max_norm, int* __restrict__ ticket) {
-    __shared__ double red[ADAM_WG / 64];
-    const int base = blockIdx.x * ADAM_SLICE + threadIdx.x;
-    float gs[4], a0[4], v0[4], p0[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {  // this workgroup's slice, loaded before the norm pass
-        const int i = base + k * ADAM_WG;
-        gs[k] = i < n ? g[i] : 0.0f;
-        a0[k] = i < n ? m1[i] : 0.0f;
-        v0[k] = i < n ? m2[i] : 0.0f;
-        p0[k] = i < n ? p[i] : 0.0f;
-    }
-    double q = 0.0;
-    int i = threadIdx.x;
-    for (; i + 7 * ADAM_WG < n; i += 8 * ADAM_WG) {
-        float v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = g[i + u * ADAM_WG];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) q += (double)v[u] * v[u];
-    }
-    for (; i < n; i += ADAM_WG) q += (double)g[i] * g[i];
-    const double norm = sqrt(block_sum(q, red));
-    const float coef = fminf((float)(max_norm / (norm + 1e-6)), 1.0f);
-    const float step = t[0] + 1.0f;
-    const float bc1 = 1.0f - powf(b1, step), bc2s = sqrtf(1.0f - powf(b2, step));
-    const float lr_t = lr / bc1;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int e = base + k * ADAM_WG;
-        if (e < n) {
-            const float gi = gs[k] * coef;
-            const float a = a0[k] + (1.0f - b1) * (gi - a0[k]);  // exp_avg.lerp_(grad, 1 - beta1)
-            const float v = v0[k] * b2 + (1.0f - b2) * gi * gi;
-            m1[e] = a;
-            m2[e] = v;
-            p[e] = p0[k] - a * lr_t / (sqrtf(v) / bc2s + eps);
-        }
-    }
-    if (ticket == nullptr) return;  // adam_tick_kernel advances the step counter
-    // with a ticket: the workgroup that finishes last advances it.  Every workgroup has consumed its
-    // read of t[0] (its updates above depend on it) before its thread 0 takes a ticket, and no
-    // workgroup reads anything another one writes, so no fence is needed.
-    __syncthreads();
-    if (threadIdx.x == 0 &&
-        __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1) {
-        t[0] = step;
-        __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-__global__ void adam_tick_kernel(float* t) {
-    if (threadIdx.x == 0) t[0] += 1.0f;
-}
+// (A spread Adam -- ceil(n / 1024) workgroups, each computing the norm -- measured 8.1 us + 3.9 us for
+// a one-thread step-counter launch against 10.8 us for this kernel; removed in round 4.)
 
 // ---------------------------------------------------------------------------- weight gradients
 // Every weight / bias gradient of the two MLPs in one launch: problem k (blockIdx.y) is
@@ -1317,20 +935,15 @@ struct WgradProblems {
 };
 constexpr int WG_TILE = 64, WG_ROWS = 256;
 
-#ifndef D2D_PPO_WGRAD_MFMA
-// 0: VALU 4 x 4 blocks from LDS tiles; 1: matrix cores straight from memory (wgrad_mfma_kernel,
-// 55 vs 36 us: load-latency bound); 2: matrix cores fed from this kernel's LDS tiles
-#define D2D_PPO_WGRAD_MFMA 2
-#endif
+// The products run on the matrix cores fed from this kernel's LDS tiles.  (Measured and removed in
+// round 4: VALU 4 x 4 blocks from the same tiles, 36 us; matrix cores straight from memory, 55 us,
+// load-latency bound.)
 __global__ __launch_bounds__(256) void wgrad_kernel(WgradProblems P, int m, int row_len, float* __restrict__ partial) {
     __shared__ float ta[WG_TILE][64 + 4];
     __shared__ float tb[WG_TILE][64 + 4];
     const WgradProblem& pr = P.k[blockIdx.y];
     const int p = pr.p, q = pr.q;
-    const int pi = (threadIdx.x >> 4) * 4, qi = (threadIdx.x & 15) * 4;  // this thread's 4 x 4 block
-    float acc[4][4] = {};
-    float bsum[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-    // the matrix-core path's tile of this wave (D2D_PPO_WGRAD_MFMA == 2)
+    // this wave's 32 x 32 output tile
     const int mw = threadIdx.x >> 6, mci = threadIdx.x & 31, mh = (threadIdx.x >> 5) & 1;
     const int nqt = (q + 31) / 32, npt = (p + 31) / 32;
     const int mp0 = (mw / max(nqt, 1)) * 32, mq0 = (mw % max(nqt, 1)) * 32;
@@ -1360,98 +973,27 @@ __global__ __launch_bounds__(256) void wgrad_kernel(WgradProblems P, int m, int 
         }
         __syncthreads();
         if (rt + WG_TILE < r1) fetch(rt + WG_TILE);
-        if (D2D_PPO_WGRAD_MFMA == 2) {
-            // wave w: the 32 x 32 output tile (p0, q0); lane l: A[k = l / 32][i = l % 32] = a[row][p0 + i],
-            // B[k][j = l % 32] = b[row][q0 + j], row = 2 t + l / 32
-            if (mw < npt * nqt) {
-#pragma unroll 8
-                for (int t = 0; t < WG_TILE / 2; ++t) {
-                    const float av = ta[2 * t + mh][mp0 + mci];
-                    macc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, tb[2 * t + mh][mq0 + mci], macc, 0, 0, 0);
-                    mbs += av;
-                }
-            }
-        } else if (pi < p && qi < q) {
-#pragma unroll 8
-            for (int r = 0; r < WG_TILE; ++r) {
-                const float4 av = *reinterpret_cast<const float4*>(&ta[r][pi]);
-                const float4 bv = *reinterpret_cast<const float4*>(&tb[r][qi]);
-                const float a4[4] = {av.x, av.y, av.z, av.w}, b4[4] = {bv.x, bv.y, bv.z, bv.w};
-#pragma unroll
-                for (int x = 0; x < 4; ++x) {
-#pragma unroll
-                    for (int y = 0; y < 4; ++y) acc[x][y] += a4[x] * b4[y];
-                }
-            }
-            if (qi == 0) {  // the bias: this thread's 4 rows of a, summed over the tile
-                for (int r = 0; r < WG_TILE; ++r) {
-#pragma unroll
-                    for (int x = 0; x < 4; ++x) bsum[x] += ta[r][pi + x];
-                }
-            }
-        }
-    }
-    float* out = partial + (size_t)blockIdx.x * row_len;
-    if (D2D_PPO_WGRAD_MFMA == 2) {
+        // wave w: the 32 x 32 output tile (p0, q0); lane l: A[k = l / 32][i = l % 32] = a[row][p0 + i],
+        // B[k][j = l % 32] = b[row][q0 + j], row = 2 t + l / 32
         if (mw < npt * nqt) {
-#pragma unroll
-            for (int v = 0; v < 16; ++v) {
-                const int i = (v & 3) + 8 * (v >> 2) + 4 * mh;  // the C/D map of the 32 x 32 MFMA
-                if (mp0 + i < p && mq0 + mci < q) out[pr.w_off + (mp0 + i) * q + mq0 + mci] = macc[v];
-            }
-            mbs += __shfl_xor(mbs, 32, 64);
-            if (mq0 == 0 && mh == 0 && mp0 + mci < p) out[pr.b_off + mp0 + mci] = mbs;
-        }
-        return;
-    }
-#pragma unroll
-    for (int x = 0; x < 4; ++x) {
-        if (pi + x >= p) continue;
-#pragma unroll
-        for (int y = 0; y < 4; ++y) {
-            if (qi + y < q) out[pr.w_off + (pi + x) * q + qi + y] = acc[x][y];
-        }
-        if (qi == 0) out[pr.b_off + pi + x] = bsum[x];
-    }
-}
-
-// The same problems on the matrix cores: v_mfma_f32_32x32x2_f32 (exact f32 in / f32 accumulate),
-// D[i][j] = sum_k A[i][k] B[k][j] with i = a's column (output unit), j = b's column (input unit),
-// k = the minibatch row.  Wave w of workgroup (c, k) owns one 32 x 32 tile of problem k's output
-// (p, q <= 64: up to 2 x 2 tiles) and steps through the chunk's rows two at a time; lane l loads
-// a[row + l / 32][p0 + l % 32] and b[row + l / 32][q0 + l % 32] (coalesced 128-byte halves).  The
-// q0 == 0 waves also sum their a values for the bias.  Same partial-row layout as wgrad_kernel.
-__global__ __launch_bounds__(256) void wgrad_mfma_kernel(WgradProblems P, int m, int row_len,
-                                                         float* __restrict__ partial) {
-    const WgradProblem& pr = P.k[blockIdx.y];
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const int nqt = (pr.q + 31) / 32, npt = (pr.p + 31) / 32;
-    if (wave >= npt * nqt) return;  // an idle wave (no workgroup barriers below)
-    const int p0 = (wave / nqt) * 32, q0 = (wave % nqt) * 32;
-    const int ci = lane & 31, h = lane >> 5;
-    const bool pa = p0 + ci < pr.p, qb = q0 + ci < pr.q;
-    const int r0 = blockIdx.x * WG_ROWS, r1 = min(m, r0 + WG_ROWS);
-    const float* __restrict__ A = pr.a + p0 + ci;
-    const float* __restrict__ B = pr.b + q0 + ci;
-    f32x16 acc = {};
-    float bs = 0.0f;
 #pragma unroll 8
-    for (int t = 0; t < WG_ROWS / 2; ++t) {  // rows past r1 contribute zeros (the last chunk)
-        const int row = r0 + 2 * t + h;
-        const bool ok = row < r1;
-        const float av = (ok && pa) ? A[(size_t)row * pr.lda] : 0.0f;
-        const float bv = (ok && qb) ? B[(size_t)row * pr.ldb] : 0.0f;
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
-        bs += av;
+            for (int t = 0; t < WG_TILE / 2; ++t) {
+                const float av = ta[2 * t + mh][mp0 + mci];
+                macc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, tb[2 * t + mh][mq0 + mci], macc, 0, 0, 0);
+                mbs += av;
+            }
+        }
     }
     float* out = partial + (size_t)blockIdx.x * row_len;
+    if (mw < npt * nqt) {
 #pragma unroll
-    for (int v = 0; v < 16; ++v) {
-        const int i = (v & 3) + 8 * (v >> 2) + 4 * h;  // the C/D map of the 32 x 32 MFMA
-        if (p0 + i < pr.p && qb) out[pr.w_off + (p0 + i) * pr.q + q0 + ci] = acc[v];
+        for (int v = 0; v < 16; ++v) {
+            const int i = (v & 3) + 8 * (v >> 2) + 4 * mh;  // the C/D map of the 32 x 32 MFMA
+            if (mp0 + i < p && mq0 + mci < q) out[pr.w_off + (mp0 + i) * q + mq0 + mci] = macc[v];
+        }
+        mbs += __shfl_xor(mbs, 32, 64);
+        if (mq0 == 0 && mh == 0 && mp0 + mci < p) out[pr.b_off + mp0 + mci] = mbs;
     }
-    bs += __shfl_xor(bs, 32, 64);  // both row parities
-    if (q0 == 0 && h == 0 && pa) out[pr.b_off + p0 + ci] = bs;
 }
 
 // g[e] = sum over the n_chunks rows of partial[.][e], e < row_len: 64 elements per workgroup, the
@@ -1480,10 +1022,10 @@ __device__ __forceinline__ void wgrad_reduce_body(int n_chunks, int row_len, con
         g[e] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
 }
 
-// ADAM: the fused-Adam instantiation (its registers stay out of the plain reduce's)
-template <bool ADAM>
+// (Clip + Adam as the last-finishing workgroup of this reduce, behind a device ticket and agent-scope
+// fences, measured 0.0403 s per update against 0.0337 s for the separate launch; removed in round 4.)
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(int n_chunks, int row_len, const float* __restrict__ partial,
-                                                           float* __restrict__ g, HeadArgs H, AdamArgs A) {
+                                                           float* __restrict__ g, HeadArgs H) {
     // with H.partial set, the last workgroup finishes the loss head (head_finish_kernel's work) and
     // writes log_std's two gradient slots, which the reduce then leaves alone
     if (H.partial != nullptr && blockIdx.x == gridDim.x - 1) {
@@ -1491,18 +1033,6 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(int n_chunks, int row
     } else {
         wgrad_reduce_body(n_chunks, row_len, partial, g, H);
     }
-    if (!ADAM) return;
-    // ADAM: the workgroup that finishes last runs the clip + Adam step on the whole of g
-    __shared__ int last;
-    __syncthreads();
-    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // the workgroup's g writes
-    if (threadIdx.x == 0)
-        last = __hip_atomic_fetch_add(A.ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1;
-    __syncthreads();
-    if (!last) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // every other workgroup's g writes
-    adam_body_256(A, g);
-    if (threadIdx.x == 0) __hip_atomic_store(A.ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 inline int32_t rc(hipError_t e) { return e == hipSuccess ? 0 : (int32_t)e; }
@@ -1537,31 +1067,16 @@ int32_t d2d_ppo_head_finish(int32_t m, int32_t n_blocks, const float* partial, c
 int32_t d2d_ppo_adam(int32_t n, float* p, float* g, float* m1, float* m2, float* t, float lr, float b1, float b2,
                      float eps, float max_norm, void* stream) {
     if (n <= 0) return 0;
-    if (D2D_PPO_ADAM_SPREAD) {
-        hipLaunchKernelGGL(adam_spread_kernel, dim3((n + ADAM_SLICE - 1) / ADAM_SLICE), dim3(ADAM_WG), 0,
-                           (hipStream_t)stream, n, p, g, m1, m2, t, lr, b1, b2, eps, max_norm, nullptr);
-        hipLaunchKernelGGL(adam_tick_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, t);
-        return rc(hipGetLastError());
-    }
     if (n > ADAM_THREADS * ADAM_PER_THREAD) return (int32_t)hipErrorInvalidValue;
     hipLaunchKernelGGL(adam_kernel, dim3(1), dim3(ADAM_THREADS), 0, (hipStream_t)stream, n, p, g, m1, m2, t, lr, b1,
                        b2, eps, max_norm);
     return rc(hipGetLastError());
 }
 
-int32_t d2d_ppo_adam_spread(int32_t n, float* p, const float* g, float* m1, float* m2, float* t, float lr, float b1,
-                            float b2, float eps, float max_norm, int32_t* ticket, void* stream) {
-    if (n <= 0) return 0;
-    if (ticket == nullptr) return (int32_t)hipErrorInvalidValue;
-    hipLaunchKernelGGL(adam_spread_kernel, dim3((n + ADAM_SLICE - 1) / ADAM_SLICE), dim3(ADAM_WG), 0,
-                       (hipStream_t)stream, n, p, g, m1, m2, t, lr, b1, b2, eps, max_norm, ticket);
-    return rc(hipGetLastError());
-}
-
 static int32_t wgrad_launch(int32_t m, int32_t n_problems, const float* const* a, const int32_t* lda,
                             const float* const* b, const int32_t* ldb, const int32_t* p, const int32_t* q,
                             const int32_t* w_off, const int32_t* b_off, int32_t row_len, float* partial, float* g,
-                            const HeadArgs& H, const AdamArgs& A, void* stream) {
+                            const HeadArgs& H, void* stream) {
     if (m <= 0 || n_problems <= 0) return 0;
     if (n_problems > D2D_PPO_WGRAD_MAX) return (int32_t)hipErrorInvalidValue;
     WgradProblems P{};
@@ -1570,32 +1085,19 @@ static int32_t wgrad_launch(int32_t m, int32_t n_problems, const float* const* a
         P.k[k] = WgradProblem{a[k], b[k], lda[k], ldb[k], p[k], q[k], w_off[k], b_off[k]};
     }
     const int nc = (m + WG_ROWS - 1) / WG_ROWS;
-    if (D2D_PPO_WGRAD_MFMA == 1)
-        hipLaunchKernelGGL(wgrad_mfma_kernel, dim3(nc, n_problems), dim3(256), 0, (hipStream_t)stream, P, m, row_len,
-                           partial);
-    else
-        hipLaunchKernelGGL(wgrad_kernel, dim3(nc, n_problems), dim3(256), 0, (hipStream_t)stream, P, m, row_len,
-                           partial);
+    hipLaunchKernelGGL(wgrad_kernel, dim3(nc, n_problems), dim3(256), 0, (hipStream_t)stream, P, m, row_len, partial);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return (int32_t)e;
     if (H.partial != nullptr && (H.ls_grad < g || H.ls_grad + 2 > g + row_len)) return (int32_t)hipErrorInvalidValue;
-    if (A.p != nullptr && (A.n != row_len || A.ticket == nullptr || A.n > ADAM_THREADS * ADAM_PER_THREAD))
-        return (int32_t)hipErrorInvalidValue;
     const dim3 rgrid((row_len + 63) / 64 + (H.partial != nullptr));
-    if (A.p != nullptr)
-        hipLaunchKernelGGL(wgrad_reduce_kernel<true>, rgrid, dim3(256), 0, (hipStream_t)stream, nc, row_len, partial, g,
-                           H, A);
-    else
-        hipLaunchKernelGGL(wgrad_reduce_kernel<false>, rgrid, dim3(256), 0, (hipStream_t)stream, nc, row_len, partial,
-                           g, H, A);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, rgrid, dim3(256), 0, (hipStream_t)stream, nc, row_len, partial, g, H);
     return rc(hipGetLastError());
 }
 
 int32_t d2d_ppo_wgrad(int32_t m, int32_t n_problems, const float* const* a, const int32_t* lda, const float* const* b,
                       const int32_t* ldb, const int32_t* p, const int32_t* q, const int32_t* w_off,
                       const int32_t* b_off, int32_t row_len, float* partial, float* g, void* stream) {
-    return wgrad_launch(m, n_problems, a, lda, b, ldb, p, q, w_off, b_off, row_len, partial, g, HeadArgs{}, AdamArgs{},
-                        stream);
+    return wgrad_launch(m, n_problems, a, lda, b, ldb, p, q, w_off, b_off, row_len, partial, g, HeadArgs{}, stream);
 }
 
 int32_t d2d_ppo_wgrad_head(int32_t m, int32_t n_problems, const float* const* a, const int32_t* lda,
@@ -1606,22 +1108,7 @@ int32_t d2d_ppo_wgrad_head(int32_t m, int32_t n_problems, const float* const* a,
                            void* stream) {
     if (head_partial == nullptr) return (int32_t)hipErrorInvalidValue;
     const HeadArgs H{m, n_blocks, head_partial, log_std, ent_coef, log_std_grad, acc_pl, acc_vl, acc_ent, acc_clip};
-    return wgrad_launch(m, n_problems, a, lda, b, ldb, p, q, w_off, b_off, row_len, partial, g, H, AdamArgs{}, stream);
-}
-
-int32_t d2d_ppo_wgrad_head_adam(int32_t m, int32_t n_problems, const float* const* a, const int32_t* lda,
-                                const float* const* b, const int32_t* ldb, const int32_t* p, const int32_t* q,
-                                const int32_t* w_off, const int32_t* b_off, int32_t row_len, float* partial, float* g,
-                                int32_t n_blocks, const float* head_partial, const float* log_std, float ent_coef,
-                                float* log_std_grad, float* acc_pl, float* acc_vl, float* acc_ent, float* acc_clip,
-                                float* params, float* m1, float* m2, float* t, float lr, float b1, float b2, float eps,
-                                float max_norm, int32_t* ticket, void* stream) {
-    if (head_partial == nullptr || params == nullptr || m1 == nullptr || m2 == nullptr || t == nullptr ||
-        ticket == nullptr)
-        return (int32_t)hipErrorInvalidValue;
-    const HeadArgs H{m, n_blocks, head_partial, log_std, ent_coef, log_std_grad, acc_pl, acc_vl, acc_ent, acc_clip};
-    const AdamArgs A{row_len, params, m1, m2, t, lr, b1, b2, eps, max_norm, ticket};
-    return wgrad_launch(m, n_problems, a, lda, b, ldb, p, q, w_off, b_off, row_len, partial, g, H, A, stream);
+    return wgrad_launch(m, n_problems, a, lda, b, ldb, p, q, w_off, b_off, row_len, partial, g, H, stream);
 }
 
 int32_t d2d_ppo_wgrad_chunks(int32_t m) { return (m + WG_ROWS - 1) / WG_ROWS; }
@@ -1641,17 +1128,8 @@ int32_t d2d_ppo_mlp_forward_adv(int32_t m, const int64_t* idx, const float* obs,
     if (m <= 0) return 0;
     if (adv != nullptr && ws == nullptr) return (int32_t)hipErrorInvalidValue;
     MlpPair P = make_pair(weights, bufs);
-    if (D2D_PPO_FWD_MFMA) {
-        hipLaunchKernelGGL(mlp_forward_mfma_kernel, dim3((m + FM_TILES * FM_SPB - 1) / (FM_TILES * FM_SPB)), dim3(256), 0,
-                           (hipStream_t)stream, P, m, idx, obs, xg, adv, ws);
-    } else {
-        if (adv != nullptr) {
-            const int32_t e = d2d_ppo_adv_stats(m, idx, adv, ws, stream);
-            if (e != 0) return e;
-        }
-        hipLaunchKernelGGL(mlp_forward_kernel, dim3((m + MLP_SPB - 1) / MLP_SPB, 2), dim3(MLP_BLOCK), 0,
-                           (hipStream_t)stream, P, m, idx, obs, xg);
-    }
+    hipLaunchKernelGGL(mlp_forward_mfma_kernel, dim3((m + FM_TILES * FM_SPB - 1) / (FM_TILES * FM_SPB)), dim3(256), 0,
+                       (hipStream_t)stream, P, m, idx, obs, xg, adv, ws);
     return rc(hipGetLastError());
 }
 
@@ -1728,9 +1206,8 @@ int32_t d2d_ppo_grad_reduce(int32_t n_rows, int32_t row_len, const float* partia
         log_std_grad + 2 > g + row_len)
         return (int32_t)hipErrorInvalidValue;
     const HeadArgs H{m, n_blocks, head_partial, log_std, ent_coef, log_std_grad, acc_pl, acc_vl, acc_ent, acc_clip};
-    const AdamArgs Z{};
-    hipLaunchKernelGGL(wgrad_reduce_kernel<false>, dim3((row_len + 63) / 64 + 1), dim3(256), 0, (hipStream_t)stream,
-                       n_rows, row_len, partial, g, H, Z);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((row_len + 63) / 64 + 1), dim3(256), 0, (hipStream_t)stream,
+                       n_rows, row_len, partial, g, H);
     return rc(hipGetLastError());
 }
 
@@ -1778,13 +1255,7 @@ int32_t d2d_ppo_mlp_backward(int32_t m, const int64_t* idx, const float* act, co
     P.net[0].gout = gout[0];
     P.net[1].gout = gout[1];
     const int nbs = (m + D2D_PPO_HEAD_BLOCK - 1) / D2D_PPO_HEAD_BLOCK;
-    static_assert(FM_TILES * FM_SPB == MLP_SPB, "the matrix-core backward keeps the partial-row count");
-    if (D2D_PPO_BWD_MFMA)
-        hipLaunchKernelGGL(mlp_backward_mfma_kernel, dim3((m + MLP_SPB - 1) / MLP_SPB), dim3(256), 0,
-                           (hipStream_t)stream, P, m, idx, act, old_logp, adv, ret, log_std, ws, nbs, normalize, clip,
-                           vf_coef, partial);
-    else
-        hipLaunchKernelGGL(mlp_backward_kernel, dim3((m + MLP_SPB - 1) / MLP_SPB, 2), dim3(MLP_BLOCK), 0,
+    hipLaunchKernelGGL(mlp_backward_kernel, dim3((m + MLP_SPB - 1) / MLP_SPB, 2), dim3(MLP_BLOCK), 0,
                            (hipStream_t)stream, P, m, idx, act, old_logp, adv, ret, log_std, ws, nbs, normalize, clip,
                            vf_coef, partial);
     return rc(hipGetLastError());

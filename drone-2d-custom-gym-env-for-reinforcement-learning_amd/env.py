@@ -199,7 +199,7 @@ class Drone2dVecEnv:
         self.env_scenario = es  # in curriculum mode: the initial map only (resets redraw on device)
         self._check(self._lib.d2d_set_scenarios(self._h, arr, n_scn, es.ctypes.data_as(C.POINTER(C.c_int32))),
               "d2d_set_scenarios")
-        if not self.cfg.scn_pool and n_scn > 1:  # step costs for the quad workgroups' heavy / light pairing
+        if not self.cfg.scn_pool and n_scn > 1:  # step costs: the grouped layout's co-residency balance
             cost = (C.c_double * n_scn)(*[SCENARIO_STEP_COST.get(s.name.removesuffix("_free"), 32.0)
                                           for s in self.scenarios])
             self._check(self._lib.d2d_set_scenario_costs(self._h, cost, n_scn), "d2d_set_scenario_costs")

@@ -153,13 +153,9 @@ def ppo_native():
             "d2d_ppo_adv_stats": [i32, vp, vp, vp, vp],
             "d2d_ppo_head_finish": [i32, i32, vp, vp, f32, vp, vp, vp, vp, vp, vp],
             "d2d_ppo_adam": [i32, vp, vp, vp, vp, vp, f32, f32, f32, f32, f32, vp],
-            "d2d_ppo_adam_spread": [i32, vp, vp, vp, vp, vp, f32, f32, f32, f32, f32, vp, vp],
             "d2d_ppo_wgrad": [i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp, vp, vp],
             "d2d_ppo_wgrad_head": [i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp, vp,
                                    i32, vp, vp, f32, vp, vp, vp, vp, vp, vp],
-            "d2d_ppo_wgrad_head_adam": [i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, i32, vp, vp,
-                                        i32, vp, vp, f32, vp, vp, vp, vp, vp,
-                                        vp, vp, vp, vp, f32, f32, f32, f32, f32, vp, vp],
             "d2d_ppo_wgrad_chunks": [i32],
             "d2d_ppo_mlp_forward": [i32, vp, vp, vp, vp, vp, vp],
             "d2d_ppo_mlp_forward_adv": [i32, vp, vp, vp, vp, vp, vp, vp, vp],
@@ -174,7 +170,7 @@ def ppo_native():
         for name, args in sig.items():
             fn = getattr(lib, name)
             fn.restype, fn.argtypes = C.c_int32, args
-        if lib.d2d_ppo_abi_version() != 5:
+        if lib.d2d_ppo_abi_version() != 6:
             raise RuntimeError("libd2d_ppo.so ABI mismatch")
         _PPO_LIB = lib
     return _PPO_LIB
@@ -227,15 +223,8 @@ class ManualStep:
         # the fused element-wise kernels on a GPU (libd2d_ppo.so, loud if missing); torch ops on CPU
         self.lib = ppo_native() if torch.device(device).type == "cuda" else None
         self._bufs = {}  # minibatch size -> (work buffers, partial rows) of the HIP path
-        # D2D_PPO_FUSE_ADAM=1 (single rank): Adam runs as the gradient reduce's last workgroup
-        # (d2d_ppo_wgrad_head_adam) instead of its own d2d_ppo_adam launch; bit-identical results, off
-        # by default (slower as measured, see DESIGN.md "PPO update")
         import os
 
-        self.fuse_adam = self.lib is not None and os.environ.get("D2D_PPO_FUSE_ADAM", "0") == "1"
-        self._ticket = torch.zeros(1, dtype=torch.int32, device=device) if self.lib is not None else None
-        # D2D_PPO_ADAM_SPREAD=1: the Adam step over ~11 workgroups (d2d_ppo_adam_spread) instead of one
-        self.adam_spread = self.lib is not None and os.environ.get("D2D_PPO_ADAM_SPREAD", "0") == "1"
         # D2D_PPO_FUSED=1 (default): forward + backward + weight gradients in one launch
         # (d2d_ppo_fused_grad) + the reduce; 0: the separate kernels (forward, backward, wgrad + reduce)
         self.fused = self.lib is not None and os.environ.get("D2D_PPO_FUSED", "1") == "1"
@@ -248,9 +237,6 @@ class ManualStep:
             o += k
 
     def step(self, idx, rollout, acc: dict, world: int = 1, adv_ws=None):
-        if self.fuse_adam and world == 1 and not self.fused:
-            self._grad_hip(idx, rollout, acc, adam=True)  # gradient + clip + Adam, no exchange between
-            return
         self.grad(idx, rollout, acc, adv_ws)
         self.apply(world)
 
@@ -290,7 +276,7 @@ class ManualStep:
             _wgrad(a, b, lin.weight.grad)
             torch.sum(a, 0, out=lin.bias.grad)
 
-    def _grad_hip(self, idx, rollout, acc, adam: bool = False):
+    def _grad_hip(self, idx, rollout, acc):
         """libd2d_ppo.so: advantage statistics, both MLPs forward (four threads per sample and net),
         loss head + backward to the hidden-layer gradients, all weight / bias gradients, log_std's."""
         import ctypes as C
@@ -334,7 +320,7 @@ class ManualStep:
         head = (prow, hb["partial"].data_ptr(), ls.data_ptr(), cfg.ent_coef, ls.grad.data_ptr(),
                 acc["policy_loss"].data_ptr(), acc["value_loss"].data_ptr(), acc["entropy"].data_ptr(),
                 acc["clip_fraction"].data_ptr())
-        self._wgrad_hip(M, layers, hb["wpart"], head, adam)
+        self._wgrad_hip(M, layers, hb["wpart"], head)
 
     def _grad_fused(self, idx, rollout, acc, adv_ws=None):
         """libd2d_ppo.so, two launches (+ the advantage statistics unless ``adv_ws`` points at this
@@ -392,10 +378,9 @@ class ManualStep:
     def _tanh_grad_torch(h, g):
         return g.mul_(1.0 - h * h)
 
-    def _wgrad_hip(self, M, layers, wpart, head=None, adam: bool = False):
+    def _wgrad_hip(self, M, layers, wpart, head=None):
         """All six weight / bias gradients in one libd2d_ppo.so launch (+ its reduce) into G; with
-        `head` (d2d_ppo_head_finish's arguments after m) the reduce launch also finishes the head, and
-        with `adam` its last workgroup also runs apply()'s clip + Adam step (single rank)."""
+        `head` (d2d_ppo_head_finish's arguments after m) the reduce launch also finishes the head."""
         import ctypes as C
 
         row_len = self.G.numel()  # all of G: log_std's slots (no problem covers them) are rewritten after
@@ -416,13 +401,6 @@ class ManualStep:
         if head is None:
             _ok(self.lib.d2d_ppo_wgrad(M, n, a_p, lda, b_p, ldb, pp, qq, wo, bo, row_len, wpart.data_ptr(), base,
                                        self._stream()), "d2d_ppo_wgrad")
-        elif adam:
-            cfg = self.cfg
-            _ok(self.lib.d2d_ppo_wgrad_head_adam(M, n, a_p, lda, b_p, ldb, pp, qq, wo, bo, row_len, wpart.data_ptr(),
-                                                 base, *head, self.P.data_ptr(), self.m.data_ptr(),
-                                                 self.v.data_ptr(), self.t.data_ptr(), cfg.learning_rate, 0.9, 0.999,
-                                                 1e-5, cfg.max_grad_norm, self._ticket.data_ptr(), self._stream()),
-                "d2d_ppo_wgrad_head_adam")
         else:
             _ok(self.lib.d2d_ppo_wgrad_head(M, n, a_p, lda, b_p, ldb, pp, qq, wo, bo, row_len, wpart.data_ptr(), base,
                                             *head, self._stream()), "d2d_ppo_wgrad_head")
@@ -463,12 +441,6 @@ class ManualStep:
         if world > 1:
             dist.all_reduce(G)  # data-parallel PPO: mean gradient over the ranks (RCCL)
             G.div_(world)
-        if self.lib is not None and self.adam_spread:
-            _ok(self.lib.d2d_ppo_adam_spread(G.numel(), self.P.data_ptr(), G.data_ptr(), self.m.data_ptr(),
-                                             self.v.data_ptr(), self.t.data_ptr(), cfg.learning_rate, 0.9, 0.999,
-                                             1e-5, cfg.max_grad_norm, self._ticket.data_ptr(), self._stream()),
-                "d2d_ppo_adam_spread")
-            return
         if self.lib is not None:
             _ok(self.lib.d2d_ppo_adam(G.numel(), self.P.data_ptr(), G.data_ptr(), self.m.data_ptr(),
                                       self.v.data_ptr(), self.t.data_ptr(), cfg.learning_rate, 0.9, 0.999, 1e-5,

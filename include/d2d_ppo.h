@@ -17,7 +17,7 @@
 extern "C" {
 #endif
 
-#define D2D_PPO_ABI_VERSION 5
+#define D2D_PPO_ABI_VERSION 6  /* v6 (round 4): d2d_ppo_adam_spread / d2d_ppo_wgrad_head_adam removed */
 #define D2D_PPO_HEAD_BLOCK 64  /* v1: 256 */
 
 int32_t d2d_ppo_abi_version(void);
@@ -37,17 +37,9 @@ int32_t d2d_ppo_head_finish(int32_t m, int32_t n_blocks, const float* partial, c
 /* clip_grad_norm_(max_norm) then one torch.optim.Adam step (betas b1, b2, eps; bias corrections
  * from the step counter *t, which is incremented) over n parameters p with gradients g and
  * moments m1, m2; g is clipped in place, as torch clips .grad.  One workgroup, n <= 16 384 (the
- * policy has ~10 k parameters).  Built with D2D_PPO_ADAM_SPREAD=1: ceil(n / 1024) workgroups, each
- * computing the full norm, then a one-thread launch increments *t, any n, g left unclipped. */
+ * policy has ~10 k parameters). */
 int32_t d2d_ppo_adam(int32_t n, float* p, float* g, float* m1, float* m2, float* t, float lr, float b1, float b2,
                      float eps, float max_norm, void* stream);
-
-/* d2d_ppo_adam's step over ceil(n / 1024) workgroups in one launch, any n: every workgroup computes
- * the full gradient norm itself and updates its slice; the last one to finish (device counter
- * `ticket`, one int32 initialised to 0, reset to 0 by that workgroup) advances *t.  g is left
- * unclipped.  Same arithmetic as d2d_ppo_adam except the norm's summation order.  Added in ABI v3. */
-int32_t d2d_ppo_adam_spread(int32_t n, float* p, const float* g, float* m1, float* m2, float* t, float lr, float b1,
-                            float b2, float eps, float max_norm, int32_t* ticket, void* stream);
 
 /* Weight and bias gradients of up to D2D_PPO_WGRAD_MAX linear layers in one launch (+ one reduce):
  * for problem k, g[w_off[k] + i q + j] = sum_r a_k[r][i] b_k[r][j] (i < p[k], j < q[k]; rows r < m;
@@ -68,21 +60,6 @@ int32_t d2d_ppo_wgrad_head(int32_t m, int32_t n_problems, const float* const* a,
                            int32_t n_blocks, const float* head_partial, const float* log_std, float ent_coef,
                            float* log_std_grad, float* acc_pl, float* acc_vl, float* acc_ent, float* acc_clip,
                            void* stream);
-/* d2d_ppo_wgrad_head and d2d_ppo_adam in one launch (single-rank training: no gradient exchange
- * between the two).  Whichever reduce workgroup finishes last (a device counter `ticket`, one
- * int32 initialised to 0, which that workgroup resets to 0) runs the clip + Adam step over
- * params[0 .. row_len) with g = the reduced gradient; same arithmetic and summation order as
- * d2d_ppo_adam, so results are bit-identical to the two-call sequence.  row_len <= 16 384.  Added in
- * ABI v3.  Measured slower than the two calls on MI355X (0.0403 vs 0.0337 s per 65 536-env update):
- * the cross-workgroup hand-off needs an L2 write-back / invalidate (agent-scope fences) and the
- * 256-thread Adam is load-latency bound, so drone2d_amd.ppo uses it only with D2D_PPO_FUSE_ADAM=1. */
-int32_t d2d_ppo_wgrad_head_adam(int32_t m, int32_t n_problems, const float* const* a, const int32_t* lda,
-                                const float* const* b, const int32_t* ldb, const int32_t* p, const int32_t* q,
-                                const int32_t* w_off, const int32_t* b_off, int32_t row_len, float* partial, float* g,
-                                int32_t n_blocks, const float* head_partial, const float* log_std, float ent_coef,
-                                float* log_std_grad, float* acc_pl, float* acc_vl, float* acc_ent, float* acc_clip,
-                                float* params, float* m1, float* m2, float* t, float lr, float b1, float b2, float eps,
-                                float max_norm, int32_t* ticket, void* stream);
 int32_t d2d_ppo_wgrad_chunks(int32_t m);
 
 /* The two MLPs (policy 27-64-64-2, value 27-64-64-1, tanh) per minibatch sample, four threads per

@@ -173,8 +173,8 @@ int32_t d2d_set_scenarios(d2d_t* h, const d2d_scn* scns, int32_t n_scn, const in
 /* Relative step cost of each scenario of the last d2d_set_scenarios (test mode; default 1.0 each).
  * With a grouped layout (several scenarios), the groups are renumbered so that the workgroups that
  * share a CU carry a balanced load (d2d_get_group_layout; the state moves along, cached reset
- * observations are recomputed, d2d_generation changes); the optional quad workgroups (D2D_QUAD=1)
- * pair heavy and light scenarios by these weights.  Placement only: results do not depend on it.
+ * observations are recomputed, d2d_generation changes).  Placement only: results do not depend
+ * on it.
  * Synchronises. */
 int32_t d2d_set_scenario_costs(d2d_t* h, const double* cost, int32_t n_scn);
 

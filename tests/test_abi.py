@@ -231,7 +231,7 @@ def test_ppo_library_exports_every_header_symbol(d2):
     for f in fns:
         assert hasattr(lib, f), f
         assert getattr(lib, f).argtypes is not None, f  # declared in ppo_native's signatures
-    assert lib.d2d_ppo_abi_version() == 5
+    assert lib.d2d_ppo_abi_version() == 6
     assert b"gfx950" in open(_build.PPO_OUT, "rb").read()
     # v4: the shuffles and the fused rollout step check their arguments before any launch
     assert lib.d2d_ppo_permute(0, 3, 1, None, None, None) == 0
@@ -248,8 +248,4 @@ def test_ppo_library_exports_every_header_symbol(d2):
     ptr = (C.c_void_p * 1)(None)
     assert lib.d2d_ppo_wgrad(64, 1, ptr, one, ptr, one, one, one, one, one, 100, None, None, None) == 1
     assert lib.d2d_ppo_wgrad(0, 1, ptr, one, ptr, one, one, one, one, one, 100, None, None, None) == 0
-    assert lib.d2d_ppo_adam_spread(64, None, None, None, None, None, 1e-3, 0.9, 0.999, 1e-5, 0.5, None, None) == 1
-    # the fused Adam needs its parameter / moment / ticket buffers (refused before any launch)
-    assert lib.d2d_ppo_wgrad_head_adam(64, 1, ptr, one, ptr, one, one, one, one, one, 100, None, None, 1, None,
-                                       None, 0.0, None, None, None, None, None, None, None, None, None, 1e-3,
-                                       0.9, 0.999, 1e-5, 0.5, None, None) == 1
+

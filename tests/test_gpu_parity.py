@@ -72,26 +72,6 @@ def test_vs_oracle_teacher_forced(d2, scn, n):
     venv.close()
 
 
-@pytest.mark.parametrize("scn", ["corridor", "mixed", "S_corridor"])
-def test_quad_workgroups_vs_oracle(d2, scn, monkeypatch):
-    """The quad-workgroup step kernel (4 groups x 4 roles in one 1 024-thread workgroup; an option,
-    D2D_QUAD=1, off by default) in parity with the oracle, teacher-forced with
-    auto-resets: identity layout (one scenario) and the scenario-grouped layout (mixed, with groups
-    straddling two scenarios and heavy / light pairs)."""
-    monkeypatch.setenv("D2D_QUAD", "1")
-    scenarios = SCENARIOS if scn == "mixed" else [scn]
-    n = 2048 + 4 * 64 + 37  # ragged: a partly empty last quad
-    venv, orc = make_pair(d2, n, scenarios, seed=41, kwargs=_cfgkw())
-    rng = np.random.default_rng(8)
-    dones = 0
-    for t in range(100):
-        act = np.clip(rng.normal(0.0, 0.6, (n, 2)), -1, 1).astype(np.float32)
-        compare_step(venv, orc, act)
-        dones += int(orc.term.sum())
-    assert dones > 30
-    venv.close()
-
-
 def test_balanced_mixed_layout_full_size(d2):
     """65 536 mixed envs (BASELINE configs[4] per GPU): the layout in use is the host's co-residency
     balanced renumbering for this device's CU count (d2d_balanced_group_layout), not the natural
@@ -396,16 +376,14 @@ def test_device_math_selftest(d2, which):
     assert bad.value == 0
 
 
-@pytest.mark.parametrize("quad", ["0", "1"])
-def test_closest_point_grid_bitwise(d2, quad, monkeypatch):
+def test_closest_point_grid_bitwise(d2):
     """Brent closest-point search over the whole plane and around every path, all 7 scenarios:
     the golden-march tables (golden-left / golden-right prefixes, resume at the first differing
     step) must give exactly the probe sequence of the plain search, so the closest / lookahead
-    points (obs 19..22) and the accumulated path error are bit-identical to the C oracle.  Both step
-    kernels: the 256-thread groups and the quad workgroups (staged tables of seven scenarios)."""
+    points (obs 19..22) and the accumulated path error are bit-identical to the C oracle (grouped
+    layout: every 64-env group stages its scenario and probe table)."""
     from drone2d_amd import abi
 
-    monkeypatch.setenv("D2D_QUAD", quad)
     per = 8192
     n = per * len(SCENARIOS)
     venv, orc = make_pair(d2, n, SCENARIOS, seed=5, kwargs=_cfgkw(), env_scenario=np.repeat(np.arange(7), per),

@@ -173,74 +173,6 @@ def test_manual_step_hip_matches_autograd(d2, M):
 
 
 @pytest.mark.gpu
-def test_fused_adam_matches_separate_launch(d2):
-    """d2d_ppo_wgrad_head_adam (Adam as the gradient reduce's last workgroup) against the separate
-    d2d_ppo_adam launch: parameters, moments, step counter, clipped gradient and loss statistics bit
-    for bit over consecutive minibatches of different sizes (the device ticket resets itself)."""
-    from drone2d_amd.ppo import ActorCritic, ManualStep, PPOConfig
-
-    torch.manual_seed(3)
-    base = ActorCritic()
-    cfg = PPOConfig()
-    g = torch.Generator().manual_seed(5)
-    T = 40000
-    rollout = tuple(t.cuda() for t in (torch.randn(T, 27, generator=g) * 0.5, torch.randn(T, 2, generator=g),
-                                       torch.randn(T, generator=g) - 3.0, torch.randn(T, generator=g),
-                                       torch.randn(T, generator=g) * 3))
-    runs = []
-    for fuse in (False, True):
-        pol = ActorCritic()
-        pol.load_state_dict(base.state_dict())
-        step = ManualStep(pol.cuda(), cfg, "cuda")
-        step.fuse_adam, step.fused = fuse, False  # the fused Adam rides on the separate gradient kernels
-        acc = {k: torch.zeros((), device="cuda") for k in ("policy_loss", "value_loss", "entropy", "clip_fraction")}
-        gi = torch.Generator().manual_seed(7)
-        with torch.no_grad():
-            for M in (32768, 1000, 64, 32768, 7232):
-                step.step(torch.randperm(T, generator=gi)[:M].cuda(), rollout, acc)
-        torch.cuda.synchronize()
-        assert int(step._ticket.item()) == 0
-        runs.append([step.P, step.m, step.v, step.t, step.G] + [acc[k] for k in sorted(acc)])
-    assert float(runs[0][3]) == 5.0
-    for a, b in zip(*runs):
-        assert torch.equal(a, b)
-
-
-@pytest.mark.gpu
-def test_spread_adam_matches_one_workgroup(d2):
-    """d2d_ppo_adam_spread (the Adam step over ~11 workgroups, step counter advanced by the last one
-    through a device ticket) against d2d_ppo_adam over consecutive minibatches: same step count,
-    parameters and moments equal up to the norm's summation order."""
-    from drone2d_amd.ppo import ActorCritic, ManualStep, PPOConfig
-
-    torch.manual_seed(4)
-    base = ActorCritic()
-    cfg = PPOConfig()
-    g = torch.Generator().manual_seed(6)
-    T = 40000
-    rollout = tuple(t.cuda() for t in (torch.randn(T, 27, generator=g) * 0.5, torch.randn(T, 2, generator=g),
-                                       torch.randn(T, generator=g) - 3.0, torch.randn(T, generator=g),
-                                       torch.randn(T, generator=g) * 3))
-    runs = []
-    for spread in (False, True):
-        pol = ActorCritic()
-        pol.load_state_dict(base.state_dict())
-        step = ManualStep(pol.cuda(), cfg, "cuda")
-        step.fuse_adam, step.adam_spread = False, spread
-        acc = {k: torch.zeros((), device="cuda") for k in ("policy_loss", "value_loss", "entropy", "clip_fraction")}
-        gi = torch.Generator().manual_seed(8)
-        with torch.no_grad():
-            for M in (32768, 1000, 64, 32768, 7232):
-                step.step(torch.randperm(T, generator=gi)[:M].cuda(), rollout, acc)
-        torch.cuda.synchronize()
-        assert int(step._ticket.item()) == 0
-        assert float(step.t) == 5.0
-        runs.append((step.P.cpu(), step.m.cpu(), step.v.cpu()))
-    for a, b in zip(*runs):
-        torch.testing.assert_close(a, b, rtol=1e-4, atol=1e-6)
-
-
-@pytest.mark.gpu
 def test_rollout_graph_matches_eager(d2):
     """The captured rollout (policy + env step + GAE replayed as one HIP graph) fills the same
     buffers as the eager loop, bit for bit, over three consecutive rollouts."""

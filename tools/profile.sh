@@ -28,6 +28,10 @@ step kt_eager 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$O
 step pmc_fetch 600 rocprofv3 $KR -T --output-format csv -d "$OUT/pmc_fetch" -o fetch --pmc FETCH_SIZE -- $B --eager --steps 40 --warmup 300
 step pmc_write 600 rocprofv3 $KR -T --output-format csv -d "$OUT/pmc_write" -o write --pmc WRITE_SIZE -- $B --eager --steps 40 --warmup 300
 step pmc_sq 600 rocprofv3 $KR -T --output-format csv -d "$OUT/pmc_sq" -o sq --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_ANY -- $B --eager --steps 40 --warmup 300
+# the VALU instruction mix (fp64 FMA / ADD / MUL / TRANS vs 32-bit int / conversions) and the fp64 flop
+# counters: the fp64 co-roofline of the bench line (tools/valu.py --mix)
+step pmc_mix 600 rocprofv3 $KR -T --output-format csv -d "$OUT/pmc_mix" -o mix --pmc SQ_INSTS_VALU SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT -- $B --eager --steps 40 --warmup 300
+step pmc_mix2 600 rocprofv3 $KR -T --output-format csv -d "$OUT/pmc_mix2" -o mix2 --pmc SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_FLOPS_FP64_TRANS SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_SALU SQ_WAVES -- $B --eager --steps 40 --warmup 300
 step pmc_clk 600 rocprofv3 $KR -T --output-format csv -d "$OUT/pmc_clk" -o clk --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES -- $B --eager --steps 40 --warmup 300
 python3 "$R/tools/traffic.py" "$OUT" --out "$OUT/traffic.json"
-python3 "$R/tools/valu.py" "$OUT"/pmc_sq/sq_counter_collection.csv --out "$OUT/valu.json"
+python3 "$R/tools/valu.py" "$OUT"/pmc_sq/sq_counter_collection.csv --mix "$OUT"/pmc_mix/mix_counter_collection.csv "$OUT"/pmc_mix2/mix2_counter_collection.csv --out "$OUT/valu.json"

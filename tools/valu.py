@@ -22,11 +22,16 @@ def main():
     ap.add_argument("csv")
     ap.add_argument("--kernel", default="d2d_step_kernel")
     ap.add_argument("--out", required=True)
+    ap.add_argument("--mix", nargs="*", default=[],
+                    help="counter CSVs of the VALU-mix passes (tools/profile.sh pmc_mix, pmc_mix2)")
+    ap.add_argument("--envs", type=int, default=65536, help="envs per launch (per-env-step figures)")
+    ap.add_argument("--commit", default=None, help="the commit the profile was taken on")
     a = ap.parse_args()
     per = defaultdict(lambda: defaultdict(float))
-    for r in csv.DictReader(open(a.csv)):
-        if a.kernel in r["Kernel_Name"]:
-            per[r["Counter_Name"]][r["Dispatch_Id"]] += float(r["Counter_Value"])
+    for f in [a.csv, *a.mix]:
+        for r in csv.DictReader(open(f)):
+            if a.kernel in r["Kernel_Name"]:
+                per[r["Counter_Name"]][(f, r["Dispatch_Id"])] += float(r["Counter_Value"])
     med = {k: statistics.median(v.values()) / SIMDS for k, v in per.items()}
     # SQ_WAVE_CYCLES and SQ_ACTIVE_INST_VALU count in units of 4 cycles (quad-cycles); SQ_WAVE_CYCLES
     # sums the lifetimes of the SIMD's waves
@@ -37,6 +42,26 @@ def main():
            "valu_insts_per_simd": med["SQ_INSTS_VALU"], "valu_active_cycles_per_simd": active,
            "wave_lifetime_cycles": life, "valu_busy_frac": active / life,
            "note": "per SIMD per launch, median over dispatches; busy = VALU-issue cycles / wave lifetime"}
+    if a.commit:
+        out["commit"] = a.commit
+    if a.mix:
+        # wave-instructions per SIMD per launch by class; each wave instruction covers 64 lanes
+        cls = ["FMA_F64", "ADD_F64", "MUL_F64", "TRANS_F64", "INT32", "INT64", "CVT",
+               "FMA_F32", "ADD_F32", "MUL_F32", "TRANS_F32"]
+        mix = {c: med.get("SQ_INSTS_VALU_" + c) for c in cls if ("SQ_INSTS_VALU_" + c) in med}
+        tot = med["SQ_INSTS_VALU"]
+        mix["other"] = tot - sum(v for v in mix.values() if v is not None)
+        per_env = SIMDS * 64.0 / a.envs  # wave-instructions per SIMD -> lane-instructions per env-step
+        f64 = 2.0 * mix["FMA_F64"] + mix["ADD_F64"] + mix["MUL_F64"]
+        out["mix_per_simd"] = mix
+        out["mix_frac"] = {c: v / tot for c, v in mix.items()}
+        out["fp64_flops_per_env_step_issued"] = f64 * per_env  # (2 FMA + ADD + MUL) x 64 lanes / env
+        out["fp64_trans_per_env_step"] = mix["TRANS_F64"] * per_env
+        if "SQ_INSTS_VALU_FLOPS_FP64" in med:
+            # the hardware's own flop counter (exec-masked lanes)
+            out["fp64_flops_per_env_step_counter"] = med["SQ_INSTS_VALU_FLOPS_FP64"] * SIMDS / a.envs
+        out["salu_per_simd"] = med.get("SQ_INSTS_SALU")
+        out["mix_sources"] = a.mix
     json.dump(out, open(a.out, "w"), indent=1)
     print(json.dumps(out, indent=1))
 
