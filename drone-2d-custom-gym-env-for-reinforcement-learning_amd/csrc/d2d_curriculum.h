@@ -178,7 +178,8 @@ __device__ inline void gen_gradient(const d2d_scn& s, double u, double& gx, doub
 
 // generate_obstacles_around_path (obstacles.py:58-89): appends up to n circles (the reference's
 // `while num_obstacles < n` with a real-valued n), rejection on |offset| <= size + 10 off the path
-__device__ inline void gen_obstacles(GenRng& R, const Scn& S, d2d_scn& s, double n, double mean, double std, bool on_path) {
+template <typename Rng>
+__device__ inline void gen_obstacles(Rng& R, const Scn& S, d2d_scn& s, double n, double mean, double std, bool on_path) {
     const double L = s.us[s.n_wps - 1];
     int num = 0, tries = 0;
     while ((double)num < n && s.n_circles < D2D_MAX_CIRCLES && tries < 4096) {
@@ -280,6 +281,258 @@ __device__ inline void gen_curriculum(const d2d_curriculum& c, double W, double 
     }
     for (int k = s.n_circles; k < D2D_MAX_CIRCLES; ++k) s.cx[k] = s.cy[k] = s.cr[k] = 0.0;
     scn_build(s, S);
+}
+
+
+// ------------------------------------------------------------------ wave-cooperative generation (K5)
+// The same scenario as gen_curriculum, built by the 64 lanes of one wave in LDS: the stream's first
+// GEN_WIN words (64 Philox blocks, one per lane), the azimuths' sincos, the segment lengths, the 20
+// QPMI2D 3 x 3 solves and the 16 interval records in parallel; the few truly sequential parts (the
+// waypoint and arc-length prefix sums, the obstacle rejection loop, which consumes a data-dependent
+// number of draws) on lane 0 reading the stream from LDS.  Every value is produced by the same
+// operations on the same operands as gen_curriculum (so the tables stay bit-identical to the CPU
+// oracle's o_gen_curriculum); only the order in which independent values are computed changes.
+constexpr int GEN_WIN = 256;   // stream words precomputed per item (corner + waypoints + ~25 obstacle tries)
+
+// serial reader of one (seed, gid, key) stream: words below GEN_WIN from the LDS window, later blocks
+// computed on demand (the same block formula as GenRng)
+struct GenStream {
+    const uint32_t* win;
+    uint32_t gid, key, k0, k1;
+    int pos, bufblk;
+    uint32_t buf[4];
+    __device__ void init(const uint32_t* w, uint64_t seed, uint32_t g, uint32_t k, int p0) {
+        win = w;
+        gid = g;
+        key = k;
+        k0 = (uint32_t)seed;
+        k1 = (uint32_t)(seed >> 32);
+        pos = p0;
+        bufblk = -1;
+    }
+    __device__ uint32_t next32() {
+        const int p = pos++;
+        if (p < GEN_WIN) return win[p];
+        const int b = p >> 2;
+        if (b != bufblk) {
+            philox(gid, key, GEN_TAG + (uint32_t)b, 0u, k0, k1, buf);
+            bufblk = b;
+        }
+        return buf[p & 3];
+    }
+    __device__ double u01() {
+        const uint32_t a = next32(), b = next32();
+        return u53(a, b);
+    }
+    __device__ double uniform(double lo, double hi) { return lo + (hi - lo) * u01(); }
+    __device__ double normal(double mean, double std) {
+        double x1, x2, r2;
+        int guard = 0;
+        do {
+            x1 = 2.0 * u01() - 1.0;
+            x2 = 2.0 * u01() - 1.0;
+            r2 = x1 * x1 + x2 * x2;
+        } while ((r2 >= 1.0 || r2 == 0.0) && ++guard < 64);
+        const double f = sqrt(-2.0 * d2d_pm_log(r2) / r2);
+        return mean + std * (f * x2);
+    }
+};
+__device__ __forceinline__ double win_u01(const uint32_t* w, int p) { return u53(w[p], w[p + 1]); }
+
+// scn_build with interval n on lane n and circle k on lane k (scalars and r_uniform on lane 0)
+__device__ inline void scn_build_lanes(const d2d_scn& a, Scn& s, int lane) {
+    const int nw = a.n_wps, nseg = nw - 2;
+    if (lane < D2D_MAX_WPS) {
+        const int n = lane;
+#if D2D_REC_RM != 1
+        s.us_[n] = (n < nw) ? a.us[n] : __builtin_inf();
+#endif
+#if D2D_REC_RM
+        s.rec_[n][REC_N] = 0.0;
+#endif
+        const int b = (n < nseg - 1) ? n : nseg - 1;
+        const int q = (n == 0) ? nseg - 1 : ((n - 1 < nseg - 1) ? n - 1 : nseg - 1);
+        const double v[REC_N] = {a.xa[b], a.xb[b], a.xc[b], a.ya[b], a.yb[b], a.yc[b],
+                                 a.xa[q], a.xb[q], a.xc[q], a.ya[q], a.yb[q], a.yc[q], 0.0, 0.0, 0.0};
+        for (int f = 0; f < REC_N; ++f) SREC(s, f, n) = v[f];
+        const int n1 = (n + 1 < D2D_MAX_WPS) ? n + 1 : D2D_MAX_WPS - 1;
+        const double u0 = (n < nw) ? a.us[n] : __builtin_inf(), u1 = (n1 < nw) ? a.us[n1] : __builtin_inf();
+        SREC(s, REC_U0, n) = u0;
+        SREC(s, REC_U1, n) = u1;
+        SREC(s, REC_IDU, n) = 1.0 / (u1 - u0);
+        const double us0 = a.us[0];  // (nw >= 3: us[0] and us[nw - 2] are real knots)
+        const double last_lo = a.us[nw - 2] - 0.001;
+        SREC(s, REC_T, n) = (n == 0) ? (us0 < last_lo ? us0 : last_lo) : (n < nw - 1 ? last_lo : -__builtin_inf());
+    }
+    if (lane < D2D_MAX_CIRCLES) {
+        s.cx[lane] = a.cx[lane];
+        s.cy[lane] = a.cy[lane];
+        s.cr[lane] = a.cr[lane];
+    }
+    if (lane == 0) {
+        s.n_wps = nw;
+        s.n_circles = a.n_circles;
+        s.wp_last_x = a.wp_last_x;
+        s.wp_last_y = a.wp_last_y;
+        s.spawn_xmin = a.spawn_xmin;
+        s.spawn_xmax = a.spawn_xmax;
+        s.spawn_ymin = a.spawn_ymin;
+        s.spawn_ymax = a.spawn_ymax;
+        s.spawn_amin = a.spawn_amin;
+        s.spawn_amax = a.spawn_amax;
+        s.r_uniform = __builtin_nan("");
+        if (a.n_circles > 0) {
+            bool same = true;
+            for (int k = 1; k < a.n_circles; ++k) same = same && (a.cr[k] == a.cr[0]);
+            if (same) s.r_uniform = a.cr[0];
+        }
+    }
+}
+
+// Per-item LDS of the wave generator.
+struct GenLds {
+    d2d_scn a;                 // the ABI record being built
+    Scn s;                     // its device form (obstacle placement, tables)
+    uint32_t win[GEN_WIN];     // the stream's first GEN_WIN words
+    double wx[D2D_MAX_WPS], wy[D2D_MAX_WPS], sa[D2D_MAX_WPS], ca[D2D_MAX_WPS], seg[D2D_MAX_WPS];
+};
+
+// one curriculum reset by the calling wave (all 64 lanes, wave-uniform arguments); the result is in
+// G.a / G.s (LDS).  Same draws and arithmetic as gen_curriculum.
+__device__ inline void gen_curriculum_wave(const d2d_curriculum& c, double W, double H, uint64_t seed, uint32_t gid,
+                                           uint32_t key, double sim, GenLds& G, int lane) {
+    {
+        uint32_t o[4];
+        philox(gid, key, GEN_TAG + (uint32_t)lane, 0u, (uint32_t)seed, (uint32_t)(seed >> 32), o);
+        for (int k = 0; k < 4; ++k) G.win[4 * lane + k] = o[k];
+    }
+    __syncthreads();
+    // stream positions (words) of the fixed-count draws: corner (random.randint), wx0, wy0, azimuths
+    int p = 0;
+    int corner = 2;
+    if (c.random_path_spawn) {
+        const int a0 = c.corner_lo, b0 = c.corner_hi;
+        const int k = (int)(win_u01(G.win, p) * (double)(b0 - a0 + 1));
+        corner = a0 + (k < b0 - a0 ? k : b0 - a0);
+        p += 2;
+    }
+    const int nw = c.n_wps < 3 ? 3 : (c.n_wps > D2D_MAX_WPS ? D2D_MAX_WPS : c.n_wps);
+    double lo, hi, x0lo, x0hi, y0lo, y0hi;
+    if (corner == 1) {
+        x0lo = 100.0; x0hi = 180.0; y0lo = 100.0; y0hi = 180.0; lo = 0.0; hi = PI / 2.0;
+    } else if (corner == 3) {
+        x0lo = 100.0; x0hi = 180.0; y0lo = H - 180.0; y0hi = H - 100.0; lo = 0.0; hi = -PI / 2.0;
+    } else if (corner == 4) {
+        x0lo = W - 180.0; x0hi = W - 100.0; y0lo = H - 180.0; y0hi = H - 100.0; lo = -PI / 2.0; hi = -PI;
+    } else {
+        x0lo = W - 180.0; x0hi = W - 100.0; y0lo = 100.0; y0hi = 180.0; lo = PI / 2.0; hi = PI;
+    }
+    const int paz = p + 4;  // azimuth i at paz + 2 i
+    if (lane < nw - 1) {
+        const double az = lo + (hi - lo) * win_u01(G.win, paz + 2 * lane);
+        double sa, ca;
+        d2d_pm_sincos(az, &sa, &ca);
+        G.sa[lane] = sa;
+        G.ca[lane] = ca;
+    }
+    __syncthreads();
+    if (lane == 0) {
+        G.wx[0] = x0lo + (x0hi - x0lo) * win_u01(G.win, p);
+        G.wy[0] = y0lo + (y0hi - y0lo) * win_u01(G.win, p + 2);
+        for (int i = 0; i + 1 < nw; ++i) {
+            G.wx[i + 1] = G.wx[i] + c.segment_length * G.ca[i];
+            G.wy[i + 1] = G.wy[i] + c.segment_length * G.sa[i];
+        }
+    }
+    __syncthreads();
+    // gen_fit: segment lengths (lanes), arc length prefix sum (lane 0), the fits (lanes)
+    d2d_scn& s = G.a;
+    if (lane + 1 < nw) {
+        const double dx = G.wx[lane + 1] - G.wx[lane], dy = G.wy[lane + 1] - G.wy[lane];
+        G.seg[lane] = sqrt(dx * dx + dy * dy);
+    }
+    if (lane < D2D_MAX_SEGS && lane >= nw - 2) s.xa[lane] = s.xb[lane] = s.xc[lane] = s.ya[lane] = s.yb[lane] = s.yc[lane] = 0.0;
+    if (lane >= nw && lane < D2D_MAX_WPS) s.us[lane] = 0.0;
+    __syncthreads();
+    if (lane == 0) {
+        s.n_wps = nw;
+        double acc = 0.0;
+        s.us[0] = 0.0;
+        for (int i = 0; i + 1 < nw; ++i) {
+            acc = acc + G.seg[i];
+            s.us[i + 1] = acc;
+        }
+    }
+    __syncthreads();
+    {
+        // lanes 0..nw-3: the x fit of interior waypoint n = lane + 1; lanes 32..32+nw-3: the y fit
+        const int n = (lane & 31) + 1;
+        if (n + 1 < nw && (lane & 31) < D2D_MAX_SEGS) {
+            const bool yfit = lane >= 32;
+            const double u[3] = {s.us[n - 1], s.us[n], s.us[n + 1]};
+            double A[3][3], b[3], x[3];
+            const double* w = yfit ? G.wy : G.wx;
+            for (int r = 0; r < 3; ++r) {
+                A[r][0] = u[r] * u[r];
+                A[r][1] = u[r];
+                A[r][2] = 1.0;
+                b[r] = w[n - 1 + r];
+            }
+            gen_solve3(A, b, x);
+            if (!yfit) {
+                s.xa[n - 1] = x[0];
+                s.xb[n - 1] = x[1];
+                s.xc[n - 1] = x[2];
+            } else {
+                s.ya[n - 1] = x[0];
+                s.yb[n - 1] = x[1];
+                s.yc[n - 1] = x[2];
+            }
+        }
+    }
+    double chance;
+    const int st = gen_stage(c, sim, &chance);
+    if (lane == 0) {
+        s.n_circles = 0;
+        s.wp_last_x = G.wx[nw - 1];
+        s.wp_last_y = G.wy[nw - 1];
+        s.spawn_xmin = s.spawn_xmax = G.wx[0];
+        s.spawn_ymin = s.spawn_ymax = G.wy[0];
+        s.spawn_amin = -PI / 4.0;
+        s.spawn_amax = PI / 4.0;
+        if (st == 2) {  // drone spawned uniformly on the screen, no obstacles (:333-337)
+            s.spawn_xmin = 100.0;
+            s.spawn_xmax = W - 100.0;
+            s.spawn_ymin = 100.0;
+            s.spawn_ymax = H - 100.0;
+        }
+    }
+    if (lane < D2D_MAX_CIRCLES) s.cx[lane] = s.cy[lane] = s.cr[lane] = 0.0;
+    __syncthreads();
+    if (st >= 3) {
+        scn_build_lanes(s, G.s, lane);  // the path, for the obstacle placement
+        __syncthreads();
+        if (lane == 0) {
+            GenStream R;
+            R.init(G.win, seed, gid, key, paz + 2 * (nw - 1));
+            if (st == 3) {
+                if (R.u01() < chance) gen_obstacles(R, G.s, s, 1.0, 0.0, 100.0, false);
+            } else if (st == 4) {
+                if (R.u01() < chance) gen_obstacles(R, G.s, s, 1.0, 0.0, 0.0, true);
+            } else {
+                double n_obs = R.normal(1.0, 4.0);
+                if (n_obs < 0.0 && n_obs > -3.0) n_obs = 1.0;
+                if (n_obs < -3.0) n_obs = 0.0;
+                if (n_obs != 0.0) {
+                    gen_obstacles(R, G.s, s, n_obs, 0.0, 100.0, false);
+                    gen_obstacles(R, G.s, s, 1.0, 0.0, 0.0, true);
+                }
+            }
+        }
+        __syncthreads();
+    }
+    scn_build_lanes(s, G.s, lane);
+    __syncthreads();
 }
 
 }  // namespace d2d

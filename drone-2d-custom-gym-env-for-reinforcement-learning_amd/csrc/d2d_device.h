@@ -69,7 +69,10 @@ enum { REC_XB = 0, REC_XA = 6, REC_U0 = 12, REC_U1 = 13, REC_IDU = 14, REC_T = 1
 constexpr int REC_W = REC_N + 1;
 struct Scn {
     int32_t n_wps, n_circles;
-#if D2D_REC_RM
+#if D2D_REC_RM == 2
+    double us_[D2D_MAX_WPS];
+    double rec_[D2D_MAX_WPS][REC_W];
+#elif D2D_REC_RM
     double rec_[D2D_MAX_WPS][REC_W];
 #else
     double us_[D2D_MAX_WPS];
@@ -82,7 +85,10 @@ struct Scn {
                        // (also keeps sizeof(Scn) % 16 == 0: the probe tables staged after it stay aligned)
 };
 static_assert(sizeof(Scn) % 16 == 0, "Scn size");
-#if D2D_REC_RM
+#if D2D_REC_RM == 2
+#define SREC(s, f, n) ((s).rec_[(n)][(f)])
+#define SUS(s, k) ((s).us_[(k)])
+#elif D2D_REC_RM
 #define SREC(s, f, n) ((s).rec_[(n)][(f)])
 #define SUS(s, k) ((s).rec_[(k)][REC_U0])
 #else
@@ -99,9 +105,10 @@ __host__ __device__ inline bool scn_build(const d2d_scn& a, Scn& s) {
     s.n_circles = a.n_circles;
     double us[D2D_MAX_WPS];
     for (int k = 0; k < D2D_MAX_WPS; ++k) us[k] = (k < nw) ? a.us[k] : __builtin_inf();
-#if !D2D_REC_RM
+#if D2D_REC_RM != 1
     for (int k = 0; k < D2D_MAX_WPS; ++k) s.us_[k] = us[k];
-#else
+#endif
+#if D2D_REC_RM
     for (int n = 0; n < D2D_MAX_WPS; ++n) s.rec_[n][REC_N] = 0.0;  // the pad
 #endif
     for (int n = 0; n < D2D_MAX_WPS; ++n) {
@@ -485,7 +492,9 @@ struct BtIt {             // probe j (0: the initial point; k + 1: the probe of 
     double dxn, dxf;      // xf - nfc, xf - fulc before step k
     double e;             // e before step k if |e| > tol1 (parabolic step tried), else 0 (never accepted)
     double am, bm;        // a - xf, b - xf before step k
+#if D2D_REC_RM != 2
     double pad;
+#endif
 };
 struct BtSnap {           // search state before step k (the f values are distances at probes j_*)
     double a, b, fulc, nfc, xf, rat, e, ka, kxf;
@@ -495,7 +504,7 @@ struct BtSnap {           // search state before step k (the f values are distan
 struct BtHot {
     BtIt it[2][BT_HOT];   // [kind][probe]
 };
-static_assert(sizeof(BtIt) == 64, "BtIt size");
+static_assert(sizeof(BtIt) == (D2D_REC_RM == 2 ? 56 : 64), "BtIt size");
 struct BrTab {
     BtHot hot;            // first member: staged into LDS as one block
     BtSnap snap[2][BT_K + 1];
@@ -522,7 +531,10 @@ __device__ __forceinline__ void brtab_build(const Scn& s, int kind, BrTab& T) {
     B.fx = B.ffulc = B.fnfc = 0.0;
     BtIt& h0 = T.hot.it[kind][0];
     path_eval_n(s, K, B.xf, B.ixf, h0.X, h0.Y, B.kxf);
-    h0.dxn = h0.dxf = h0.e = h0.am = h0.bm = h0.pad = 0.0;
+    h0.dxn = h0.dxf = h0.e = h0.am = h0.bm = 0.0;
+#if D2D_REC_RM != 2
+    h0.pad = 0.0;
+#endif
     int jf = 0, jn = 0, jx = 0;  // probe indices of fulc, nfc, xf
     int k = 0;
     for (; k < BT_K && brent_active(B); ++k) {
@@ -537,7 +549,9 @@ __device__ __forceinline__ void brtab_build(const Scn& s, int kind, BrTab& T) {
         h.e = (fabs(B.e) > tol1) ? B.e : 0.0;
         h.am = a - xf;
         h.bm = b - xf;
+#if D2D_REC_RM != 2
         h.pad = 0.0;
+#endif
         // golden step (brent_step with par == false)
         const double e_g = (xf >= xm) ? a - xf : b - xf;
         const double rat = BR_GOLDEN * e_g;
@@ -608,7 +622,11 @@ __device__ __forceinline__ BtIt bt_hot(const BtHot* hot, int kind, int j) {
     if (!LT) return hot->it[kind][j];
     using HL = __attribute__((address_space(3))) const double;
     const HL* q = (const HL*)&hot->it[kind][j];
+#if D2D_REC_RM == 2
+    return BtIt{q[0], q[1], q[2], q[3], q[4], q[5], q[6]};
+#else
     return BtIt{q[0], q[1], q[2], q[3], q[4], q[5], q[6], q[7]};
+#endif
 }
 template <bool LT>
 __device__ __forceinline__ double bt_dist(const BtHot* hot, int kind, int j, double px, double py) {

@@ -18,6 +18,7 @@
 using namespace d2dk;
 
 
+
 namespace {
 thread_local std::string g_err;
 
@@ -68,6 +69,7 @@ struct d2d_handle {
     d2d_curriculum cur{};        // fresh mode: generator parameters
     int32_t* scn_tag = nullptr;  // fresh mode: [2 n] episode key of each slot
     int64_t* gclk = nullptr;     // fresh mode: [2 n] clock at generation
+    int32_t* fresh_q = nullptr;  // fresh mode: [2 n + 1] K5's queue of slots to generate + its length
     int64_t* clock = nullptr;    // [1] the step clock (K1 advances it)
     uint64_t fresh_seed = 0;
     bool fresh_seeded = false;
@@ -87,7 +89,8 @@ StepArgs make_args(const d2d_t* h) {
     a.ist = h->ist;
     a.acc = h->acc;
     a.scn = h->scn;
-    a.brt = h->brt;
+    // (diagnostic A/B: D2D_FRESH_NOTAB=1 drops the golden-march tables in fresh mode)
+    a.brt = (D2D_FRESH_NOTAB && h->cfg.scn_pool == 2) ? nullptr : h->brt;
     a.env_scn = h->env_scn;
     a.pool_base = h->pool_dev;
     a.pool_n = h->pool_n;
@@ -125,9 +128,16 @@ hipError_t fresh_regen(d2d_t* h, hipStream_t stream, bool restore = false) {
     f.tag = h->scn_tag;
     f.gclk = h->gclk;
     f.clock = h->clock;
+    f.queue = h->fresh_q;
+    f.qcount = h->fresh_q + 2 * (size_t)h->n;
     f.restore = restore ? 1 : 0;
     const int items = restore ? 2 * h->n : h->n;
-    hipLaunchKernelGGL(d2d_fresh_kernel, dim3((items + 63) / 64), dim3(64), 0, stream, f);
+    hipError_t e = hipMemsetAsync(f.qcount, 0, sizeof(int32_t), stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(d2d_fresh_scan_kernel, dim3((items + 255) / 256), dim3(256), 0, stream, f);
+    // one wave per queued slot: ~90 per step at 65 536 envs; a reset queues every env (the grid's
+    // workgroups then take several each)
+    hipLaunchKernelGGL(d2d_fresh_gen_kernel, dim3(std::min(items, 2048)), dim3(64), 0, stream, f);
     return hipGetLastError();
 }
 bool fresh_mode(const d2d_t* h) { return h->cfg.scn_pool == 2; }
@@ -423,6 +433,7 @@ void d2d_destroy(d2d_t* h) {
     if (h->abi) (void)hipFree(h->abi);
     if (h->scn_tag) (void)hipFree(h->scn_tag);
     if (h->gclk) (void)hipFree(h->gclk);
+    if (h->fresh_q) (void)hipFree(h->fresh_q);
     delete h;
 }
 
@@ -874,19 +885,22 @@ int32_t d2d_set_curriculum(d2d_t* h, const d2d_curriculum* c) {
     const size_t S = 2 * (size_t)h->n;
     if (h->n_scn != (int)S || !h->scn_tag) {
         if ((e = hipDeviceSynchronize()) != hipSuccess) return hip_fail(e, "d2d_set_curriculum: sync");
-        for (void* p : {(void*)h->scn, (void*)h->brt, (void*)h->abi, (void*)h->scn_tag, (void*)h->gclk})
+        for (void* p : {(void*)h->scn, (void*)h->brt, (void*)h->abi, (void*)h->scn_tag, (void*)h->gclk,
+                        (void*)h->fresh_q})
             if (p) (void)hipFree(p);
         h->scn = nullptr;
         h->brt = nullptr;
         h->abi = nullptr;
         h->scn_tag = nullptr;
         h->gclk = nullptr;
+        h->fresh_q = nullptr;
         h->n_scn = 0;
         if ((e = hipMalloc(&h->scn, sizeof(d2d::Scn) * S)) != hipSuccess ||
             (e = hipMalloc(&h->brt, sizeof(d2d::BrTab) * S)) != hipSuccess ||
             (e = hipMalloc(&h->abi, sizeof(d2d_scn) * S)) != hipSuccess ||
             (e = hipMalloc(&h->scn_tag, sizeof(int32_t) * S)) != hipSuccess ||
             (e = hipMalloc(&h->gclk, sizeof(int64_t) * S)) != hipSuccess ||
+            (e = hipMalloc(&h->fresh_q, sizeof(int32_t) * (S + 1))) != hipSuccess ||
             (e = hipMemset(h->scn, 0, sizeof(d2d::Scn) * S)) != hipSuccess ||
             (e = hipMemset(h->brt, 0, sizeof(d2d::BrTab) * S)) != hipSuccess ||
             (e = hipMemset(h->abi, 0, sizeof(d2d_scn) * S)) != hipSuccess ||

@@ -113,6 +113,9 @@ struct StepArgs {
 #define D2D_ABL 0        // diagnostic builds only: bit r skips role r's compute, bit 4 = perfect
                          // reset cache (no fills, every entry taken as ready): timing ablations
 #endif
+#ifndef D2D_FRESH_NOTAB
+#define D2D_FRESH_NOTAB 0  // diagnostic A/B builds only: fresh curriculum without golden-march tables
+#endif
 #ifndef D2D_SPLIT3
 #define D2D_SPLIT3 -1    // W2, W1 and W3 re-check one third each of the golden-march table: 1 always,
                          // 0 never, -1 when K1 has at most one workgroup per CU (chosen in d2d_step)
@@ -1036,11 +1039,20 @@ __global__ __launch_bounds__(BLOCK, 4) void d2d_fill_kernel(StepArgs a) {
 }
 
 // ------------------------------------------------------------------------ fresh curriculum (K5)
-// Scenario generation for the fresh curriculum (d2d_curriculum.h), one thread per env: the scenario
-// of the episode env i's next reset starts (key = its episode counter) goes into slot 2 i + (key & 1)
-// unless that slot already holds it; the other slot holds the running episode's.  Launched after
-// every K1 (the slot is needed one step later at the earliest), before and after K2, and after
-// d2d_set_state; restore = 1 regenerates every slot from its recipe (key, clock) instead.
+// Scenario generation for the fresh curriculum (d2d_curriculum.h).  The scenario of the episode env
+// i's next reset starts (key = its episode counter) goes into slot 2 i + (key & 1) unless that slot
+// already holds it; the other slot holds the running episode's.  Launched after every K1 (the slot is
+// needed one step later at the earliest), before and after K2, and after d2d_set_state; restore = 1
+// regenerates every slot from its recipe (key, clock) instead.  Two launches:
+//   K5a d2d_fresh_scan_kernel  one thread per env (slot when restoring): the slots to generate are
+//                              appended to a device queue (one atomic per wave)
+//   K5b d2d_fresh_gen_kernel   one wave per queued slot: gen_curriculum_wave builds the scenario in
+//                              LDS with all 64 lanes, then the golden-march tables (lanes 0 and 1, one
+//                              forced run each) and coalesced copies of the ABI record and the device
+//                              table.  ~90 slots per step at 65 536 envs: they run side by side, so the
+//                              launch lasts about one slot's latency.
+// (Round 3's K5 built each scenario serially on one lane, with the device table in global memory:
+// 320 us mean, 3.8 ms max per launch.)
 struct FreshArgs {
     int n;                   // envs (pool modes keep the identity slot layout: slot == env)
     const int32_t* ist;      // [NISTATE][n] (episode counters)
@@ -1055,35 +1067,70 @@ struct FreshArgs {
     int32_t* tag;            // [2 n] episode key of each slot (-1: empty)
     int64_t* gclk;           // [2 n] clock at generation
     const int64_t* clock;    // the step clock (K1 advances it)
+    int32_t* queue;          // [2 n] slots to generate (K5a -> K5b)
+    int32_t* qcount;         // [1] queue length (zeroed before K5a)
     int restore;
 };
-__global__ __launch_bounds__(64) void d2d_fresh_kernel(FreshArgs f) {
-    const int t = blockIdx.x * 64 + threadIdx.x;
-    int slot, key, i;
-    int64_t clk;
+__global__ __launch_bounds__(256) void d2d_fresh_scan_kernel(FreshArgs f) {
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    bool need = false;
+    int slot = 0;
     if (f.restore) {
-        if (t >= 2 * f.n) return;
-        slot = t;
-        key = f.tag[slot];
-        if (key < 0) return;
-        i = slot >> 1;
-        clk = f.gclk[slot];
-    } else {
-        if (t >= f.n) return;
-        i = t;
-        const int32_t ep = f.ist[(size_t)D2D_I_EPISODE * f.n + i];
-        f.env_scn[i] = fresh_slot(i, (uint32_t)(ep - 1));
-        key = ep;
-        slot = fresh_slot(i, (uint32_t)key);
-        if (f.tag[slot] == key) return;
-        clk = *f.clock;
+        if (t < 2 * f.n) {
+            slot = t;
+            need = f.tag[slot] >= 0;
+        }
+    } else if (t < f.n) {
+        const int32_t ep = f.ist[(size_t)D2D_I_EPISODE * f.n + t];
+        f.env_scn[t] = fresh_slot(t, (uint32_t)(ep - 1));
+        slot = fresh_slot(t, (uint32_t)ep);
+        need = f.tag[slot] != ep;
     }
-    const double sim = f.cur.sim_num0 + (double)clk * f.cur.envs_total;
-    gen_curriculum(f.cur, f.W, f.H, f.seed, f.env_id_base + (uint32_t)i, (uint32_t)key, sim, f.abi[slot], f.scn[slot]);
-    brtab_build(f.scn[slot], 0, f.brt[slot]);
-    brtab_build(f.scn[slot], 1, f.brt[slot]);
-    f.gclk[slot] = clk;
-    f.tag[slot] = key;
+    const uint64_t m = __ballot(need);
+    if (m == 0ull) return;
+    const int lane = threadIdx.x & 63, first = __ffsll((unsigned long long)m) - 1;
+    int base = 0;
+    if (lane == first) base = atomicAdd(f.qcount, __popcll(m));
+    base = __shfl(base, first);
+    if (need) f.queue[base + __popcll(m & ((1ull << lane) - 1ull))] = slot;
+}
+__global__ __launch_bounds__(64) void d2d_fresh_gen_kernel(FreshArgs f) {
+    __shared__ __attribute__((aligned(16))) GenLds G;
+    const int lane = threadIdx.x;
+    const int count = __hip_atomic_load(f.qcount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int it = blockIdx.x; it < count; it += gridDim.x) {
+        const int slot = f.queue[it];
+        const int i = slot >> 1;
+        int key;
+        int64_t clk;
+        if (f.restore) {
+            key = f.tag[slot];
+            clk = f.gclk[slot];
+        } else {
+            key = f.ist[(size_t)D2D_I_EPISODE * f.n + i];
+            clk = *f.clock;
+        }
+        const double sim = f.cur.sim_num0 + (double)clk * f.cur.envs_total;
+        gen_curriculum_wave(f.cur, f.W, f.H, f.seed, f.env_id_base + (uint32_t)i, (uint32_t)key, sim, G, lane);
+        // the device table and the ABI record, 8-byte words across the wave
+        {
+            const double* src = reinterpret_cast<const double*>(&G.s);
+            double* dst = reinterpret_cast<double*>(f.scn + slot);
+            for (int k = lane; k < (int)(sizeof(Scn) / 8); k += 64) dst[k] = src[k];
+            static_assert(sizeof(d2d_scn) % 8 == 0, "d2d_scn size");
+            const double* sa = reinterpret_cast<const double*>(&G.a);
+            double* da = reinterpret_cast<double*>(f.abi + slot);
+            for (int k = lane; k < (int)(sizeof(d2d_scn) / 8); k += 64) da[k] = sa[k];
+        }
+#if !D2D_FRESH_NOTAB
+        if (lane < 2) brtab_build(G.s, lane, f.brt[slot]);  // kind = lane, from the LDS table
+#endif
+        if (lane == 0) {
+            f.gclk[slot] = clk;
+            f.tag[slot] = key;
+        }
+        __syncthreads();  // G is reused by the next item
+    }
 }
 
 // ------------------------------------------------------------------------- golden-march tables
