@@ -19,10 +19,6 @@ def env_headers() -> list:
 
 HDRS = env_headers()
 OUT = os.path.join(PKG_DIR, "_lib", "libdrone2d_hip.so")
-# the same source with record-major scenario records (D2D_REC_RM=1, d2d_device.h): the build the fresh
-# curriculum loads, whose per-env scenarios are read from global memory (1.7 x faster there, slower on
-# the LDS-staged test scenarios)
-OUT_RM = os.path.join(PKG_DIR, "_lib", "libdrone2d_hip_rm.so")
 # the PPO update's fused element-wise kernels (include/d2d_ppo.h)
 PPO_SRC = os.path.join(PKG_DIR, "csrc", "d2d_ppo.hip")
 PPO_HDRS = [os.path.join(REPO, "include", "d2d_ppo.h")]
@@ -66,12 +62,13 @@ def _compile(src: str, out: str, verbose: bool, flags=None):
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
-    """The in-tree libraries: the env (libdrone2d_hip.so, and libdrone2d_hip_rm.so for the fresh curriculum)
-    and the PPO update kernels (libd2d_ppo.so)."""
+    """The in-tree libraries: the env (libdrone2d_hip.so: every mode, one scenario layout) and the PPO
+    update kernels (libd2d_ppo.so)."""
+    stale = os.path.join(PKG_DIR, "_lib", "libdrone2d_hip_rm.so")  # rounds 1-3's second layout build
+    if os.path.exists(stale):
+        os.remove(stale)
     if force or needs_build():
         _compile(SRC, OUT, verbose)
-    if force or needs_build(OUT_RM):
-        _compile(SRC, OUT_RM, verbose, HIPCC_FLAGS + ["-DD2D_REC_RM=1"])
     if force or needs_build(PPO_OUT, PPO_SRC, PPO_HDRS):
         _compile(PPO_SRC, PPO_OUT, verbose, PPO_FLAGS)
     return OUT

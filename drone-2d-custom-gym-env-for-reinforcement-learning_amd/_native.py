@@ -14,8 +14,6 @@ from . import abi
 LIB_NAME = "libdrone2d_hip.so"
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
 LIB_PATH = os.path.join(LIB_DIR, LIB_NAME)
-# the record-major build of the same source (fresh curriculum: per-env scenarios in global memory)
-LIB_PATH_RM = os.path.join(LIB_DIR, "libdrone2d_hip_rm.so")
 
 # every entry point of include/drone2d.h: name -> (restype, argtypes)
 _VP = C.c_void_p

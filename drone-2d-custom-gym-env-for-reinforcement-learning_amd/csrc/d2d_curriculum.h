@@ -344,12 +344,8 @@ __device__ inline void scn_build_lanes(const d2d_scn& a, Scn& s, int lane) {
     const int nw = a.n_wps, nseg = nw - 2;
     if (lane < D2D_MAX_WPS) {
         const int n = lane;
-#if D2D_REC_RM != 1
         s.us_[n] = (n < nw) ? a.us[n] : __builtin_inf();
-#endif
-#if D2D_REC_RM
         s.rec_[n][REC_N] = 0.0;
-#endif
         const int b = (n < nseg - 1) ? n : nseg - 1;
         const int q = (n == 0) ? nseg - 1 : ((n - 1 < nseg - 1) ? n - 1 : nseg - 1);
         const double v[REC_N] = {a.xa[b], a.xb[b], a.xc[b], a.ya[b], a.yb[b], a.yc[b],
@@ -395,7 +391,74 @@ struct GenLds {
     Scn s;                     // its device form (obstacle placement, tables)
     uint32_t win[GEN_WIN];     // the stream's first GEN_WIN words
     double wx[D2D_MAX_WPS], wy[D2D_MAX_WPS], sa[D2D_MAX_WPS], ca[D2D_MAX_WPS], seg[D2D_MAX_WPS];
+    // golden-march table build (brtab_build_wave): per kind, the probes and their knot intervals
+    double bx[2][BT_K + 1], bk[2][BT_K + 1];
+    int32_t bix[2][BT_K + 1], bta[2][BT_K], blen[2];
+    // obstacle placement (gen_obstacles_wave): the trial that starts at stream word w0 + 2 l, per lane l
+    double ox[64], oy[64], osz[64];
+    int32_t ook[64], ocons[64];
+    int32_t wpos;            // the stream position after the obstacle calls
 };
+
+// generate_obstacles_around_path (gen_obstacles) with the wave: one rejection trial is a pure function
+// of the stream word it starts at (every draw consumes an even number of words), so lane l evaluates
+// the trial starting at word w0 + 2 l and lane 0 then walks the chain of trials the serial loop would
+// run (w -> w + words consumed), appending the accepted circles in order; a chain that leaves the 64
+// evaluated starts continues from a new w0.  Same trials, same order, same arithmetic as gen_obstacles.
+__device__ inline void gen_obstacles_wave(GenLds& G, uint64_t seed, uint32_t gid, uint32_t key, double n, double mean,
+                                          double std, bool on_path, int lane) {
+    d2d_scn& s = G.a;
+    const double L = s.us[s.n_wps - 1];
+    int num = 0, tries = 0, w = G.wpos;
+    bool more = true;
+    while (more) {  // (wave-uniform: the walk below runs on lane 0, its state goes through LDS)
+        {
+            GenStream R;
+            R.init(G.win, seed, gid, key, w + 2 * lane);
+            const double u = R.uniform(0.20 * L, 0.90 * L);
+            double gx, gy;
+            gen_gradient(s, u, gx, gy);
+            const double dist = R.normal(mean, std);
+            double x, y;
+            path_eval(G.s, u, x, y);
+            const double g = sqrt(gx * gx + gy * gy);
+            const double ox = x + dist * (gy / g), oy = y + dist * (-gx / g);
+            const double size = R.uniform(10.0, 50.0);
+            const double dx = ox - x, dy = oy - y;
+            const double off = sqrt(dx * dx + dy * dy);
+            const bool ok = on_path || off > size + 10.0;
+            G.ox[lane] = on_path ? x : ox;
+            G.oy[lane] = on_path ? y : oy;
+            G.osz[lane] = size;
+            G.ook[lane] = ok ? 1 : 0;
+            G.ocons[lane] = R.pos - (w + 2 * lane);
+        }
+        __syncthreads();
+        if (lane == 0) {
+            const int w0 = w;
+            while ((double)num < n && s.n_circles < D2D_MAX_CIRCLES && tries < 4096 && w < w0 + 128) {
+                const int t = (w - w0) >> 1;
+                ++tries;
+                if (G.ook[t]) {
+                    s.cx[s.n_circles] = G.ox[t];
+                    s.cy[s.n_circles] = G.oy[t];
+                    s.cr[s.n_circles] = G.osz[t];
+                    s.n_circles += 1;
+                    ++num;
+                }
+                w += G.ocons[t];
+            }
+            G.ook[0] = ((double)num < n && s.n_circles < D2D_MAX_CIRCLES && tries < 4096) ? 1 : 0;
+            G.ocons[0] = w;
+        }
+        __syncthreads();
+        more = G.ook[0] != 0;
+        w = G.ocons[0];
+        __syncthreads();  // (G.ook / G.ocons are rewritten by the next round)
+    }
+    if (lane == 0) G.wpos = w;
+    __syncthreads();
+}
 
 // one curriculum reset by the calling wave (all 64 lanes, wave-uniform arguments); the result is in
 // G.a / G.s (LDS).  Same draws and arithmetic as gen_curriculum.
@@ -509,30 +572,150 @@ __device__ inline void gen_curriculum_wave(const d2d_curriculum& c, double W, do
     }
     if (lane < D2D_MAX_CIRCLES) s.cx[lane] = s.cy[lane] = s.cr[lane] = 0.0;
     __syncthreads();
-    if (st >= 3) {
+    if (st >= 3 && !(D2D_ABLATE & 128)) {  // (128: diagnostic timing builds skip the obstacles)
         scn_build_lanes(s, G.s, lane);  // the path, for the obstacle placement
-        __syncthreads();
+        // the draws before the obstacle calls (lane 0), then the calls (gen_obstacles_wave)
+        __shared__ double s_nobs;
         if (lane == 0) {
             GenStream R;
             R.init(G.win, seed, gid, key, paz + 2 * (nw - 1));
-            if (st == 3) {
-                if (R.u01() < chance) gen_obstacles(R, G.s, s, 1.0, 0.0, 100.0, false);
-            } else if (st == 4) {
-                if (R.u01() < chance) gen_obstacles(R, G.s, s, 1.0, 0.0, 0.0, true);
+            double n_obs = 0.0;
+            if (st == 3 || st == 4) {
+                n_obs = (R.u01() < chance) ? 1.0 : 0.0;
             } else {
-                double n_obs = R.normal(1.0, 4.0);
+                n_obs = R.normal(1.0, 4.0);
                 if (n_obs < 0.0 && n_obs > -3.0) n_obs = 1.0;
                 if (n_obs < -3.0) n_obs = 0.0;
-                if (n_obs != 0.0) {
-                    gen_obstacles(R, G.s, s, n_obs, 0.0, 100.0, false);
-                    gen_obstacles(R, G.s, s, 1.0, 0.0, 0.0, true);
-                }
             }
+            s_nobs = n_obs;
+            G.wpos = R.pos;
         }
         __syncthreads();
+        const double n_obs = s_nobs;
+        if (st == 3) {
+            if (n_obs != 0.0) gen_obstacles_wave(G, seed, gid, key, 1.0, 0.0, 100.0, false, lane);
+        } else if (st == 4) {
+            if (n_obs != 0.0) gen_obstacles_wave(G, seed, gid, key, 1.0, 0.0, 0.0, true, lane);
+        } else if (n_obs != 0.0) {
+            gen_obstacles_wave(G, seed, gid, key, n_obs, 0.0, 100.0, false, lane);
+            gen_obstacles_wave(G, seed, gid, key, 1.0, 0.0, 0.0, true, lane);
+        }
     }
     scn_build_lanes(s, G.s, lane);
     __syncthreads();
+}
+
+
+// brtab_build for both kinds with the wave (d2d_device.h: the forced runs).  The forced decisions make
+// the search's floating-point state (a, b, fulc, nfc, xf, e, rat) a function of the step number alone,
+// so lanes 0 and 1 (kind = lane) first run that recurrence with no path evaluation, recording each
+// step's probe; then every lane evaluates probes (knot interval + QPMI2D point), independent of each
+// other; then lanes 0 and 1 replay the interval bookkeeping (ia, ka, ib, ixf, kxf) from the probes'
+// intervals.  Every stored value is computed by the same operations as in brtab_build, so the tables
+// are identical to it.
+__device__ inline void brtab_build_wave(const Scn& s, BrTab& T, GenLds& G, int lane) {
+    const PathK K = path_k(s);
+    if (lane < 2) {
+        const int kind = lane;
+        double a = 0.0 - 10.0, b = K.L + 10.0;
+        double fulc = a + BR_GOLDEN * (b - a);
+        double nfc = fulc, xf = fulc, rat = 0.0, e = 0.0;
+        int num = 1, jf = 0, jn = 0, jx = 0;
+        G.bx[kind][0] = xf;
+        BtIt& h0 = T.hot.it[kind][0];
+        h0.dxn = h0.dxf = h0.e = h0.am = h0.bm = h0.pad = 0.0;
+        int k = 0;
+        for (; k < BT_K; ++k) {
+            {
+                const double xm0 = 0.5 * (a + b);
+                const double t1 = BR_SQRT_EPS * fabs(xf) + BR_XATOL3;
+                const double t2 = 2.0 * t1;
+                if (!((fabs(xf - xm0) > (t2 - 0.5 * (b - a))) & (num < 500))) break;  // brent_active
+            }
+            BtSnap& S = T.snap[kind][k];
+            S.a = a; S.b = b; S.fulc = fulc; S.nfc = nfc; S.xf = xf; S.rat = rat; S.e = e;
+            S.num = num; S.j_fulc = jf; S.j_nfc = jn; S.j_xf = jx; S.pad = 0;
+            const double xm = 0.5 * (a + b);
+            const double tol1 = BR_SQRT_EPS * fabs(xf) + BR_XATOL3;
+            BtIt& h = T.hot.it[kind][k + 1];
+            h.dxn = xf - nfc;
+            h.dxf = xf - fulc;
+            h.e = (fabs(e) > tol1) ? e : 0.0;
+            h.am = a - xf;
+            h.bm = b - xf;
+            h.pad = 0.0;
+            const double e_g = (xf >= xm) ? a - xf : b - xf;
+            rat = BR_GOLDEN * e_g;
+            e = e_g;
+            const double mx = fmax(fabs(rat), tol1);
+            const double x = xf + ((rat < 0.0) ? -mx : mx);
+            G.bx[kind][k + 1] = x;
+            num += 1;
+            const bool le = !(kind == 0 && k == 0);
+            const bool c1 = !le;
+            const bool ge = x >= xf;
+            const bool to_a = le == ge;
+            G.bta[kind][k] = to_a ? 1 : 0;
+            const double t = le ? xf : x;
+            a = to_a ? t : a;
+            b = to_a ? b : t;
+            const int j = k + 1;
+            const double nfulc = (le | c1) ? nfc : fulc;
+            const int njf = (le | c1) ? jn : jf;
+            const double nnfc = le ? xf : (c1 ? x : nfc);
+            const int njn = le ? jx : (c1 ? j : jn);
+            fulc = nfulc;
+            nfc = nnfc;
+            xf = le ? x : xf;
+            jf = njf;
+            jn = njn;
+            jx = le ? j : jx;
+        }
+        BtSnap& S = T.snap[kind][k];
+        S.a = a; S.b = b; S.fulc = fulc; S.nfc = nfc; S.xf = xf; S.rat = rat; S.e = e;
+        S.num = num; S.j_fulc = jf; S.j_nfc = jn; S.j_xf = jx; S.pad = 0;
+        G.blen[kind] = k;
+        T.len[kind] = k;
+    }
+    __syncthreads();
+    // every probe j <= len of both kinds: knot interval, path point, upper knot
+    const int n0 = G.blen[0] + 1, n1 = G.blen[1] + 1;
+    for (int q = lane; q < n0 + n1; q += 64) {
+        const int kind = q < n0 ? 0 : 1, j = q < n0 ? q : q - n0;
+        const double x = G.bx[kind][j];
+        const int ix = u_index(s, x);
+        double X, Y, kx;
+        path_eval_n(s, K, x, ix, X, Y, kx);
+        BtIt& h = T.hot.it[kind][j];
+        h.X = X;
+        h.Y = Y;
+        G.bix[kind][j] = ix;
+        G.bk[kind][j] = kx;
+    }
+    __syncthreads();
+    if (lane < 2) {
+        const int kind = lane, len = G.blen[kind];
+        int ia = u_index(s, 0.0 - 10.0), ib = u_index(s, K.L + 10.0);
+        double ka = SREC(s, REC_U1, ia);
+        int ixf = G.bix[kind][0];
+        double kxf = G.bk[kind][0];
+        for (int k = 0; k <= len; ++k) {
+            BtSnap& S = T.snap[kind][k];
+            S.ka = ka; S.kxf = kxf; S.ia = ia; S.ib = ib; S.ixf = ixf;
+            if (k == len) break;
+            const bool le = !(kind == 0 && k == 0);
+            const bool to_a = G.bta[kind][k] != 0;
+            const int ix = G.bix[kind][k + 1];
+            const double kx = G.bk[kind][k + 1];
+            const int ti = le ? ixf : ix;
+            const double tk = le ? kxf : kx;
+            ia = to_a ? ti : ia;
+            ka = to_a ? tk : ka;
+            ib = to_a ? ib : ti;
+            ixf = le ? ix : ixf;
+            kxf = le ? kx : kxf;
+        }
+    }
 }
 
 }  // namespace d2d

@@ -30,7 +30,8 @@
 
 // Diagnostic-only ablation mask (tools/ablate.py builds separate timing-only libraries with it;
 // the product is always built with 0): 1 skip Brent, 2 skip sensing, 4 skip joint iterations,
-// 8 skip collision test, 16 skip the Brent continuation after the golden-march tables.
+// 8 skip collision test, 16 skip the Brent continuation after the golden-march tables, 128 the fresh
+// curriculum generator skips the obstacles.
 #ifndef D2D_ABLATE
 #define D2D_ABLATE 0
 #endif
@@ -54,30 +55,19 @@ constexpr double VEL_MAX = 1330.0;            // drone_2d_env.py:635
 //   RN(1 / (us[n+1] - us[n])), and the blend threshold T: in interval n QPMI2D.__call__ blends the
 //   two quadratics exactly when u < T[n] (below).
 enum { REC_XB = 0, REC_XA = 6, REC_U0 = 12, REC_U1 = 13, REC_IDU = 14, REC_T = 15, REC_N = 16 };
-// Record layout.  D2D_REC_RM = 1: record-major with a one-double pad (interval n's 16 fields are
-// contiguous, 136 bytes apart): from LDS a wave whose lanes sit in different intervals still reads
-// 16 different banks per field (n x 34 dwords mod 64 is distinct for n < 16), and from global memory
-// (the fresh curriculum's per-lane scenarios) one QPMI2D evaluation touches 2-3 cache lines per lane
-// instead of 16.  The knots are the records' u0 column (us[k] = rec[k][REC_U0]; +inf past n_wps).
-// 0: field-major rec[f][n] plus a separate us[] (rounds 1-3).  Same size either way.  Measured
-// (profiles/r03/recrm/, parity green with either): 1 makes the fresh curriculum's step 1.70 x
-// faster (883 -> 521 us at 65 536 envs) but the LDS paths 0.7 % (corridor) to 3.7 % (mixed) slower,
-// so the BASELINE configs keep 0 until the global-memory instantiations get their own layout.
-#ifndef D2D_REC_RM
-#define D2D_REC_RM 0
-#endif
+// Layout (one for every path since round 4): the knots us_[k] contiguous (the knot scan of u_index
+// reads one or two cache lines from global memory, one 16-byte LDS broadcast per two knots) and the
+// interval records record-major with a one-double pad (interval n's 16 fields contiguous, 136 bytes
+// apart): from LDS a wave whose lanes sit in different intervals still reads 16 different banks per
+// field (n x 34 dwords mod 64 is distinct for n < 16), and from global memory (the fresh curriculum's
+// per-lane scenarios) one QPMI2D evaluation touches two cache lines per lane instead of 16.
+// Measured against the field-major rounds 1-3 layout (profiles/r04/layout/): corridor / S_corridor
+// / mixed unchanged, the fresh curriculum's step kernel 179 -> 105 us at 65 536 envs.
 constexpr int REC_W = REC_N + 1;
 struct Scn {
     int32_t n_wps, n_circles;
-#if D2D_REC_RM == 2
     double us_[D2D_MAX_WPS];
     double rec_[D2D_MAX_WPS][REC_W];
-#elif D2D_REC_RM
-    double rec_[D2D_MAX_WPS][REC_W];
-#else
-    double us_[D2D_MAX_WPS];
-    double rec_[REC_N][D2D_MAX_WPS];
-#endif
     double cx[D2D_MAX_CIRCLES], cy[D2D_MAX_CIRCLES], cr[D2D_MAX_CIRCLES];
     double wp_last_x, wp_last_y;
     double spawn_xmin, spawn_xmax, spawn_ymin, spawn_ymax, spawn_amin, spawn_amax;
@@ -85,16 +75,8 @@ struct Scn {
                        // (also keeps sizeof(Scn) % 16 == 0: the probe tables staged after it stay aligned)
 };
 static_assert(sizeof(Scn) % 16 == 0, "Scn size");
-#if D2D_REC_RM == 2
 #define SREC(s, f, n) ((s).rec_[(n)][(f)])
 #define SUS(s, k) ((s).us_[(k)])
-#elif D2D_REC_RM
-#define SREC(s, f, n) ((s).rec_[(n)][(f)])
-#define SUS(s, k) ((s).rec_[(k)][REC_U0])
-#else
-#define SREC(s, f, n) ((s).rec_[(f)][(n)])
-#define SUS(s, k) ((s).us_[(k)])
-#endif
 
 // Returns false if the table is outside what the record form reproduces exactly: the last-segment
 // window us[nw-2] - 0.001 must not reach back past us[nw-3] (always true for real waypoints).
@@ -105,12 +87,8 @@ __host__ __device__ inline bool scn_build(const d2d_scn& a, Scn& s) {
     s.n_circles = a.n_circles;
     double us[D2D_MAX_WPS];
     for (int k = 0; k < D2D_MAX_WPS; ++k) us[k] = (k < nw) ? a.us[k] : __builtin_inf();
-#if D2D_REC_RM != 1
     for (int k = 0; k < D2D_MAX_WPS; ++k) s.us_[k] = us[k];
-#endif
-#if D2D_REC_RM
     for (int n = 0; n < D2D_MAX_WPS; ++n) s.rec_[n][REC_N] = 0.0;  // the pad
-#endif
     for (int n = 0; n < D2D_MAX_WPS; ++n) {
         const int b = (n < nseg - 1) ? n : nseg - 1;
         const int q = (n == 0) ? nseg - 1 : ((n - 1 < nseg - 1) ? n - 1 : nseg - 1);
@@ -492,9 +470,7 @@ struct BtIt {             // probe j (0: the initial point; k + 1: the probe of 
     double dxn, dxf;      // xf - nfc, xf - fulc before step k
     double e;             // e before step k if |e| > tol1 (parabolic step tried), else 0 (never accepted)
     double am, bm;        // a - xf, b - xf before step k
-#if D2D_REC_RM != 2
     double pad;
-#endif
 };
 struct BtSnap {           // search state before step k (the f values are distances at probes j_*)
     double a, b, fulc, nfc, xf, rat, e, ka, kxf;
@@ -504,7 +480,7 @@ struct BtSnap {           // search state before step k (the f values are distan
 struct BtHot {
     BtIt it[2][BT_HOT];   // [kind][probe]
 };
-static_assert(sizeof(BtIt) == (D2D_REC_RM == 2 ? 56 : 64), "BtIt size");
+static_assert(sizeof(BtIt) == 64, "BtIt size");
 struct BrTab {
     BtHot hot;            // first member: staged into LDS as one block
     BtSnap snap[2][BT_K + 1];
@@ -531,10 +507,7 @@ __device__ __forceinline__ void brtab_build(const Scn& s, int kind, BrTab& T) {
     B.fx = B.ffulc = B.fnfc = 0.0;
     BtIt& h0 = T.hot.it[kind][0];
     path_eval_n(s, K, B.xf, B.ixf, h0.X, h0.Y, B.kxf);
-    h0.dxn = h0.dxf = h0.e = h0.am = h0.bm = 0.0;
-#if D2D_REC_RM != 2
-    h0.pad = 0.0;
-#endif
+    h0.dxn = h0.dxf = h0.e = h0.am = h0.bm = h0.pad = 0.0;
     int jf = 0, jn = 0, jx = 0;  // probe indices of fulc, nfc, xf
     int k = 0;
     for (; k < BT_K && brent_active(B); ++k) {
@@ -549,9 +522,7 @@ __device__ __forceinline__ void brtab_build(const Scn& s, int kind, BrTab& T) {
         h.e = (fabs(B.e) > tol1) ? B.e : 0.0;
         h.am = a - xf;
         h.bm = b - xf;
-#if D2D_REC_RM != 2
         h.pad = 0.0;
-#endif
         // golden step (brent_step with par == false)
         const double e_g = (xf >= xm) ? a - xf : b - xf;
         const double rat = BR_GOLDEN * e_g;
@@ -622,11 +593,7 @@ __device__ __forceinline__ BtIt bt_hot(const BtHot* hot, int kind, int j) {
     if (!LT) return hot->it[kind][j];
     using HL = __attribute__((address_space(3))) const double;
     const HL* q = (const HL*)&hot->it[kind][j];
-#if D2D_REC_RM == 2
-    return BtIt{q[0], q[1], q[2], q[3], q[4], q[5], q[6]};
-#else
     return BtIt{q[0], q[1], q[2], q[3], q[4], q[5], q[6], q[7]};
-#endif
 }
 template <bool LT>
 __device__ __forceinline__ double bt_dist(const BtHot* hot, int kind, int j, double px, double py) {

@@ -69,7 +69,7 @@ struct d2d_handle {
     d2d_curriculum cur{};        // fresh mode: generator parameters
     int32_t* scn_tag = nullptr;  // fresh mode: [2 n] episode key of each slot
     int64_t* gclk = nullptr;     // fresh mode: [2 n] clock at generation
-    int32_t* fresh_q = nullptr;  // fresh mode: [2 n + 1] K5's queue of slots to generate + its length
+    int32_t* fresh_q = nullptr;  // fresh mode: [2 n + 2] K5's queue of slots to generate, its length, a ticket
     int64_t* clock = nullptr;    // [1] the step clock (K1 advances it)
     uint64_t fresh_seed = 0;
     bool fresh_seeded = false;
@@ -132,8 +132,6 @@ hipError_t fresh_regen(d2d_t* h, hipStream_t stream, bool restore = false) {
     f.qcount = h->fresh_q + 2 * (size_t)h->n;
     f.restore = restore ? 1 : 0;
     const int items = restore ? 2 * h->n : h->n;
-    hipError_t e = hipMemsetAsync(f.qcount, 0, sizeof(int32_t), stream);
-    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(d2d_fresh_scan_kernel, dim3((items + 255) / 256), dim3(256), 0, stream, f);
     // one wave per queued slot: ~90 per step at 65 536 envs; a reset queues every env (the grid's
     // workgroups then take several each)
@@ -900,7 +898,8 @@ int32_t d2d_set_curriculum(d2d_t* h, const d2d_curriculum* c) {
             (e = hipMalloc(&h->abi, sizeof(d2d_scn) * S)) != hipSuccess ||
             (e = hipMalloc(&h->scn_tag, sizeof(int32_t) * S)) != hipSuccess ||
             (e = hipMalloc(&h->gclk, sizeof(int64_t) * S)) != hipSuccess ||
-            (e = hipMalloc(&h->fresh_q, sizeof(int32_t) * (S + 1))) != hipSuccess ||
+            (e = hipMalloc(&h->fresh_q, sizeof(int32_t) * (S + 2))) != hipSuccess ||
+            (e = hipMemset(h->fresh_q, 0, sizeof(int32_t) * (S + 2))) != hipSuccess ||
             (e = hipMemset(h->scn, 0, sizeof(d2d::Scn) * S)) != hipSuccess ||
             (e = hipMemset(h->brt, 0, sizeof(d2d::BrTab) * S)) != hipSuccess ||
             (e = hipMemset(h->abi, 0, sizeof(d2d_scn) * S)) != hipSuccess ||

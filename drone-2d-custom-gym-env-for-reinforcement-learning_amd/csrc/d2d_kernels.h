@@ -278,7 +278,6 @@ __device__ __forceinline__ int next_scenario(const StepArgs& a, int j, uint32_t 
 //   f_pre   W0 -> W2        velocity part of the reward (RewardVel)
 //   f_ver   W3 -> W2        first differing step in the second half of the table re-check
 struct K1Shared {
-    double acc[D2D_NSTATS][EPB];  // W3 -> W0: episode accumulators of envs that end (prefetched)
     double cas[6][EPB];       // W1 -> W0, W2: CAStatic (d, os, oc, lpa, lca, rr)
     int scn[EPB];             // scenario index per env
     uint32_t cause[EPB];      // W0 -> W1, W2, W3: end cause (0: the env keeps running)
@@ -297,6 +296,7 @@ struct K1Shared {
         struct {
             double pre[4][EPB];            // W0 -> W2: RewardVel
             double post[7][EPB];           // W2 -> W0: reward, pa, pp, dist, aa, coll, reach
+            double acc[D2D_NSTATS][EPB];   // W3 -> W0: episode accumulators of envs that end (prefetched)
             alignas(16) float obs[EPB * D2D_OBS_DIM];  // the workgroup's obs rows (16-B aligned: float4 stores)
         } p;                               // after f_gs
     } u;
@@ -673,10 +673,12 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const Scn* scns, cons
         flag_wait(sh.f_done);
         const bool cv = valid && sh.cvalid[lane] != 0u;
         if (valid) done = sh.cause[lane] != 0u;
+        double accp[D2D_NSTATS];
         if (valid && done) {
-            // finished-episode accumulators, read now so the epilogue does not wait on them
+            // finished-episode accumulators, read now so the epilogue does not wait on them (to LDS
+            // once the joint sweep's buffer is free, below)
 #pragma unroll
-            for (int k = 0; k < D2D_NSTATS; ++k) sh.acc[k][lane] = fld(a.acc, k, n, i);
+            for (int k = 0; k < D2D_NSTATS; ++k) accp[k] = fld(a.acc, k, n, i);
         }
         if (valid && done && auto_reset && !(D2D_ABL & 8)) {
             // the next episode: spawn state, reset observation (cached or computed), new state
@@ -712,6 +714,10 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const Scn* scns, cons
         STAMP(4);
         flag_wait(sh.f_gs);
         STAMP(5);
+        if (valid && done) {
+#pragma unroll
+            for (int k = 0; k < D2D_NSTATS; ++k) sh.u.p.acc[k][lane] = accp[k];
+        }
         if (valid && done && auto_reset) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) orow[19 + k] = (float)po[k];
@@ -781,14 +787,14 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const Scn* scns, cons
             // finished-episode accumulators (info counters of drone_2d_env.py:593-613)
             const bool c1 = cause & D2D_END_COLLISION, c2 = cause & D2D_END_REACH;
             const bool c4 = cause & D2D_END_TIMEUP, c5 = cause & D2D_END_AA;
-            fld(a.acc, D2D_ST_RETURN, n, i) = sh.acc[D2D_ST_RETURN][lane] + tot_rew;
-            fld(a.acc, D2D_ST_EPISODES, n, i) = sh.acc[D2D_ST_EPISODES][lane] + 1.0;
-            fld(a.acc, D2D_ST_SUCCESS, n, i) = sh.acc[D2D_ST_SUCCESS][lane] + (c2 ? 1.0 : 0.0);
-            fld(a.acc, D2D_ST_FAIL, n, i) = sh.acc[D2D_ST_FAIL][lane] + ((c1 || c4 || c5) ? 1.0 : 0.0);
+            fld(a.acc, D2D_ST_RETURN, n, i) = sh.u.p.acc[D2D_ST_RETURN][lane] + tot_rew;
+            fld(a.acc, D2D_ST_EPISODES, n, i) = sh.u.p.acc[D2D_ST_EPISODES][lane] + 1.0;
+            fld(a.acc, D2D_ST_SUCCESS, n, i) = sh.u.p.acc[D2D_ST_SUCCESS][lane] + (c2 ? 1.0 : 0.0);
+            fld(a.acc, D2D_ST_FAIL, n, i) = sh.u.p.acc[D2D_ST_FAIL][lane] + ((c1 || c4 || c5) ? 1.0 : 0.0);
             fld(a.acc, D2D_ST_COLLISION, n, i) =
-                sh.acc[D2D_ST_COLLISION][lane] + ((c1 && !c2 && !c4 && !c5) ? 1.0 : 0.0);
-            fld(a.acc, D2D_ST_APE, n, i) = sh.acc[D2D_ST_APE][lane] + ape;
-            fld(a.acc, D2D_ST_LEN, n, i) = sh.acc[D2D_ST_LEN][lane] + (double)t;
+                sh.u.p.acc[D2D_ST_COLLISION][lane] + ((c1 && !c2 && !c4 && !c5) ? 1.0 : 0.0);
+            fld(a.acc, D2D_ST_APE, n, i) = sh.u.p.acc[D2D_ST_APE][lane] + ape;
+            fld(a.acc, D2D_ST_LEN, n, i) = sh.u.p.acc[D2D_ST_LEN][lane] + (double)t;
         }
         if (!(done && auto_reset)) {
             fld(a.st, D2D_S_PATH_ERR, n, i) = path_err;
@@ -1068,7 +1074,8 @@ struct FreshArgs {
     int64_t* gclk;           // [2 n] clock at generation
     const int64_t* clock;    // the step clock (K1 advances it)
     int32_t* queue;          // [2 n] slots to generate (K5a -> K5b)
-    int32_t* qcount;         // [1] queue length (zeroed before K5a)
+    int32_t* qcount;         // [2] queue length (K5b's last workgroup to finish zeroes it again) and
+                             // K5b's finished-workgroup ticket
     int restore;
 };
 __global__ __launch_bounds__(256) void d2d_fresh_scan_kernel(FreshArgs f) {
@@ -1123,13 +1130,20 @@ __global__ __launch_bounds__(64) void d2d_fresh_gen_kernel(FreshArgs f) {
             for (int k = lane; k < (int)(sizeof(d2d_scn) / 8); k += 64) da[k] = sa[k];
         }
 #if !D2D_FRESH_NOTAB
-        if (lane < 2) brtab_build(G.s, lane, f.brt[slot]);  // kind = lane, from the LDS table
+        brtab_build_wave(G.s, f.brt[slot], G, lane);  // both kinds, from the LDS table
 #endif
         if (lane == 0) {
             f.gclk[slot] = clk;
             f.tag[slot] = key;
         }
         __syncthreads();  // G is reused by the next item
+    }
+    // every workgroup has read the queue length (above); the last one to finish resets it for the
+    // next K5a, so no memset is needed between launches
+    if (lane == 0 &&
+        __hip_atomic_fetch_add(&f.qcount[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1) {
+        __hip_atomic_store(&f.qcount[0], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&f.qcount[1], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 

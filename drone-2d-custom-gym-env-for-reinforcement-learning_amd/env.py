@@ -17,7 +17,7 @@ import numpy as np
 import torch
 
 from . import abi
-from ._native import LIB_PATH_RM, check, load
+from ._native import check, load
 from .config import CURRICULUM_STAGES, SCENARIO_STEP_COST, TEST_SCENARIOS, make_cfg
 from .scenarios import Scenario, create_test_scenario, free_flight
 
@@ -138,11 +138,8 @@ class Drone2dVecEnv:
                  native_lib: str | None = None, envs_total: int | None = None, **kwargs):
         self.kwargs = dict(kwargs)
         self.fresh = is_fresh_curriculum(self.kwargs)
-        # curriculum batches (fresh, or a pool of more than one scenario: two pool halves never fit
-        # K1's LDS) read each env's scenario from global memory: the record-major build of the same
-        # source (D2D_REC_RM=1, 1.7 x faster there); native_lib: an alternative build (diagnostics)
-        rm = is_curriculum(self.kwargs) and (self.fresh or int(self.kwargs.get("curriculum_pool") or 0) > 1)
-        self._lib = load(native_lib if native_lib is not None else (LIB_PATH_RM if rm else None))
+        # native_lib: an alternative build of the same source (diagnostic A/B builds only)
+        self._lib = load(native_lib)
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device())
         self.device = torch.device(device)

@@ -159,6 +159,12 @@ class OracleBatch:
             raise ValueError("scenario table range")
         return out
 
+    def set_curriculum(self, curriculum):
+        """d2dcpu_set_curriculum (as d2d_set_curriculum: empties the slots and zeroes the step clock)."""
+        self._cur = curriculum
+        if self.lib.d2dcpu_set_curriculum(self.h, C.byref(curriculum)) != 0:
+            raise ValueError("d2dcpu_set_curriculum: cfg.scn_pool must be 2")
+
     def fresh_recipes(self, keys=None, clocks=None, clock=None):
         """get (no arguments) -> (keys int32[2n], clocks int64[2n], clock); set with all three."""
         n2 = 2 * self.n

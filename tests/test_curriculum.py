@@ -205,3 +205,54 @@ def test_fresh_oracle_backend_every_episode_new(d2, oracle_mod):
     tab = be.orc.scenario_table(0, 2 * n)
     assert any(tab[s].spawn_xmin == 100.0 and tab[s].spawn_xmax == 1200.0 for s in range(2 * n))
     be.close()
+
+
+def _fresh_oracle(n, sim_num=0):
+    import oracle
+
+    import drone2d_amd  # noqa: F401
+    from drone2d_amd.config import ENV_TRAIN_CONFIG, make_cfg
+    from drone2d_amd.env import make_curriculum
+
+    kw = dict(ENV_TRAIN_CONFIG, mode="curriculum", scenario="curriculum", sim_num=sim_num)
+    cfg = make_cfg(dict(kw))
+    cfg.scn_pool = 2
+    return oracle.OracleBatch(cfg, [], n, curriculum=make_curriculum(kw, n)), kw
+
+
+def test_oracle_set_curriculum_restarts_clock():
+    """d2d_set_curriculum's contract, restated by the oracle: the step clock restarts at
+    zero, so the schedule starts at the new sim_num0, not at sim_num0 + the steps already taken."""
+    from drone2d_amd.env import make_curriculum
+
+    n = 16
+    orc, kw = _fresh_oracle(n)
+    orc.reset(3)
+    rng = np.random.default_rng(0)
+    for _ in range(7):
+        orc.step(rng.uniform(-1, 1, (n, 2)).astype(np.float32))
+    assert orc.fresh_recipes()[2] == 7
+    orc.set_curriculum(make_curriculum(dict(kw, sim_num=1_200_000), n))
+    assert orc.fresh_recipes()[2] == 0
+    orc.reset(3)
+    keys, clocks, clock = orc.fresh_recipes()
+    tab = orc.scenario_table(0, 2 * n)
+    for s in np.flatnonzero(keys >= 0):  # generated at clock 0 of sim_num 1.2e6: stage 3
+        assert clocks[s] == 0 and tab[s].n_circles <= 1 and tab[s].spawn_xmin == tab[s].spawn_xmax
+    orc.close()
+
+
+def test_oracle_masked_fresh_reset_keeps_seed():
+    """A masked fresh-curriculum reset must pass the previous full reset's seed (d2d_reset's rule):
+    the envs it leaves running would otherwise keep scenarios no (key, clock) recipe regenerates."""
+    n = 8
+    orc, _ = _fresh_oracle(n)
+    mask = np.zeros(n, np.uint8)
+    mask[::2] = 1
+    with pytest.raises(RuntimeError):
+        orc.reset(5, mask)  # no full reset yet
+    orc.reset(5)
+    with pytest.raises(RuntimeError):
+        orc.reset(6, mask)
+    orc.reset(5, mask)
+    orc.close()

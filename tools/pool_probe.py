@@ -14,7 +14,7 @@ from drone2d_amd.config import ENV_TRAIN_CONFIG  # noqa: E402
 pool = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 300
 n = 65536
-for lib in (_native.LIB_PATH, _native.LIB_PATH_RM):
+for lib in (_native.LIB_PATH,):
     venv = d2.Drone2dVecEnv(n, seed=0, with_info=False, native_lib=lib,
                             **dict(ENV_TRAIN_CONFIG, mode="curriculum", scenario="stage_3", curriculum_pool=pool))
     venv.reset(seed=0)
