@@ -258,19 +258,19 @@ __device__ inline void gen_curriculum(const d2d_curriculum& c, double W, double 
     s.spawn_amin = -PI / 4.0;
     s.spawn_amax = PI / 4.0;
     double chance;
-    const int st = gen_stage(c, sim, &chance);
-    if (st == 2) {  // drone spawned uniformly on the screen, no obstacles (:333-337)
+    const int stg = gen_stage(c, sim, &chance);
+    if (stg == 2) {  // drone spawned uniformly on the screen, no obstacles (:333-337)
         s.spawn_xmin = 100.0;
         s.spawn_xmax = W - 100.0;
         s.spawn_ymin = 100.0;
         s.spawn_ymax = H - 100.0;
     }
     scn_build(s, S);  // the path, for the obstacle placement
-    if (st == 3) {
+    if (stg == 3) {
         if (R.u01() < chance) gen_obstacles(R, S, s, 1.0, 0.0, 100.0, false);
-    } else if (st == 4) {
+    } else if (stg == 4) {
         if (R.u01() < chance) gen_obstacles(R, S, s, 1.0, 0.0, 0.0, true);
-    } else if (st == 5) {
+    } else if (stg == 5) {
         double n_obs = R.normal(1.0, 4.0);
         if (n_obs < 0.0 && n_obs > -3.0) n_obs = 1.0;
         if (n_obs < -3.0) n_obs = 0.0;
@@ -293,6 +293,14 @@ __device__ inline void gen_curriculum(const d2d_curriculum& c, double W, double 
 // operations on the same operands as gen_curriculum (so the tables stay bit-identical to the CPU
 // oracle's o_gen_curriculum); only the order in which independent values are computed changes.
 constexpr int GEN_WIN = 256;   // stream words precomputed per item (corner + waypoints + ~25 obstacle tries)
+
+// LDS hand-off between the lanes of ONE wave (each generator part below runs on a single wave of
+// K5b's workgroup, the other wave runs other code, so no workgroup barrier)
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
 
 // serial reader of one (seed, gid, key) stream: words below GEN_WIN from the LDS window, later blocks
 // computed on demand (the same block formula as GenRng)
@@ -339,8 +347,8 @@ struct GenStream {
 };
 __device__ __forceinline__ double win_u01(const uint32_t* w, int p) { return u53(w[p], w[p + 1]); }
 
-// scn_build with interval n on lane n and circle k on lane k (scalars and r_uniform on lane 0)
-__device__ inline void scn_build_lanes(const d2d_scn& a, Scn& s, int lane) {
+// scn_build with interval n on lane n (the path part: knots, interval records, n_wps) ...
+__device__ inline void scn_build_path_lanes(const d2d_scn& a, Scn& s, int lane) {
     const int nw = a.n_wps, nseg = nw - 2;
     if (lane < D2D_MAX_WPS) {
         const int n = lane;
@@ -360,13 +368,16 @@ __device__ inline void scn_build_lanes(const d2d_scn& a, Scn& s, int lane) {
         const double last_lo = a.us[nw - 2] - 0.001;
         SREC(s, REC_T, n) = (n == 0) ? (us0 < last_lo ? us0 : last_lo) : (n < nw - 1 ? last_lo : -__builtin_inf());
     }
+    if (lane == 0) s.n_wps = nw;
+}
+// ... and the rest: circle k on lane k, the scalars and r_uniform on lane 0
+__device__ inline void scn_build_rest_lanes(const d2d_scn& a, Scn& s, int lane) {
     if (lane < D2D_MAX_CIRCLES) {
         s.cx[lane] = a.cx[lane];
         s.cy[lane] = a.cy[lane];
         s.cr[lane] = a.cr[lane];
     }
     if (lane == 0) {
-        s.n_wps = nw;
         s.n_circles = a.n_circles;
         s.wp_last_x = a.wp_last_x;
         s.wp_last_y = a.wp_last_y;
@@ -394,10 +405,12 @@ struct GenLds {
     // golden-march table build (brtab_build_wave): per kind, the probes and their knot intervals
     double bx[2][BT_K + 1], bk[2][BT_K + 1];
     int32_t bix[2][BT_K + 1], bta[2][BT_K], blen[2];
+    alignas(16) BrTab t;       // the tables, built here and copied out whole
     // obstacle placement (gen_obstacles_wave): the trial that starts at stream word w0 + 2 l, per lane l
     double ox[64], oy[64], osz[64];
     int32_t ook[64], ocons[64];
     int32_t wpos;            // the stream position after the obstacle calls
+    uint32_t fpath;          // K5b: wave 0 -> wave 1, G.s's path part is built (the tables may start)
 };
 
 // generate_obstacles_around_path (gen_obstacles) with the wave: one rejection trial is a pure function
@@ -433,7 +446,7 @@ __device__ inline void gen_obstacles_wave(GenLds& G, uint64_t seed, uint32_t gid
             G.ook[lane] = ok ? 1 : 0;
             G.ocons[lane] = R.pos - (w + 2 * lane);
         }
-        __syncthreads();
+        wave_sync();
         if (lane == 0) {
             const int w0 = w;
             while ((double)num < n && s.n_circles < D2D_MAX_CIRCLES && tries < 4096 && w < w0 + 128) {
@@ -451,25 +464,41 @@ __device__ inline void gen_obstacles_wave(GenLds& G, uint64_t seed, uint32_t gid
             G.ook[0] = ((double)num < n && s.n_circles < D2D_MAX_CIRCLES && tries < 4096) ? 1 : 0;
             G.ocons[0] = w;
         }
-        __syncthreads();
+        wave_sync();
         more = G.ook[0] != 0;
         w = G.ocons[0];
-        __syncthreads();  // (G.ook / G.ocons are rewritten by the next round)
+        wave_sync();  // (G.ook / G.ocons are rewritten by the next round)
     }
     if (lane == 0) G.wpos = w;
-    __syncthreads();
+    wave_sync();
 }
 
-// one curriculum reset by the calling wave (all 64 lanes, wave-uniform arguments); the result is in
-// G.a / G.s (LDS).  Same draws and arithmetic as gen_curriculum.
-__device__ inline void gen_curriculum_wave(const d2d_curriculum& c, double W, double H, uint64_t seed, uint32_t gid,
-                                           uint32_t key, double sim, GenLds& G, int lane) {
+// one curriculum reset by the calling wave (all 64 lanes, wave-uniform arguments) in two parts: the
+// path (gen_path_wave: waypoints, fit, G.s's knots and interval records -- all the golden-march tables
+// need) and the rest (gen_rest_wave: stage fields, obstacles, G.s's circles and scalars).  The result
+// is in G.a / G.s (LDS).  Same draws and arithmetic as gen_curriculum.
+#ifdef D2D_GEN_STAMPS  // diagnostic builds only: s_memtime at K5b's phase boundaries, 8 per item
+#define GSTAMP(st, k)                                                   \
+    do {                                                                \
+        if ((st) && lane == 0) (st)[k] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
+#else
+#define GSTAMP(st, k) \
+    do {              \
+    } while (0)
+#endif
+// returns the stream position of the first draw after the azimuths
+__device__ inline int gen_path_wave(const d2d_curriculum& c, double W, double H, uint64_t seed, uint32_t gid,
+                                    uint32_t key, GenLds& G, int lane, uint64_t* st = nullptr) {
+    (void)st;
+    GSTAMP(st, 0);
     {
         uint32_t o[4];
         philox(gid, key, GEN_TAG + (uint32_t)lane, 0u, (uint32_t)seed, (uint32_t)(seed >> 32), o);
         for (int k = 0; k < 4; ++k) G.win[4 * lane + k] = o[k];
     }
-    __syncthreads();
+    wave_sync();
+    GSTAMP(st, 1);
     // stream positions (words) of the fixed-count draws: corner (random.randint), wx0, wy0, azimuths
     int p = 0;
     int corner = 2;
@@ -498,7 +527,7 @@ __device__ inline void gen_curriculum_wave(const d2d_curriculum& c, double W, do
         G.sa[lane] = sa;
         G.ca[lane] = ca;
     }
-    __syncthreads();
+    wave_sync();
     if (lane == 0) {
         G.wx[0] = x0lo + (x0hi - x0lo) * win_u01(G.win, p);
         G.wy[0] = y0lo + (y0hi - y0lo) * win_u01(G.win, p + 2);
@@ -507,7 +536,7 @@ __device__ inline void gen_curriculum_wave(const d2d_curriculum& c, double W, do
             G.wy[i + 1] = G.wy[i] + c.segment_length * G.sa[i];
         }
     }
-    __syncthreads();
+    wave_sync();
     // gen_fit: segment lengths (lanes), arc length prefix sum (lane 0), the fits (lanes)
     d2d_scn& s = G.a;
     if (lane + 1 < nw) {
@@ -516,7 +545,7 @@ __device__ inline void gen_curriculum_wave(const d2d_curriculum& c, double W, do
     }
     if (lane < D2D_MAX_SEGS && lane >= nw - 2) s.xa[lane] = s.xb[lane] = s.xc[lane] = s.ya[lane] = s.yb[lane] = s.yc[lane] = 0.0;
     if (lane >= nw && lane < D2D_MAX_WPS) s.us[lane] = 0.0;
-    __syncthreads();
+    wave_sync();
     if (lane == 0) {
         s.n_wps = nw;
         double acc = 0.0;
@@ -526,7 +555,7 @@ __device__ inline void gen_curriculum_wave(const d2d_curriculum& c, double W, do
             s.us[i + 1] = acc;
         }
     }
-    __syncthreads();
+    wave_sync();
     {
         // lanes 0..nw-3: the x fit of interior waypoint n = lane + 1; lanes 32..32+nw-3: the y fit
         const int n = (lane & 31) + 1;
@@ -553,8 +582,19 @@ __device__ inline void gen_curriculum_wave(const d2d_curriculum& c, double W, do
             }
         }
     }
+    wave_sync();
+    scn_build_path_lanes(s, G.s, lane);
+    wave_sync();
+    GSTAMP(st, 2);
+    return paz + 2 * (nw - 1);
+}
+__device__ inline void gen_rest_wave(const d2d_curriculum& c, double W, double H, uint64_t seed, uint32_t gid,
+                                     uint32_t key, double sim, int pos, GenLds& G, int lane, uint64_t* st = nullptr) {
+    (void)st;
+    d2d_scn& s = G.a;
+    const int nw = s.n_wps;
     double chance;
-    const int st = gen_stage(c, sim, &chance);
+    const int stg = gen_stage(c, sim, &chance);
     if (lane == 0) {
         s.n_circles = 0;
         s.wp_last_x = G.wx[nw - 1];
@@ -563,7 +603,7 @@ __device__ inline void gen_curriculum_wave(const d2d_curriculum& c, double W, do
         s.spawn_ymin = s.spawn_ymax = G.wy[0];
         s.spawn_amin = -PI / 4.0;
         s.spawn_amax = PI / 4.0;
-        if (st == 2) {  // drone spawned uniformly on the screen, no obstacles (:333-337)
+        if (stg == 2) {  // drone spawned uniformly on the screen, no obstacles (:333-337)
             s.spawn_xmin = 100.0;
             s.spawn_xmax = W - 100.0;
             s.spawn_ymin = 100.0;
@@ -571,16 +611,16 @@ __device__ inline void gen_curriculum_wave(const d2d_curriculum& c, double W, do
         }
     }
     if (lane < D2D_MAX_CIRCLES) s.cx[lane] = s.cy[lane] = s.cr[lane] = 0.0;
-    __syncthreads();
-    if (st >= 3 && !(D2D_ABLATE & 128)) {  // (128: diagnostic timing builds skip the obstacles)
-        scn_build_lanes(s, G.s, lane);  // the path, for the obstacle placement
-        // the draws before the obstacle calls (lane 0), then the calls (gen_obstacles_wave)
+    wave_sync();
+    if (stg >= 3 && !(D2D_ABLATE & 128)) {  // (128: diagnostic timing builds skip the obstacles)
+        // the draws before the obstacle calls (lane 0), then the calls (gen_obstacles_wave; the path
+        // in G.s is already built)
         __shared__ double s_nobs;
         if (lane == 0) {
             GenStream R;
-            R.init(G.win, seed, gid, key, paz + 2 * (nw - 1));
+            R.init(G.win, seed, gid, key, pos);
             double n_obs = 0.0;
-            if (st == 3 || st == 4) {
+            if (stg == 3 || stg == 4) {
                 n_obs = (R.u01() < chance) ? 1.0 : 0.0;
             } else {
                 n_obs = R.normal(1.0, 4.0);
@@ -590,31 +630,38 @@ __device__ inline void gen_curriculum_wave(const d2d_curriculum& c, double W, do
             s_nobs = n_obs;
             G.wpos = R.pos;
         }
-        __syncthreads();
+        wave_sync();
         const double n_obs = s_nobs;
-        if (st == 3) {
+        if (stg == 3) {
             if (n_obs != 0.0) gen_obstacles_wave(G, seed, gid, key, 1.0, 0.0, 100.0, false, lane);
-        } else if (st == 4) {
+        } else if (stg == 4) {
             if (n_obs != 0.0) gen_obstacles_wave(G, seed, gid, key, 1.0, 0.0, 0.0, true, lane);
         } else if (n_obs != 0.0) {
             gen_obstacles_wave(G, seed, gid, key, n_obs, 0.0, 100.0, false, lane);
             gen_obstacles_wave(G, seed, gid, key, 1.0, 0.0, 0.0, true, lane);
         }
     }
-    scn_build_lanes(s, G.s, lane);
-    __syncthreads();
+    GSTAMP(st, 4);
+    scn_build_rest_lanes(s, G.s, lane);
+    wave_sync();
+    GSTAMP(st, 5);
 }
 
 
-// brtab_build for both kinds with the wave (d2d_device.h: the forced runs).  The forced decisions make
-// the search's floating-point state (a, b, fulc, nfc, xf, e, rat) a function of the step number alone,
-// so lanes 0 and 1 (kind = lane) first run that recurrence with no path evaluation, recording each
-// step's probe; then every lane evaluates probes (knot interval + QPMI2D point), independent of each
-// other; then lanes 0 and 1 replay the interval bookkeeping (ia, ka, ib, ixf, kxf) from the probes'
-// intervals.  Every stored value is computed by the same operations as in brtab_build, so the tables
-// are identical to it.
+// brtab_build for both kinds with the wave (d2d_device.h: the forced runs), built in LDS (G.t) and
+// copied out with the whole wave.  The forced decisions make the search's floating-point state (a, b,
+// fulc, nfc, xf, e, rat) a function of the step number alone, so lanes 0 and 1 (kind = lane) first run
+// that recurrence with no path evaluation, recording each step's probe; then every lane evaluates
+// probes (knot interval + QPMI2D point), independent of each other; then lane k of each kind derives
+// the interval bookkeeping (ia, ka, ib, ixf, kxf) before step k in closed form: ixf / kxf are the
+// latest probe's (the forced run's xf is always the newest probe, except after kind 0's first step),
+// ia / ka the value the last step j < k with to_a[j] moved a to, ib that of the last step without
+// (ballot masks of to_a, highest set bit below k).  Every stored value is computed by the same
+// operations as in brtab_build, so the tables are identical to it.  (A single lane storing the
+// tables straight to global memory ran into the wave's limit of outstanding stores: ~900 of them.)
 __device__ inline void brtab_build_wave(const Scn& s, BrTab& T, GenLds& G, int lane) {
     const PathK K = path_k(s);
+    BrTab& W = G.t;
     if (lane < 2) {
         const int kind = lane;
         double a = 0.0 - 10.0, b = K.L + 10.0;
@@ -622,7 +669,7 @@ __device__ inline void brtab_build_wave(const Scn& s, BrTab& T, GenLds& G, int l
         double nfc = fulc, xf = fulc, rat = 0.0, e = 0.0;
         int num = 1, jf = 0, jn = 0, jx = 0;
         G.bx[kind][0] = xf;
-        BtIt& h0 = T.hot.it[kind][0];
+        BtIt& h0 = W.hot.it[kind][0];
         h0.dxn = h0.dxf = h0.e = h0.am = h0.bm = h0.pad = 0.0;
         int k = 0;
         for (; k < BT_K; ++k) {
@@ -632,12 +679,12 @@ __device__ inline void brtab_build_wave(const Scn& s, BrTab& T, GenLds& G, int l
                 const double t2 = 2.0 * t1;
                 if (!((fabs(xf - xm0) > (t2 - 0.5 * (b - a))) & (num < 500))) break;  // brent_active
             }
-            BtSnap& S = T.snap[kind][k];
+            BtSnap& S = W.snap[kind][k];
             S.a = a; S.b = b; S.fulc = fulc; S.nfc = nfc; S.xf = xf; S.rat = rat; S.e = e;
             S.num = num; S.j_fulc = jf; S.j_nfc = jn; S.j_xf = jx; S.pad = 0;
             const double xm = 0.5 * (a + b);
             const double tol1 = BR_SQRT_EPS * fabs(xf) + BR_XATOL3;
-            BtIt& h = T.hot.it[kind][k + 1];
+            BtIt& h = W.hot.it[kind][k + 1];
             h.dxn = xf - nfc;
             h.dxf = xf - fulc;
             h.e = (fabs(e) > tol1) ? e : 0.0;
@@ -671,51 +718,70 @@ __device__ inline void brtab_build_wave(const Scn& s, BrTab& T, GenLds& G, int l
             jn = njn;
             jx = le ? j : jx;
         }
-        BtSnap& S = T.snap[kind][k];
+        BtSnap& S = W.snap[kind][k];
         S.a = a; S.b = b; S.fulc = fulc; S.nfc = nfc; S.xf = xf; S.rat = rat; S.e = e;
         S.num = num; S.j_fulc = jf; S.j_nfc = jn; S.j_xf = jx; S.pad = 0;
         G.blen[kind] = k;
-        T.len[kind] = k;
+        W.len[kind] = k;
+        W.pad[kind] = 0;
     }
-    __syncthreads();
-    // every probe j <= len of both kinds: knot interval, path point, upper knot
+    wave_sync();
+    // every probe j <= len of both kinds: knot interval, path point, upper knot; entries past len zeroed
     const int n0 = G.blen[0] + 1, n1 = G.blen[1] + 1;
-    for (int q = lane; q < n0 + n1; q += 64) {
-        const int kind = q < n0 ? 0 : 1, j = q < n0 ? q : q - n0;
-        const double x = G.bx[kind][j];
-        const int ix = u_index(s, x);
-        double X, Y, kx;
-        path_eval_n(s, K, x, ix, X, Y, kx);
-        BtIt& h = T.hot.it[kind][j];
-        h.X = X;
-        h.Y = Y;
-        G.bix[kind][j] = ix;
-        G.bk[kind][j] = kx;
-    }
-    __syncthreads();
-    if (lane < 2) {
-        const int kind = lane, len = G.blen[kind];
-        int ia = u_index(s, 0.0 - 10.0), ib = u_index(s, K.L + 10.0);
-        double ka = SREC(s, REC_U1, ia);
-        int ixf = G.bix[kind][0];
-        double kxf = G.bk[kind][0];
-        for (int k = 0; k <= len; ++k) {
-            BtSnap& S = T.snap[kind][k];
-            S.ka = ka; S.kxf = kxf; S.ia = ia; S.ib = ib; S.ixf = ixf;
-            if (k == len) break;
-            const bool le = !(kind == 0 && k == 0);
-            const bool to_a = G.bta[kind][k] != 0;
-            const int ix = G.bix[kind][k + 1];
-            const double kx = G.bk[kind][k + 1];
-            const int ti = le ? ixf : ix;
-            const double tk = le ? kxf : kx;
-            ia = to_a ? ti : ia;
-            ka = to_a ? tk : ka;
-            ib = to_a ? ib : ti;
-            ixf = le ? ix : ixf;
-            kxf = le ? kx : kxf;
+    for (int q = lane; q < 2 * BT_HOT; q += 64) {
+        const int kind = q < BT_HOT ? 0 : 1, j = q < BT_HOT ? q : q - BT_HOT;
+        BtIt& h = W.hot.it[kind][j];
+        if (j < (kind ? n1 : n0)) {
+            const double x = G.bx[kind][j];
+            const int ix = u_index(s, x);
+            double X, Y, kx;
+            path_eval_n(s, K, x, ix, X, Y, kx);
+            h.X = X;
+            h.Y = Y;
+            G.bix[kind][j] = ix;
+            G.bk[kind][j] = kx;
+        } else {
+            h = BtIt{0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
         }
     }
+    wave_sync();
+    {
+        const int ia0 = u_index(s, 0.0 - 10.0), ib0 = u_index(s, K.L + 10.0);
+        const double ka0 = SREC(s, REC_U1, ia0);
+        for (int kind = 0; kind < 2; ++kind) {
+            const int len = G.blen[kind], k = lane;
+            const bool ta = (k < len) && G.bta[kind][k] != 0;
+            const uint64_t mA = __ballot(ta), mB = __ballot((k < len) && !ta);
+            if (k <= len) {
+                // (ti, tk) of step j: kind 0's first step moves to its own probe; otherwise the probe
+                // xf held before the step (probe j, except kind 0's step 1: the initial point)
+                auto tix = [&](int j) { return (kind == 0 && j == 0) ? 1 : ((kind == 0 && j == 1) ? 0 : j); };
+                const uint64_t below = (1ull << k) - 1ull;  // (k <= BT_K < 64)
+                const uint64_t ma = mA & below, mb = mB & below;
+                int ia = ia0, ib = ib0;
+                double ka = ka0;
+                if (ma) {
+                    const int jj = tix(63 - __clzll((long long)ma));
+                    ia = G.bix[kind][jj];
+                    ka = G.bk[kind][jj];
+                }
+                if (mb) ib = G.bix[kind][tix(63 - __clzll((long long)mb))];
+                const int jx = (kind == 0 && k == 1) ? 0 : k;
+                BtSnap& S = W.snap[kind][k];
+                S.ka = ka;
+                S.kxf = G.bk[kind][jx];
+                S.ia = ia;
+                S.ib = ib;
+                S.ixf = G.bix[kind][jx];
+            }
+        }
+    }
+    wave_sync();
+    // the table to global memory, 16-byte words across the wave
+    static_assert(sizeof(BrTab) % 16 == 0, "BrTab size");
+    const uint4* src = reinterpret_cast<const uint4*>(&W);
+    uint4* dst = reinterpret_cast<uint4*>(&T);
+    for (int q = lane; q < (int)(sizeof(BrTab) / 16); q += 64) dst[q] = src[q];
 }
 
 }  // namespace d2d

@@ -32,6 +32,9 @@
 // the product is always built with 0): 1 skip Brent, 2 skip sensing, 4 skip joint iterations,
 // 8 skip collision test, 16 skip the Brent continuation after the golden-march tables, 128 the fresh
 // curriculum generator skips the obstacles.
+#ifndef D2D_RECPF
+#define D2D_RECPF 0  // A/B: brent_step prefetches a's interval record (see there)
+#endif
 #ifndef D2D_ABLATE
 #define D2D_ABLATE 0
 #endif
@@ -359,6 +362,13 @@ __device__ __forceinline__ void brent_step(const Scn& s, const PathK& K, double 
     // the upper knot of a's interval, for the one-compare interval test.  (Carrying it in the state,
     // or prefetching a's whole record before the candidate is known, measured no faster.)
     const double ka = SREC(s, REC_U1, B.ia);
+#if D2D_RECPF
+    // A/B (tables in global memory): a's record, loaded before the probe is known (the probe's interval
+    // is a's in most late steps), so the path evaluation waits on one memory round trip instead of two
+    double rpf[REC_N];
+#pragma unroll
+    for (int f = 0; f < REC_N; ++f) rpf[f] = SREC(s, f, B.ia);
+#endif
     const double xm = 0.5 * (a + b);
     const double tol1 = BR_SQRT_EPS * fabs(xf) + BR_XATOL3;
     const double tol2 = 2.0 * tol1;
@@ -407,7 +417,17 @@ __device__ __forceinline__ void brent_step(const Scn& s, const PathK& K, double 
         ix = u_index(*sp, x);
     }
     double kx;
+#if D2D_RECPF
+    if (ix != B.ia) {
+#pragma unroll
+        for (int f = 0; f < REC_N; ++f) rpf[f] = SREC(s, f, ix);
+    }
+    double xx, yy;
+    path_eval_rec(rpf, K, x, ix, xx, yy, kx);
+    const double fu = norm2(xx - px, yy - py);
+#else
     const double fu = path_dist_n(s, K, x, ix, px, py, kx);
+#endif
     B.num += 1;
     const bool le = fu <= fx;
     const bool c1 = !le & ((fu <= B.fnfc) | (nfc == xf));
@@ -462,8 +482,11 @@ __device__ __forceinline__ double closest_u(const Scn& s, double px, double py, 
 //      (its fx / fnfc / ffulc are the distances at recorded probes) and continues with brent_step.
 // Both stages perform exactly the operations brent_step performs on the same operands, so the
 // result is bit-identical to closest_u for every point (tests/test_gpu_parity.py grid test).
+#ifndef D2D_BT_MASK
+#define D2D_BT_MASK 1  // exec-masked table loads in the re-check (global-memory tables only; A/B: 0)
+#endif
 constexpr int BT_K = 48;    // recorded steps per kind (longer marches continue in brent_step)
-constexpr int BT_HOT = BT_K + 4;  // probe entries per kind: 0..BT_K, plus zero entries the 3-step
+constexpr int BT_HOT = BT_K + 3;  // probe entries per kind: 0..BT_K, plus zero entries the 3-step
                                   // unrolled check may read past a table's end
 struct BtIt {             // probe j (0: the initial point; k + 1: the probe of step k) + step k's operands
     double X, Y;          // path(probe)
@@ -635,8 +658,19 @@ __device__ __forceinline__ void bt_verify(const BtHot* hot, BtLane& L, int k0, i
     int dev = L.dev;
     const int kind = L.kind;
     for (int k = k0; __ballot(k < min(dev, k1)) != 0ull; k += 3) {
+#if D2D_BT_MASK
+        // tables in global memory (a lane's own scenario): a lane that is done loads nothing, so a
+        // wave's long marches do not drag every lane's table lines in from HBM
+        BtIt ha{}, hb{}, hc{};
+        if (LT || k < min(dev, k1)) {
+            ha = bt_hot<LT>(hot, kind, k + 1);
+            hb = bt_hot<LT>(hot, kind, k + 2);
+            hc = bt_hot<LT>(hot, kind, k + 3);
+        }
+#else
         const BtIt ha = bt_hot<LT>(hot, kind, k + 1), hb = bt_hot<LT>(hot, kind, k + 2),
                    hc = bt_hot<LT>(hot, kind, k + 3);
+#endif
         const double fd = bt_check(ha, k, px, py, fa, fb, fc, dev);
         const double fe = bt_check(hb, k + 1, px, py, fb, fc, fd, dev);
         const double ff = bt_check(hc, k + 2, px, py, fc, fd, fe, dev);

@@ -108,11 +108,18 @@ StepArgs make_args(const d2d_t* h) {
     a.wg_scn = h->wg_scn;
     a.scn_tag = h->scn_tag;
     a.clock = h->clock;
+    if (D2D_K1_QUEUE && h->cfg.scn_pool == 2 && h->fresh_q) {
+        a.fq = h->fresh_q;
+        a.fqc = h->fresh_q + 2 * (size_t)h->n;
+    }
     return a;
 }
 
+#ifndef D2D_GEN_GRID
+#define D2D_GEN_GRID 2048  // K5b workgroups (A/B)
+#endif
 // K5: the fresh curriculum's scenario slots (restore: every slot from its recipe), on `stream`
-hipError_t fresh_regen(d2d_t* h, hipStream_t stream, bool restore = false) {
+hipError_t fresh_regen(d2d_t* h, hipStream_t stream, bool restore = false, bool queued = false) {
     FreshArgs f{};
     f.n = h->n;
     f.ist = h->ist;
@@ -131,11 +138,15 @@ hipError_t fresh_regen(d2d_t* h, hipStream_t stream, bool restore = false) {
     f.queue = h->fresh_q;
     f.qcount = h->fresh_q + 2 * (size_t)h->n;
     f.restore = restore ? 1 : 0;
+#ifdef D2D_GEN_STAMPS
+    f.stamps = h->stamps;
+#endif
     const int items = restore ? 2 * h->n : h->n;
-    hipLaunchKernelGGL(d2d_fresh_scan_kernel, dim3((items + 255) / 256), dim3(256), 0, stream, f);
-    // one wave per queued slot: ~90 per step at 65 536 envs; a reset queues every env (the grid's
+    if (!queued) hipLaunchKernelGGL(d2d_fresh_scan_kernel, dim3((items + 255) / 256), dim3(256), 0, stream, f);
+    // one two-wave workgroup per queued slot: ~800 per step at 65 536 envs stepped with random
+    // actions (the items of the step all run at once); a reset queues every env (the grid's
     // workgroups then take several each)
-    hipLaunchKernelGGL(d2d_fresh_gen_kernel, dim3(std::min(items, 2048)), dim3(64), 0, stream, f);
+    hipLaunchKernelGGL(d2d_fresh_gen_kernel, dim3(std::min(items, D2D_GEN_GRID)), dim3(D2D_GEN_ONEWAVE ? 64 : 128), 0, stream, f);
     return hipGetLastError();
 }
 bool fresh_mode(const d2d_t* h) { return h->cfg.scn_pool == 2; }
@@ -437,7 +448,7 @@ void d2d_destroy(d2d_t* h) {
 
 int32_t d2d_n_envs(const d2d_t* h) { return h ? h->n : -1; }
 
-#ifdef D2D_STAMPS
+#if defined(D2D_STAMPS) || defined(D2D_GEN_STAMPS)
 // diagnostic builds only: K1 writes 8 s_memtime stamps per wave into buf ([n_blocks*4][8] u64)
 int32_t d2d_debug_stamps(d2d_t* h, uint64_t* buf) {
     if (!h) return fail(D2D_E_ARG, "d2d_debug_stamps: null handle");
@@ -675,7 +686,8 @@ int32_t d2d_step(d2d_t* h, const float* act_dev, float* obs_dev, float* rew_dev,
     }
     e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "d2d_step launch");
-    if (fresh_mode(h) && (e = fresh_regen(h, (hipStream_t)stream)) != hipSuccess)
+    if (fresh_mode(h) && (e = fresh_regen(h, (hipStream_t)stream, false, D2D_K1_QUEUE && h->cfg.auto_reset)) !=
+                             hipSuccess)
         return hip_fail(e, "d2d_step: fresh scenarios");
     if (h->cfg.auto_reset && ++h->n_steps % FILL_PERIOD == 0 &&
         (e = rc_fill(h, (hipStream_t)stream)) != hipSuccess)
@@ -956,6 +968,35 @@ int32_t d2d_get_scenario_table(d2d_t* h, int32_t first, int32_t count, d2d_scn* 
     if ((e = hipDeviceSynchronize()) != hipSuccess ||
         (e = hipMemcpy(out, h->abi + first, sizeof(d2d_scn) * (size_t)count, hipMemcpyDeviceToHost)) != hipSuccess)
         return hip_fail(e, "d2d_get_scenario_table");
+    return D2D_OK;
+}
+
+int32_t d2d_check_tables(d2d_t* h, uint64_t* mismatches) {
+    if (!h || !mismatches) return fail(D2D_E_ARG, "d2d_check_tables: null handle/out");
+    if (!h->brt || !h->scn) return fail(D2D_E_STATE, "d2d_check_tables: no tables");
+    DeviceGuard g(h->device);
+    const int ns = h->n_scn;
+    d2d::BrTab* ref = nullptr;
+    unsigned long long* bad = nullptr;
+    hipError_t e;
+    if ((e = hipDeviceSynchronize()) != hipSuccess || (e = hipMalloc(&ref, sizeof(d2d::BrTab) * (size_t)ns)) != hipSuccess ||
+        (e = hipMemset(ref, 0, sizeof(d2d::BrTab) * (size_t)ns)) != hipSuccess ||
+        (e = hipMalloc(&bad, sizeof(unsigned long long))) != hipSuccess ||
+        (e = hipMemset(bad, 0, sizeof(unsigned long long))) != hipSuccess) {
+        if (ref) (void)hipFree(ref);
+        if (bad) (void)hipFree(bad);
+        return hip_fail(e, "d2d_check_tables: alloc");
+    }
+    hipLaunchKernelGGL(d2d_brtab_kernel, dim3((2 * ns + 63) / 64), dim3(64), 0, 0, h->scn, ns, ref);
+    hipLaunchKernelGGL(d2d_brtab_cmp_kernel, dim3((2 * ns + 255) / 256), dim3(256), 0, 0, h->brt, ref, ns,
+                       fresh_mode(h) ? h->scn_tag : nullptr, bad);
+    unsigned long long c = 0;
+    if ((e = hipGetLastError()) == hipSuccess && (e = hipDeviceSynchronize()) == hipSuccess)
+        e = hipMemcpy(&c, bad, sizeof(c), hipMemcpyDeviceToHost);
+    (void)hipFree(ref);
+    (void)hipFree(bad);
+    if (e != hipSuccess) return hip_fail(e, "d2d_check_tables");
+    *mismatches = c;
     return D2D_OK;
 }
 

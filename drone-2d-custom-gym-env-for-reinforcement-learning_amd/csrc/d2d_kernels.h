@@ -99,6 +99,10 @@ struct StepArgs {
     // reset observation only once its scenario exists) and the step clock K1 advances
     const int32_t* scn_tag;   // [2 n]
     int64_t* clock;           // [1]
+    // ... and K5's queue: K1 appends the slot of the episode after next of every env it resets
+    // (D2D_K1_QUEUE; null: K5a scans for them)
+    int32_t* fq;              // [2 n] slots
+    int32_t* fqc;             // [0]: queue length
 };
 
 // Auto-reset observation cache.  The observation an env gets when it auto-resets depends only on
@@ -112,6 +116,15 @@ struct StepArgs {
 #ifndef D2D_ABL
 #define D2D_ABL 0        // diagnostic builds only: bit r skips role r's compute, bit 4 = perfect
                          // reset cache (no fills, every entry taken as ready): timing ablations
+#endif
+#ifndef D2D_GEN_ONEWAVE
+#define D2D_GEN_ONEWAVE 0  // A/B: K5b as one wave per slot (tables after the scenario)
+#endif
+#ifndef D2D_K1_QUEUE
+#define D2D_K1_QUEUE 1  // K1 queues the fresh curriculum's slots itself (no K5a scan per step; A/B: 0)
+#endif
+#ifndef D2D_GLOBAL_NOSPLIT
+#define D2D_GLOBAL_NOSPLIT 1  // tables in global memory: W2 re-checks the whole table, W3 none (A/B: 0)
 #endif
 #ifndef D2D_FRESH_NOTAB
 #define D2D_FRESH_NOTAB 0  // diagnostic A/B builds only: fresh curriculum without golden-march tables
@@ -288,6 +301,7 @@ struct K1Shared {
     double sina[EPB];         // W0 -> W2: sin of the post-step frame angle (AA reward)
     uint32_t f_done, f_ca, f_gs, f_pre, f_ver, f_ver1;
     double pe[2][EPB];        // W3 -> W0: path_err, total_reward (prefetched for the epilogue)
+    double acc[D2D_NSTATS][EPB];  // W3 -> W0: episode accumulators of envs that end (prefetched)
     union {
         struct {
             double jb[6 * JB_PER_JOINT][EPB];  // W0's joint sweep: per-joint K^-1 + bias
@@ -296,7 +310,6 @@ struct K1Shared {
         struct {
             double pre[4][EPB];            // W0 -> W2: RewardVel
             double post[7][EPB];           // W2 -> W0: reward, pa, pp, dist, aa, coll, reach
-            double acc[D2D_NSTATS][EPB];   // W3 -> W0: episode accumulators of envs that end (prefetched)
             alignas(16) float obs[EPB * D2D_OBS_DIM];  // the workgroup's obs rows (16-B aligned: float4 stores)
         } p;                               // after f_gs
     } u;
@@ -587,7 +600,8 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const Scn* scns, cons
                 // golden-march re-check of steps [1, split); W3 checks [split, len) meanwhile
                 const BtHot* hot = LTAB ? hots + sh.scn[lane] : &T->hot;
                 BtLane L = bt_start<LTAB>(*T, hot, F.px, F.py);
-                bt_verify<LTAB>(hot, L, 1, S3 ? bt_third(*T, 1) : bt_split(*T), F.px, F.py);
+                bt_verify<LTAB>(hot, L, 1, (D2D_GLOBAL_NOSPLIT && !LDS) ? BT_K : S3 ? bt_third(*T, 1) : bt_split(*T),
+                                F.px, F.py);
                 flag_wait(sh.f_ver);
                 if (S3) flag_wait(sh.f_ver1);
                 L.dev = min(L.dev, (int)sh.pflags[lane]);
@@ -647,7 +661,9 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const Scn* scns, cons
         // ---------------------------------------------------------------- auto-reset observation
         __builtin_amdgcn_s_setprio(PRIO_W2);  // the re-check below is on W2's critical path
         double po[8];
-        if (valid && !(D2D_ABL & 4) && !(D2D_ABLATE & 1) && a.brt) {
+        if (D2D_GLOBAL_NOSPLIT && !LDS) {
+            sh.pflags[lane] = 0x7fffffffu;
+        } else if (valid && !(D2D_ABL & 4) && !(D2D_ABLATE & 1) && a.brt) {
             // second half of W2's golden-march re-check (its first wave-priority work)
             const BrTab& T = a.brt[sh.scn[lane]];
             const BtHot* hot = LTAB ? hots + sh.scn[lane] : &T.hot;
@@ -673,12 +689,10 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const Scn* scns, cons
         flag_wait(sh.f_done);
         const bool cv = valid && sh.cvalid[lane] != 0u;
         if (valid) done = sh.cause[lane] != 0u;
-        double accp[D2D_NSTATS];
         if (valid && done) {
-            // finished-episode accumulators, read now so the epilogue does not wait on them (to LDS
-            // once the joint sweep's buffer is free, below)
+            // finished-episode accumulators, read now so the epilogue does not wait on them
 #pragma unroll
-            for (int k = 0; k < D2D_NSTATS; ++k) accp[k] = fld(a.acc, k, n, i);
+            for (int k = 0; k < D2D_NSTATS; ++k) sh.acc[k][lane] = fld(a.acc, k, n, i);
         }
         if (valid && done && auto_reset && !(D2D_ABL & 8)) {
             // the next episode: spawn state, reset observation (cached or computed), new state
@@ -711,13 +725,22 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const Scn* scns, cons
             fld(a.ist, D2D_I_EPISODE, n, i) = (int32_t)(ep + 1u);
             if (a.cfg.scn_pool && a.env_scn) a.env_scn[ie] = nscn;
         }
+        if (D2D_K1_QUEUE && a.fq) {
+            // fresh curriculum: the slot the finished episode ran on now takes the episode after
+            // next (key ep + 2 - 1 = the new counter), generated by K5 after this launch
+            const bool need = valid && done && auto_reset;
+            const uint64_t m = __ballot(need);
+            if (m != 0ull) {
+                const int first = __ffsll((unsigned long long)m) - 1;
+                int base = 0;
+                if (lane == first) base = atomicAdd(a.fqc, __popcll(m));
+                base = __shfl(base, first);
+                if (need) a.fq[base + __popcll(m & ((1ull << lane) - 1ull))] = fresh_slot(ie, sh.ep[lane] + 1u);
+            }
+        }
         STAMP(4);
         flag_wait(sh.f_gs);
         STAMP(5);
-        if (valid && done) {
-#pragma unroll
-            for (int k = 0; k < D2D_NSTATS; ++k) sh.u.p.acc[k][lane] = accp[k];
-        }
         if (valid && done && auto_reset) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) orow[19 + k] = (float)po[k];
@@ -787,14 +810,14 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const Scn* scns, cons
             // finished-episode accumulators (info counters of drone_2d_env.py:593-613)
             const bool c1 = cause & D2D_END_COLLISION, c2 = cause & D2D_END_REACH;
             const bool c4 = cause & D2D_END_TIMEUP, c5 = cause & D2D_END_AA;
-            fld(a.acc, D2D_ST_RETURN, n, i) = sh.u.p.acc[D2D_ST_RETURN][lane] + tot_rew;
-            fld(a.acc, D2D_ST_EPISODES, n, i) = sh.u.p.acc[D2D_ST_EPISODES][lane] + 1.0;
-            fld(a.acc, D2D_ST_SUCCESS, n, i) = sh.u.p.acc[D2D_ST_SUCCESS][lane] + (c2 ? 1.0 : 0.0);
-            fld(a.acc, D2D_ST_FAIL, n, i) = sh.u.p.acc[D2D_ST_FAIL][lane] + ((c1 || c4 || c5) ? 1.0 : 0.0);
+            fld(a.acc, D2D_ST_RETURN, n, i) = sh.acc[D2D_ST_RETURN][lane] + tot_rew;
+            fld(a.acc, D2D_ST_EPISODES, n, i) = sh.acc[D2D_ST_EPISODES][lane] + 1.0;
+            fld(a.acc, D2D_ST_SUCCESS, n, i) = sh.acc[D2D_ST_SUCCESS][lane] + (c2 ? 1.0 : 0.0);
+            fld(a.acc, D2D_ST_FAIL, n, i) = sh.acc[D2D_ST_FAIL][lane] + ((c1 || c4 || c5) ? 1.0 : 0.0);
             fld(a.acc, D2D_ST_COLLISION, n, i) =
-                sh.u.p.acc[D2D_ST_COLLISION][lane] + ((c1 && !c2 && !c4 && !c5) ? 1.0 : 0.0);
-            fld(a.acc, D2D_ST_APE, n, i) = sh.u.p.acc[D2D_ST_APE][lane] + ape;
-            fld(a.acc, D2D_ST_LEN, n, i) = sh.u.p.acc[D2D_ST_LEN][lane] + (double)t;
+                sh.acc[D2D_ST_COLLISION][lane] + ((c1 && !c2 && !c4 && !c5) ? 1.0 : 0.0);
+            fld(a.acc, D2D_ST_APE, n, i) = sh.acc[D2D_ST_APE][lane] + ape;
+            fld(a.acc, D2D_ST_LEN, n, i) = sh.acc[D2D_ST_LEN][lane] + (double)t;
         }
         if (!(done && auto_reset)) {
             fld(a.st, D2D_S_PATH_ERR, n, i) = path_err;
@@ -1076,6 +1099,7 @@ struct FreshArgs {
     int32_t* queue;          // [2 n] slots to generate (K5a -> K5b)
     int32_t* qcount;         // [2] queue length (K5b's last workgroup to finish zeroes it again) and
                              // K5b's finished-workgroup ticket
+    uint64_t* stamps;        // diagnostic builds only (D2D_GEN_STAMPS): [queue position][8]
     int restore;
 };
 __global__ __launch_bounds__(256) void d2d_fresh_scan_kernel(FreshArgs f) {
@@ -1101,10 +1125,16 @@ __global__ __launch_bounds__(256) void d2d_fresh_scan_kernel(FreshArgs f) {
     base = __shfl(base, first);
     if (need) f.queue[base + __popcll(m & ((1ull << lane) - 1ull))] = slot;
 }
-__global__ __launch_bounds__(64) void d2d_fresh_gen_kernel(FreshArgs f) {
+// K5b: one 128-thread workgroup per queued slot.  Wave 0 generates the scenario (path, then stage
+// fields and obstacles) and writes the device table and the ABI record; wave 1 builds the golden-march
+// tables as soon as the path part is in LDS (they do not depend on the obstacles), so the two run
+// side by side.
+__global__ __launch_bounds__(128) void d2d_fresh_gen_kernel(FreshArgs f) {
     __shared__ __attribute__((aligned(16))) GenLds G;
-    const int lane = threadIdx.x;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int count = __hip_atomic_load(f.qcount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) G.fpath = 0u;
+    __syncthreads();
     for (int it = blockIdx.x; it < count; it += gridDim.x) {
         const int slot = f.queue[it];
         const int i = slot >> 1;
@@ -1117,10 +1147,17 @@ __global__ __launch_bounds__(64) void d2d_fresh_gen_kernel(FreshArgs f) {
             key = f.ist[(size_t)D2D_I_EPISODE * f.n + i];
             clk = *f.clock;
         }
-        const double sim = f.cur.sim_num0 + (double)clk * f.cur.envs_total;
-        gen_curriculum_wave(f.cur, f.W, f.H, f.seed, f.env_id_base + (uint32_t)i, (uint32_t)key, sim, G, lane);
-        // the device table and the ABI record, 8-byte words across the wave
-        {
+        uint64_t* st = nullptr;
+#ifdef D2D_GEN_STAMPS
+        if (f.stamps) st = f.stamps + (size_t)it * 8;
+#endif
+        if (wave == 0) {
+            const double sim = f.cur.sim_num0 + (double)clk * f.cur.envs_total;
+            const uint32_t gid = f.env_id_base + (uint32_t)i;
+            const int pos = gen_path_wave(f.cur, f.W, f.H, f.seed, gid, (uint32_t)key, G, lane, st);
+            flag_raise(G.fpath);
+            gen_rest_wave(f.cur, f.W, f.H, f.seed, gid, (uint32_t)key, sim, pos, G, lane, st);
+            // the device table and the ABI record, 8-byte words across the wave
             const double* src = reinterpret_cast<const double*>(&G.s);
             double* dst = reinterpret_cast<double*>(f.scn + slot);
             for (int k = lane; k < (int)(sizeof(Scn) / 8); k += 64) dst[k] = src[k];
@@ -1128,19 +1165,29 @@ __global__ __launch_bounds__(64) void d2d_fresh_gen_kernel(FreshArgs f) {
             const double* sa = reinterpret_cast<const double*>(&G.a);
             double* da = reinterpret_cast<double*>(f.abi + slot);
             for (int k = lane; k < (int)(sizeof(d2d_scn) / 8); k += 64) da[k] = sa[k];
-        }
-#if !D2D_FRESH_NOTAB
-        brtab_build_wave(G.s, f.brt[slot], G, lane);  // both kinds, from the LDS table
+            GSTAMP(st, 6);
+#if D2D_GEN_ONEWAVE && !D2D_FRESH_NOTAB
+            brtab_build_wave(G.s, f.brt[slot], G, lane);
+            GSTAMP(st, 7);
 #endif
-        if (lane == 0) {
+        } else {
+#if !D2D_FRESH_NOTAB
+            flag_wait(G.fpath);
+            brtab_build_wave(G.s, f.brt[slot], G, lane);  // both kinds, from the LDS path
+#endif
+            GSTAMP(st, 7);
+        }
+        __syncthreads();  // G is reused by the next item
+        if (threadIdx.x == 0) {
+            G.fpath = 0u;
             f.gclk[slot] = clk;
             f.tag[slot] = key;
         }
-        __syncthreads();  // G is reused by the next item
+        __syncthreads();
     }
     // every workgroup has read the queue length (above); the last one to finish resets it for the
-    // next K5a, so no memset is needed between launches
-    if (lane == 0 &&
+    // next launch, so no memset is needed between launches
+    if (threadIdx.x == 0 &&
         __hip_atomic_fetch_add(&f.qcount[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1) {
         __hip_atomic_store(&f.qcount[0], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(&f.qcount[1], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1153,6 +1200,30 @@ __global__ __launch_bounds__(64) void d2d_brtab_kernel(const Scn* scn, int n_scn
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= 2 * n_scn) return;
     brtab_build(scn[t >> 1], t & 1, out[t >> 1]);
+}
+
+// table self-check: words of the stored tables `got` that differ from `ref` (d2d_brtab_kernel) over
+// each kind's recorded steps; slots whose tag is negative (never generated) are skipped
+__global__ __launch_bounds__(256) void d2d_brtab_cmp_kernel(const BrTab* got, const BrTab* ref, int n_scn,
+                                                            const int32_t* tag, unsigned long long* bad) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= 2 * n_scn) return;
+    const int sl = t >> 1, kind = t & 1;
+    if (tag && tag[sl] < 0) return;
+    const BrTab& G = got[sl];
+    const BrTab& R = ref[sl];
+    unsigned long long c = (G.len[kind] != R.len[kind]) ? 1ull : 0ull;
+    const int len = min(R.len[kind], BT_K);
+    auto cmp = [&](const void* a, const void* b, int bytes) {
+        const uint64_t* x = reinterpret_cast<const uint64_t*>(a);
+        const uint64_t* y = reinterpret_cast<const uint64_t*>(b);
+        for (int w = 0; w < bytes / 8; ++w) c += (x[w] != y[w]) ? 1ull : 0ull;
+    };
+    for (int j = 0; j <= len; ++j) {
+        cmp(&G.hot.it[kind][j], &R.hot.it[kind][j], (int)sizeof(BtIt));
+        cmp(&G.snap[kind][j], &R.snap[kind][j], (int)sizeof(BtSnap));
+    }
+    if (c) atomicAdd(bad, c);
 }
 
 // ------------------------------------------------------------------------------------ self-test
