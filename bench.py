@@ -57,7 +57,8 @@ def parse():
                         "of envs (the first episodes after reset all start at the spawn boxes)")
     p.add_argument("--envs", type=int, default=ENVS_PER_GPU)
     p.add_argument("--scenario", default=SCENARIO,
-                   help="test scenario name, NAME_free (no obstacles: configs[1]) or 'mixed' (configs[4])")
+                   help="test scenario name, NAME_free (no obstacles: configs[1]), 'mixed' (configs[4]) or "
+                        "'curriculum' (the fresh training curriculum: a new device-generated scenario per episode)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (s)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--info", action="store_true",
@@ -231,7 +232,12 @@ def main():
 
     rank, world, local = setup_dist(args)
 
-    kwargs = dict(ENV_TRAIN_CONFIG, scenario=MIXED if args.scenario == "mixed" else args.scenario)
+    if args.scenario == "curriculum":
+        # the reference's training distribution: every reset on its own device-generated scenario,
+        # stages 1-5 on the device step clock (starts at stage 1, stage 5 after 2 M global steps)
+        kwargs = dict(ENV_TRAIN_CONFIG, mode="curriculum", scenario="curriculum", sim_num=0)
+    else:
+        kwargs = dict(ENV_TRAIN_CONFIG, scenario=MIXED if args.scenario == "mixed" else args.scenario)
     dev = torch.device("cuda", torch.cuda.current_device())
     n = args.envs
     # this rank's block of a global batch of world x n envs (global env ids, no step collective)
@@ -385,7 +391,12 @@ def main():
                     "note": "flops = (2 FMA + ADD + MUL) f64 wave-instructions x 64 lanes per env-step "
                             "(issued lanes); the kernel is bound by VALU issue, of which fp64 arithmetic "
                             "is the mix_frac share"}
-        if not args.no_cpu_baseline and world == 1:
+        if args.scenario == "curriculum":
+            line["config"]["workload"] = (f"fresh training curriculum (a new device-generated scenario per episode, "
+                                          f"stage from the device step clock), {n} envs per GPU, U(-1,1) f32 "
+                                          f"actions, in-kernel auto-reset")
+            line["kernel_note"] = "per step: step kernel + scenario generator (K5) + queue clear + fill/16"
+        elif not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(args, kwargs)
         print(json.dumps(line), flush=True)
     venv.close()

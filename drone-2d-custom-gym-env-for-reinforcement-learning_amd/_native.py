@@ -42,7 +42,6 @@ SIGNATURES = {
     "d2d_fresh_recipes": (C.c_int32, [_VP, _VP, _VP, C.POINTER(C.c_int64), C.c_int32]),
     "d2d_get_scenario_table": (C.c_int32, [_VP, C.c_int32, C.c_int32, C.POINTER(abi.D2DScn)]),
     "d2d_generation": (C.c_int32, [_VP]),
-    "d2d_check_tables": (C.c_int32, [_VP, C.POINTER(C.c_uint64)]),
     "d2d_set_scenario_costs": (C.c_int32, [_VP, C.POINTER(C.c_double), C.c_int32]),
 }
 

@@ -294,8 +294,7 @@ __device__ inline void gen_curriculum(const d2d_curriculum& c, double W, double 
 // oracle's o_gen_curriculum); only the order in which independent values are computed changes.
 constexpr int GEN_WIN = 256;   // stream words precomputed per item (corner + waypoints + ~25 obstacle tries)
 
-// LDS hand-off between the lanes of ONE wave (each generator part below runs on a single wave of
-// K5b's workgroup, the other wave runs other code, so no workgroup barrier)
+// LDS hand-off between the lanes of the one wave that runs the generator
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
@@ -402,15 +401,10 @@ struct GenLds {
     Scn s;                     // its device form (obstacle placement, tables)
     uint32_t win[GEN_WIN];     // the stream's first GEN_WIN words
     double wx[D2D_MAX_WPS], wy[D2D_MAX_WPS], sa[D2D_MAX_WPS], ca[D2D_MAX_WPS], seg[D2D_MAX_WPS];
-    // golden-march table build (brtab_build_wave): per kind, the probes and their knot intervals
-    double bx[2][BT_K + 1], bk[2][BT_K + 1];
-    int32_t bix[2][BT_K + 1], bta[2][BT_K], blen[2];
-    alignas(16) BrTab t;       // the tables, built here and copied out whole
     // obstacle placement (gen_obstacles_wave): the trial that starts at stream word w0 + 2 l, per lane l
     double ox[64], oy[64], osz[64];
     int32_t ook[64], ocons[64];
     int32_t wpos;            // the stream position after the obstacle calls
-    uint32_t fpath;          // K5b: wave 0 -> wave 1, G.s's path part is built (the tables may start)
 };
 
 // generate_obstacles_around_path (gen_obstacles) with the wave: one rejection trial is a pure function
@@ -474,9 +468,9 @@ __device__ inline void gen_obstacles_wave(GenLds& G, uint64_t seed, uint32_t gid
 }
 
 // one curriculum reset by the calling wave (all 64 lanes, wave-uniform arguments) in two parts: the
-// path (gen_path_wave: waypoints, fit, G.s's knots and interval records -- all the golden-march tables
-// need) and the rest (gen_rest_wave: stage fields, obstacles, G.s's circles and scalars).  The result
-// is in G.a / G.s (LDS).  Same draws and arithmetic as gen_curriculum.
+// path (gen_path_wave: waypoints, fit, G.s's knots and interval records) and the rest (gen_rest_wave:
+// stage fields, obstacles, G.s's circles and scalars).  The result is in G.a / G.s (LDS).  Same draws
+// and arithmetic as gen_curriculum.
 #ifdef D2D_GEN_STAMPS  // diagnostic builds only: s_memtime at K5b's phase boundaries, 8 per item
 #define GSTAMP(st, k)                                                   \
     do {                                                                \
@@ -647,141 +641,5 @@ __device__ inline void gen_rest_wave(const d2d_curriculum& c, double W, double H
     GSTAMP(st, 5);
 }
 
-
-// brtab_build for both kinds with the wave (d2d_device.h: the forced runs), built in LDS (G.t) and
-// copied out with the whole wave.  The forced decisions make the search's floating-point state (a, b,
-// fulc, nfc, xf, e, rat) a function of the step number alone, so lanes 0 and 1 (kind = lane) first run
-// that recurrence with no path evaluation, recording each step's probe; then every lane evaluates
-// probes (knot interval + QPMI2D point), independent of each other; then lane k of each kind derives
-// the interval bookkeeping (ia, ka, ib, ixf, kxf) before step k in closed form: ixf / kxf are the
-// latest probe's (the forced run's xf is always the newest probe, except after kind 0's first step),
-// ia / ka the value the last step j < k with to_a[j] moved a to, ib that of the last step without
-// (ballot masks of to_a, highest set bit below k).  Every stored value is computed by the same
-// operations as in brtab_build, so the tables are identical to it.  (A single lane storing the
-// tables straight to global memory ran into the wave's limit of outstanding stores: ~900 of them.)
-__device__ inline void brtab_build_wave(const Scn& s, BrTab& T, GenLds& G, int lane) {
-    const PathK K = path_k(s);
-    BrTab& W = G.t;
-    if (lane < 2) {
-        const int kind = lane;
-        double a = 0.0 - 10.0, b = K.L + 10.0;
-        double fulc = a + BR_GOLDEN * (b - a);
-        double nfc = fulc, xf = fulc, rat = 0.0, e = 0.0;
-        int num = 1, jf = 0, jn = 0, jx = 0;
-        G.bx[kind][0] = xf;
-        BtIt& h0 = W.hot.it[kind][0];
-        h0.dxn = h0.dxf = h0.e = h0.am = h0.bm = h0.pad = 0.0;
-        int k = 0;
-        for (; k < BT_K; ++k) {
-            {
-                const double xm0 = 0.5 * (a + b);
-                const double t1 = BR_SQRT_EPS * fabs(xf) + BR_XATOL3;
-                const double t2 = 2.0 * t1;
-                if (!((fabs(xf - xm0) > (t2 - 0.5 * (b - a))) & (num < 500))) break;  // brent_active
-            }
-            BtSnap& S = W.snap[kind][k];
-            S.a = a; S.b = b; S.fulc = fulc; S.nfc = nfc; S.xf = xf; S.rat = rat; S.e = e;
-            S.num = num; S.j_fulc = jf; S.j_nfc = jn; S.j_xf = jx; S.pad = 0;
-            const double xm = 0.5 * (a + b);
-            const double tol1 = BR_SQRT_EPS * fabs(xf) + BR_XATOL3;
-            BtIt& h = W.hot.it[kind][k + 1];
-            h.dxn = xf - nfc;
-            h.dxf = xf - fulc;
-            h.e = (fabs(e) > tol1) ? e : 0.0;
-            h.am = a - xf;
-            h.bm = b - xf;
-            h.pad = 0.0;
-            const double e_g = (xf >= xm) ? a - xf : b - xf;
-            rat = BR_GOLDEN * e_g;
-            e = e_g;
-            const double mx = fmax(fabs(rat), tol1);
-            const double x = xf + ((rat < 0.0) ? -mx : mx);
-            G.bx[kind][k + 1] = x;
-            num += 1;
-            const bool le = !(kind == 0 && k == 0);
-            const bool c1 = !le;
-            const bool ge = x >= xf;
-            const bool to_a = le == ge;
-            G.bta[kind][k] = to_a ? 1 : 0;
-            const double t = le ? xf : x;
-            a = to_a ? t : a;
-            b = to_a ? b : t;
-            const int j = k + 1;
-            const double nfulc = (le | c1) ? nfc : fulc;
-            const int njf = (le | c1) ? jn : jf;
-            const double nnfc = le ? xf : (c1 ? x : nfc);
-            const int njn = le ? jx : (c1 ? j : jn);
-            fulc = nfulc;
-            nfc = nnfc;
-            xf = le ? x : xf;
-            jf = njf;
-            jn = njn;
-            jx = le ? j : jx;
-        }
-        BtSnap& S = W.snap[kind][k];
-        S.a = a; S.b = b; S.fulc = fulc; S.nfc = nfc; S.xf = xf; S.rat = rat; S.e = e;
-        S.num = num; S.j_fulc = jf; S.j_nfc = jn; S.j_xf = jx; S.pad = 0;
-        G.blen[kind] = k;
-        W.len[kind] = k;
-        W.pad[kind] = 0;
-    }
-    wave_sync();
-    // every probe j <= len of both kinds: knot interval, path point, upper knot; entries past len zeroed
-    const int n0 = G.blen[0] + 1, n1 = G.blen[1] + 1;
-    for (int q = lane; q < 2 * BT_HOT; q += 64) {
-        const int kind = q < BT_HOT ? 0 : 1, j = q < BT_HOT ? q : q - BT_HOT;
-        BtIt& h = W.hot.it[kind][j];
-        if (j < (kind ? n1 : n0)) {
-            const double x = G.bx[kind][j];
-            const int ix = u_index(s, x);
-            double X, Y, kx;
-            path_eval_n(s, K, x, ix, X, Y, kx);
-            h.X = X;
-            h.Y = Y;
-            G.bix[kind][j] = ix;
-            G.bk[kind][j] = kx;
-        } else {
-            h = BtIt{0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-        }
-    }
-    wave_sync();
-    {
-        const int ia0 = u_index(s, 0.0 - 10.0), ib0 = u_index(s, K.L + 10.0);
-        const double ka0 = SREC(s, REC_U1, ia0);
-        for (int kind = 0; kind < 2; ++kind) {
-            const int len = G.blen[kind], k = lane;
-            const bool ta = (k < len) && G.bta[kind][k] != 0;
-            const uint64_t mA = __ballot(ta), mB = __ballot((k < len) && !ta);
-            if (k <= len) {
-                // (ti, tk) of step j: kind 0's first step moves to its own probe; otherwise the probe
-                // xf held before the step (probe j, except kind 0's step 1: the initial point)
-                auto tix = [&](int j) { return (kind == 0 && j == 0) ? 1 : ((kind == 0 && j == 1) ? 0 : j); };
-                const uint64_t below = (1ull << k) - 1ull;  // (k <= BT_K < 64)
-                const uint64_t ma = mA & below, mb = mB & below;
-                int ia = ia0, ib = ib0;
-                double ka = ka0;
-                if (ma) {
-                    const int jj = tix(63 - __clzll((long long)ma));
-                    ia = G.bix[kind][jj];
-                    ka = G.bk[kind][jj];
-                }
-                if (mb) ib = G.bix[kind][tix(63 - __clzll((long long)mb))];
-                const int jx = (kind == 0 && k == 1) ? 0 : k;
-                BtSnap& S = W.snap[kind][k];
-                S.ka = ka;
-                S.kxf = G.bk[kind][jx];
-                S.ia = ia;
-                S.ib = ib;
-                S.ixf = G.bix[kind][jx];
-            }
-        }
-    }
-    wave_sync();
-    // the table to global memory, 16-byte words across the wave
-    static_assert(sizeof(BrTab) % 16 == 0, "BrTab size");
-    const uint4* src = reinterpret_cast<const uint4*>(&W);
-    uint4* dst = reinterpret_cast<uint4*>(&T);
-    for (int q = lane; q < (int)(sizeof(BrTab) / 16); q += 64) dst[q] = src[q];
-}
 
 }  // namespace d2d

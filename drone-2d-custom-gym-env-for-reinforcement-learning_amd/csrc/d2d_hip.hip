@@ -69,7 +69,7 @@ struct d2d_handle {
     d2d_curriculum cur{};        // fresh mode: generator parameters
     int32_t* scn_tag = nullptr;  // fresh mode: [2 n] episode key of each slot
     int64_t* gclk = nullptr;     // fresh mode: [2 n] clock at generation
-    int32_t* fresh_q = nullptr;  // fresh mode: [2 n + 2] K5's queue of slots to generate, its length, a ticket
+    int32_t* fresh_q = nullptr;  // fresh mode: [2 n + 2] K5's queue of slots to generate, its length (+1 spare)
     int64_t* clock = nullptr;    // [1] the step clock (K1 advances it)
     uint64_t fresh_seed = 0;
     bool fresh_seeded = false;
@@ -89,8 +89,7 @@ StepArgs make_args(const d2d_t* h) {
     a.ist = h->ist;
     a.acc = h->acc;
     a.scn = h->scn;
-    // (diagnostic A/B: D2D_FRESH_NOTAB=1 drops the golden-march tables in fresh mode)
-    a.brt = (D2D_FRESH_NOTAB && h->cfg.scn_pool == 2) ? nullptr : h->brt;
+    a.brt = h->brt;  // (null in fresh curriculum mode: DESIGN.md "Round 4")
     a.env_scn = h->env_scn;
     a.pool_base = h->pool_dev;
     a.pool_n = h->pool_n;
@@ -131,7 +130,6 @@ hipError_t fresh_regen(d2d_t* h, hipStream_t stream, bool restore = false, bool 
     f.env_id_base = (uint32_t)h->cfg.env_id_base;
     f.abi = h->abi;
     f.scn = h->scn;
-    f.brt = h->brt;
     f.tag = h->scn_tag;
     f.gclk = h->gclk;
     f.clock = h->clock;
@@ -143,11 +141,14 @@ hipError_t fresh_regen(d2d_t* h, hipStream_t stream, bool restore = false, bool 
 #endif
     const int items = restore ? 2 * h->n : h->n;
     if (!queued) hipLaunchKernelGGL(d2d_fresh_scan_kernel, dim3((items + 255) / 256), dim3(256), 0, stream, f);
-    // one two-wave workgroup per queued slot: ~800 per step at 65 536 envs stepped with random
-    // actions (the items of the step all run at once); a reset queues every env (the grid's
-    // workgroups then take several each)
-    hipLaunchKernelGGL(d2d_fresh_gen_kernel, dim3(std::min(items, D2D_GEN_GRID)), dim3(D2D_GEN_ONEWAVE ? 64 : 128), 0, stream, f);
-    return hipGetLastError();
+    // one wave per queued slot: ~800 per step at 65 536 envs stepped with random actions (the items
+    // of a step all run at once); a reset queues every env (the grid's workgroups then take several)
+    hipLaunchKernelGGL(d2d_fresh_gen_kernel, dim3(std::min(items, D2D_GEN_GRID)), dim3(64), 0, stream, f);
+    hipError_t e = hipGetLastError();
+    // the queue length back to 0 for the next K1 (a last-workgroup ticket instead costs ~2 048
+    // same-address atomics: +14 us per step)
+    if (e == hipSuccess) e = hipMemsetAsync(f.qcount, 0, sizeof(int32_t), stream);
+    return e;
 }
 bool fresh_mode(const d2d_t* h) { return h->cfg.scn_pool == 2; }
 
@@ -896,7 +897,7 @@ int32_t d2d_set_curriculum(d2d_t* h, const d2d_curriculum* c) {
     if (h->n_scn != (int)S || !h->scn_tag) {
         if ((e = hipDeviceSynchronize()) != hipSuccess) return hip_fail(e, "d2d_set_curriculum: sync");
         for (void* p : {(void*)h->scn, (void*)h->brt, (void*)h->abi, (void*)h->scn_tag, (void*)h->gclk,
-                        (void*)h->fresh_q})
+                        (void*)h->fresh_q})  // (fresh mode keeps no golden-march tables: brt stays null)
             if (p) (void)hipFree(p);
         h->scn = nullptr;
         h->brt = nullptr;
@@ -906,14 +907,12 @@ int32_t d2d_set_curriculum(d2d_t* h, const d2d_curriculum* c) {
         h->fresh_q = nullptr;
         h->n_scn = 0;
         if ((e = hipMalloc(&h->scn, sizeof(d2d::Scn) * S)) != hipSuccess ||
-            (e = hipMalloc(&h->brt, sizeof(d2d::BrTab) * S)) != hipSuccess ||
             (e = hipMalloc(&h->abi, sizeof(d2d_scn) * S)) != hipSuccess ||
             (e = hipMalloc(&h->scn_tag, sizeof(int32_t) * S)) != hipSuccess ||
             (e = hipMalloc(&h->gclk, sizeof(int64_t) * S)) != hipSuccess ||
             (e = hipMalloc(&h->fresh_q, sizeof(int32_t) * (S + 2))) != hipSuccess ||
             (e = hipMemset(h->fresh_q, 0, sizeof(int32_t) * (S + 2))) != hipSuccess ||
             (e = hipMemset(h->scn, 0, sizeof(d2d::Scn) * S)) != hipSuccess ||
-            (e = hipMemset(h->brt, 0, sizeof(d2d::BrTab) * S)) != hipSuccess ||
             (e = hipMemset(h->abi, 0, sizeof(d2d_scn) * S)) != hipSuccess ||
             (e = hipMemset(h->gclk, 0, sizeof(int64_t) * S)) != hipSuccess)
             return hip_fail(e, "d2d_set_curriculum: hipMalloc");
@@ -968,35 +967,6 @@ int32_t d2d_get_scenario_table(d2d_t* h, int32_t first, int32_t count, d2d_scn* 
     if ((e = hipDeviceSynchronize()) != hipSuccess ||
         (e = hipMemcpy(out, h->abi + first, sizeof(d2d_scn) * (size_t)count, hipMemcpyDeviceToHost)) != hipSuccess)
         return hip_fail(e, "d2d_get_scenario_table");
-    return D2D_OK;
-}
-
-int32_t d2d_check_tables(d2d_t* h, uint64_t* mismatches) {
-    if (!h || !mismatches) return fail(D2D_E_ARG, "d2d_check_tables: null handle/out");
-    if (!h->brt || !h->scn) return fail(D2D_E_STATE, "d2d_check_tables: no tables");
-    DeviceGuard g(h->device);
-    const int ns = h->n_scn;
-    d2d::BrTab* ref = nullptr;
-    unsigned long long* bad = nullptr;
-    hipError_t e;
-    if ((e = hipDeviceSynchronize()) != hipSuccess || (e = hipMalloc(&ref, sizeof(d2d::BrTab) * (size_t)ns)) != hipSuccess ||
-        (e = hipMemset(ref, 0, sizeof(d2d::BrTab) * (size_t)ns)) != hipSuccess ||
-        (e = hipMalloc(&bad, sizeof(unsigned long long))) != hipSuccess ||
-        (e = hipMemset(bad, 0, sizeof(unsigned long long))) != hipSuccess) {
-        if (ref) (void)hipFree(ref);
-        if (bad) (void)hipFree(bad);
-        return hip_fail(e, "d2d_check_tables: alloc");
-    }
-    hipLaunchKernelGGL(d2d_brtab_kernel, dim3((2 * ns + 63) / 64), dim3(64), 0, 0, h->scn, ns, ref);
-    hipLaunchKernelGGL(d2d_brtab_cmp_kernel, dim3((2 * ns + 255) / 256), dim3(256), 0, 0, h->brt, ref, ns,
-                       fresh_mode(h) ? h->scn_tag : nullptr, bad);
-    unsigned long long c = 0;
-    if ((e = hipGetLastError()) == hipSuccess && (e = hipDeviceSynchronize()) == hipSuccess)
-        e = hipMemcpy(&c, bad, sizeof(c), hipMemcpyDeviceToHost);
-    (void)hipFree(ref);
-    (void)hipFree(bad);
-    if (e != hipSuccess) return hip_fail(e, "d2d_check_tables");
-    *mismatches = c;
     return D2D_OK;
 }
 

@@ -117,17 +117,11 @@ struct StepArgs {
 #define D2D_ABL 0        // diagnostic builds only: bit r skips role r's compute, bit 4 = perfect
                          // reset cache (no fills, every entry taken as ready): timing ablations
 #endif
-#ifndef D2D_GEN_ONEWAVE
-#define D2D_GEN_ONEWAVE 0  // A/B: K5b as one wave per slot (tables after the scenario)
-#endif
 #ifndef D2D_K1_QUEUE
 #define D2D_K1_QUEUE 1  // K1 queues the fresh curriculum's slots itself (no K5a scan per step; A/B: 0)
 #endif
 #ifndef D2D_GLOBAL_NOSPLIT
 #define D2D_GLOBAL_NOSPLIT 1  // tables in global memory: W2 re-checks the whole table, W3 none (A/B: 0)
-#endif
-#ifndef D2D_FRESH_NOTAB
-#define D2D_FRESH_NOTAB 0  // diagnostic A/B builds only: fresh curriculum without golden-march tables
 #endif
 #ifndef D2D_SPLIT3
 #define D2D_SPLIT3 -1    // W2, W1 and W3 re-check one third each of the golden-march table: 1 always,
@@ -1092,13 +1086,11 @@ struct FreshArgs {
     uint32_t env_id_base;
     d2d_scn* abi;            // [2 n] ABI records (read back for the oracle)
     Scn* scn;                // [2 n]
-    BrTab* brt;              // [2 n] golden-march tables
     int32_t* tag;            // [2 n] episode key of each slot (-1: empty)
     int64_t* gclk;           // [2 n] clock at generation
     const int64_t* clock;    // the step clock (K1 advances it)
     int32_t* queue;          // [2 n] slots to generate (K5a -> K5b)
-    int32_t* qcount;         // [2] queue length (K5b's last workgroup to finish zeroes it again) and
-                             // K5b's finished-workgroup ticket
+    int32_t* qcount;         // [1] queue length (cleared by a memset after K5b)
     uint64_t* stamps;        // diagnostic builds only (D2D_GEN_STAMPS): [queue position][8]
     int restore;
 };
@@ -1125,16 +1117,13 @@ __global__ __launch_bounds__(256) void d2d_fresh_scan_kernel(FreshArgs f) {
     base = __shfl(base, first);
     if (need) f.queue[base + __popcll(m & ((1ull << lane) - 1ull))] = slot;
 }
-// K5b: one 128-thread workgroup per queued slot.  Wave 0 generates the scenario (path, then stage
-// fields and obstacles) and writes the device table and the ABI record; wave 1 builds the golden-march
-// tables as soon as the path part is in LDS (they do not depend on the obstacles), so the two run
-// side by side.
-__global__ __launch_bounds__(128) void d2d_fresh_gen_kernel(FreshArgs f) {
+// K5b: one wave per queued slot generates the scenario in LDS (d2d_curriculum.h) and writes the device
+// table and the ABI record.  (No golden-march tables in fresh mode: built per scenario they cost K5b
+// more than they save K1, DESIGN.md "Round 4".)  The host clears the queue length after the launch.
+__global__ __launch_bounds__(64) void d2d_fresh_gen_kernel(FreshArgs f) {
     __shared__ __attribute__((aligned(16))) GenLds G;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int lane = threadIdx.x;
     const int count = __hip_atomic_load(f.qcount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (threadIdx.x == 0) G.fpath = 0u;
-    __syncthreads();
     for (int it = blockIdx.x; it < count; it += gridDim.x) {
         const int slot = f.queue[it];
         const int i = slot >> 1;
@@ -1151,46 +1140,24 @@ __global__ __launch_bounds__(128) void d2d_fresh_gen_kernel(FreshArgs f) {
 #ifdef D2D_GEN_STAMPS
         if (f.stamps) st = f.stamps + (size_t)it * 8;
 #endif
-        if (wave == 0) {
-            const double sim = f.cur.sim_num0 + (double)clk * f.cur.envs_total;
-            const uint32_t gid = f.env_id_base + (uint32_t)i;
-            const int pos = gen_path_wave(f.cur, f.W, f.H, f.seed, gid, (uint32_t)key, G, lane, st);
-            flag_raise(G.fpath);
-            gen_rest_wave(f.cur, f.W, f.H, f.seed, gid, (uint32_t)key, sim, pos, G, lane, st);
-            // the device table and the ABI record, 8-byte words across the wave
-            const double* src = reinterpret_cast<const double*>(&G.s);
-            double* dst = reinterpret_cast<double*>(f.scn + slot);
-            for (int k = lane; k < (int)(sizeof(Scn) / 8); k += 64) dst[k] = src[k];
-            static_assert(sizeof(d2d_scn) % 8 == 0, "d2d_scn size");
-            const double* sa = reinterpret_cast<const double*>(&G.a);
-            double* da = reinterpret_cast<double*>(f.abi + slot);
-            for (int k = lane; k < (int)(sizeof(d2d_scn) / 8); k += 64) da[k] = sa[k];
-            GSTAMP(st, 6);
-#if D2D_GEN_ONEWAVE && !D2D_FRESH_NOTAB
-            brtab_build_wave(G.s, f.brt[slot], G, lane);
-            GSTAMP(st, 7);
-#endif
-        } else {
-#if !D2D_FRESH_NOTAB
-            flag_wait(G.fpath);
-            brtab_build_wave(G.s, f.brt[slot], G, lane);  // both kinds, from the LDS path
-#endif
-            GSTAMP(st, 7);
-        }
-        __syncthreads();  // G is reused by the next item
-        if (threadIdx.x == 0) {
-            G.fpath = 0u;
+        const double sim = f.cur.sim_num0 + (double)clk * f.cur.envs_total;
+        const uint32_t gid = f.env_id_base + (uint32_t)i;
+        const int pos = gen_path_wave(f.cur, f.W, f.H, f.seed, gid, (uint32_t)key, G, lane, st);
+        gen_rest_wave(f.cur, f.W, f.H, f.seed, gid, (uint32_t)key, sim, pos, G, lane, st);
+        // the device table and the ABI record, 8-byte words across the wave
+        const double* src = reinterpret_cast<const double*>(&G.s);
+        double* dst = reinterpret_cast<double*>(f.scn + slot);
+        for (int k = lane; k < (int)(sizeof(Scn) / 8); k += 64) dst[k] = src[k];
+        static_assert(sizeof(d2d_scn) % 8 == 0, "d2d_scn size");
+        const double* sa = reinterpret_cast<const double*>(&G.a);
+        double* da = reinterpret_cast<double*>(f.abi + slot);
+        for (int k = lane; k < (int)(sizeof(d2d_scn) / 8); k += 64) da[k] = sa[k];
+        GSTAMP(st, 6);
+        if (lane == 0) {
             f.gclk[slot] = clk;
             f.tag[slot] = key;
         }
-        __syncthreads();
-    }
-    // every workgroup has read the queue length (above); the last one to finish resets it for the
-    // next launch, so no memset is needed between launches
-    if (threadIdx.x == 0 &&
-        __hip_atomic_fetch_add(&f.qcount[1], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1) {
-        __hip_atomic_store(&f.qcount[0], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&f.qcount[1], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();  // G is reused by the next item
     }
 }
 
@@ -1200,30 +1167,6 @@ __global__ __launch_bounds__(64) void d2d_brtab_kernel(const Scn* scn, int n_scn
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= 2 * n_scn) return;
     brtab_build(scn[t >> 1], t & 1, out[t >> 1]);
-}
-
-// table self-check: words of the stored tables `got` that differ from `ref` (d2d_brtab_kernel) over
-// each kind's recorded steps; slots whose tag is negative (never generated) are skipped
-__global__ __launch_bounds__(256) void d2d_brtab_cmp_kernel(const BrTab* got, const BrTab* ref, int n_scn,
-                                                            const int32_t* tag, unsigned long long* bad) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= 2 * n_scn) return;
-    const int sl = t >> 1, kind = t & 1;
-    if (tag && tag[sl] < 0) return;
-    const BrTab& G = got[sl];
-    const BrTab& R = ref[sl];
-    unsigned long long c = (G.len[kind] != R.len[kind]) ? 1ull : 0ull;
-    const int len = min(R.len[kind], BT_K);
-    auto cmp = [&](const void* a, const void* b, int bytes) {
-        const uint64_t* x = reinterpret_cast<const uint64_t*>(a);
-        const uint64_t* y = reinterpret_cast<const uint64_t*>(b);
-        for (int w = 0; w < bytes / 8; ++w) c += (x[w] != y[w]) ? 1ull : 0ull;
-    };
-    for (int j = 0; j <= len; ++j) {
-        cmp(&G.hot.it[kind][j], &R.hot.it[kind][j], (int)sizeof(BtIt));
-        cmp(&G.snap[kind][j], &R.snap[kind][j], (int)sizeof(BtSnap));
-    }
-    if (c) atomicAdd(bad, c);
 }
 
 // ------------------------------------------------------------------------------------ self-test

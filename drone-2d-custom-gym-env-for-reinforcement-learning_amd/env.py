@@ -351,12 +351,6 @@ class Drone2dVecEnv:
         (set_scenarios / set_curriculum): holders of a captured graph re-capture it."""
         return int(self._lib.d2d_generation(self._h))
 
-    def check_tables(self) -> int:
-        """Words of the golden-march tables that differ from a one-thread-per-kind rebuild
-        (``d2d_check_tables``; 0 expected).  Diagnostic, synchronous."""
-        bad = C.c_uint64(0)
-        self._check(self._lib.d2d_check_tables(self._h, C.byref(bad)), "d2d_check_tables")
-        return int(bad.value)
 
     def scenario_table(self, first: int = 0, count: int | None = None):
         """ABI records (abi.D2DScn array) of scenario-table slots [first, first + count): the pool's two

@@ -264,13 +264,6 @@ int32_t d2d_episode_stats(d2d_t* h, double* out_dev, int32_t clear, void* stream
 #define D2D_SELFTEST_RECIP_DIV 2 /* division by a precomputed reciprocal (path blend)    */
 int32_t d2d_selftest(int32_t which, int64_t n, uint64_t seed, uint64_t* mismatches);
 
-/* Golden-march table self-check (no reference counterpart): rebuilds the tables of every scenario of
- * the handle (every generated slot in fresh curriculum mode) with the one-thread-per-kind forced runs
- * and stores in *mismatches (host pointer) the number of 8-byte words that differ from the stored
- * tables over each kind's recorded steps (probe entries 0..len, snapshots 0..len, len).  Synchronous.
- * Added in round 4 (the fresh curriculum builds its tables with a whole wave per scenario). */
-int32_t d2d_check_tables(d2d_t* h, uint64_t* mismatches);
-
 /* The internal slot layout d2d_set_scenarios builds for a static env->scenario map with several
  * scenarios (host-only, no device needed; for tests and diagnostics, no reference counterpart):
  * envs sorted by (scenario, id) are cut into ceil(n/64) groups of 64 slots; slot_env[64 g + l] is

@@ -45,8 +45,6 @@ def _tables_equal(venv, orc):
     n2 = 2 * venv.num_envs
     g, o = venv.scenario_table(0, n2), orc.scenario_table(0, n2)
     assert bytes(g) == bytes(o) or _diff(g, o)
-    # the golden-march tables K5 built with a whole wave per scenario == the one-thread forced runs
-    assert venv.check_tables() == 0
     kg, cg, tg = venv.fresh_recipes()
     ko, co, to = orc.fresh_recipes()
     np.testing.assert_array_equal(kg, ko)
