@@ -402,7 +402,7 @@ struct GenLds {
     uint32_t win[GEN_WIN];     // the stream's first GEN_WIN words
     double wx[D2D_MAX_WPS], wy[D2D_MAX_WPS], sa[D2D_MAX_WPS], ca[D2D_MAX_WPS], seg[D2D_MAX_WPS];
     // obstacle placement (gen_obstacles_wave): the trial that starts at stream word w0 + 2 l, per lane l
-    double ox[64], oy[64], osz[64];
+    double ox[64], oy[64], osz[64], px[64], py[64];
     int32_t ook[64], ocons[64];
     int32_t wpos;            // the stream position after the obstacle calls
 };
@@ -412,11 +412,17 @@ struct GenLds {
 // the trial starting at word w0 + 2 l and lane 0 then walks the chain of trials the serial loop would
 // run (w -> w + words consumed), appending the accepted circles in order; a chain that leaves the 64
 // evaluated starts continues from a new w0.  Same trials, same order, same arithmetic as gen_obstacles.
+// then_on_path: the reference's next call, generate_obstacles_around_path(1, mean 0, std 0, on_path)
+// (stage 5), is folded in.  Its trial at a word consumes the same draws as this call's trial there and
+// is always accepted (on the path: the circle sits at the trial's path point), so once this call's
+// chain ends at word w, the next call's one obstacle is the trial evaluated at w -- no second round of
+// trials (unless w left the evaluated window).  Same trials, same order as the two separate calls.
 __device__ inline void gen_obstacles_wave(GenLds& G, uint64_t seed, uint32_t gid, uint32_t key, double n, double mean,
-                                          double std, bool on_path, int lane) {
+                                          double std, bool on_path, int lane, bool then_on_path = false) {
     d2d_scn& s = G.a;
     const double L = s.us[s.n_wps - 1];
     int num = 0, tries = 0, w = G.wpos;
+    int phase = 0;  // (lane 0) 0: this call's chain, 1: the folded on-path call, 2: done
     bool more = true;
     while (more) {  // (wave-uniform: the walk below runs on lane 0, its state goes through LDS)
         {
@@ -436,6 +442,8 @@ __device__ inline void gen_obstacles_wave(GenLds& G, uint64_t seed, uint32_t gid
             const bool ok = on_path || off > size + 10.0;
             G.ox[lane] = on_path ? x : ox;
             G.oy[lane] = on_path ? y : oy;
+            G.px[lane] = x;
+            G.py[lane] = y;
             G.osz[lane] = size;
             G.ook[lane] = ok ? 1 : 0;
             G.ocons[lane] = R.pos - (w + 2 * lane);
@@ -443,19 +451,40 @@ __device__ inline void gen_obstacles_wave(GenLds& G, uint64_t seed, uint32_t gid
         wave_sync();
         if (lane == 0) {
             const int w0 = w;
-            while ((double)num < n && s.n_circles < D2D_MAX_CIRCLES && tries < 4096 && w < w0 + 128) {
-                const int t = (w - w0) >> 1;
-                ++tries;
-                if (G.ook[t]) {
-                    s.cx[s.n_circles] = G.ox[t];
-                    s.cy[s.n_circles] = G.oy[t];
+            if (phase == 0) {
+                while ((double)num < n && s.n_circles < D2D_MAX_CIRCLES && tries < 4096 && w < w0 + 128) {
+                    const int t = (w - w0) >> 1;
+                    ++tries;
+                    if (G.ook[t]) {
+                        s.cx[s.n_circles] = G.ox[t];
+                        s.cy[s.n_circles] = G.oy[t];
+                        s.cr[s.n_circles] = G.osz[t];
+                        s.n_circles += 1;
+                        ++num;
+                    }
+                    w += G.ocons[t];
+                }
+                if (!((double)num < n && s.n_circles < D2D_MAX_CIRCLES && tries < 4096)) {
+                    phase = then_on_path ? 1 : 2;
+                    num = 0;
+                    tries = 0;
+                }
+            }
+            if (phase == 1) {
+                // generate_obstacles_around_path(1.0, 0.0, 0.0, on_path=True): one trial, accepted
+                if (s.n_circles >= D2D_MAX_CIRCLES) {
+                    phase = 2;
+                } else if (w < w0 + 128) {
+                    const int t = (w - w0) >> 1;
+                    s.cx[s.n_circles] = G.px[t];
+                    s.cy[s.n_circles] = G.py[t];
                     s.cr[s.n_circles] = G.osz[t];
                     s.n_circles += 1;
-                    ++num;
+                    w += G.ocons[t];
+                    phase = 2;
                 }
-                w += G.ocons[t];
             }
-            G.ook[0] = ((double)num < n && s.n_circles < D2D_MAX_CIRCLES && tries < 4096) ? 1 : 0;
+            G.ook[0] = (phase != 2) ? 1 : 0;
             G.ocons[0] = w;
         }
         wave_sync();
@@ -631,8 +660,8 @@ __device__ inline void gen_rest_wave(const d2d_curriculum& c, double W, double H
         } else if (stg == 4) {
             if (n_obs != 0.0) gen_obstacles_wave(G, seed, gid, key, 1.0, 0.0, 0.0, true, lane);
         } else if (n_obs != 0.0) {
-            gen_obstacles_wave(G, seed, gid, key, n_obs, 0.0, 100.0, false, lane);
-            gen_obstacles_wave(G, seed, gid, key, 1.0, 0.0, 0.0, true, lane);
+            // the two calls of stage 5 (obstacles around the path, then one on it) in one walk
+            gen_obstacles_wave(G, seed, gid, key, n_obs, 0.0, 100.0, false, lane, true);
         }
     }
     GSTAMP(st, 4);

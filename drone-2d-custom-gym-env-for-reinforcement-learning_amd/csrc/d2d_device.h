@@ -32,9 +32,6 @@
 // the product is always built with 0): 1 skip Brent, 2 skip sensing, 4 skip joint iterations,
 // 8 skip collision test, 16 skip the Brent continuation after the golden-march tables, 128 the fresh
 // curriculum generator skips the obstacles.
-#ifndef D2D_RECPF
-#define D2D_RECPF 0  // A/B: brent_step prefetches a's interval record (see there)
-#endif
 #ifndef D2D_ABLATE
 #define D2D_ABLATE 0
 #endif
@@ -360,15 +357,9 @@ __device__ __forceinline__ bool brent_active(const Brent& B) {
 __device__ __forceinline__ void brent_step(const Scn& s, const PathK& K, double px, double py, Brent& B) {
     const double a = B.a, b = B.b, xf = B.xf, fx = B.fx, nfc = B.nfc, fulc = B.fulc;
     // the upper knot of a's interval, for the one-compare interval test.  (Carrying it in the state,
-    // or prefetching a's whole record before the candidate is known, measured no faster.)
+    // or prefetching a's whole record before the candidate is known, measured no faster -- also with
+    // the scenarios in global memory, round 4: 92.4 vs 93.0 us per fresh-curriculum step.)
     const double ka = SREC(s, REC_U1, B.ia);
-#if D2D_RECPF
-    // A/B (tables in global memory): a's record, loaded before the probe is known (the probe's interval
-    // is a's in most late steps), so the path evaluation waits on one memory round trip instead of two
-    double rpf[REC_N];
-#pragma unroll
-    for (int f = 0; f < REC_N; ++f) rpf[f] = SREC(s, f, B.ia);
-#endif
     const double xm = 0.5 * (a + b);
     const double tol1 = BR_SQRT_EPS * fabs(xf) + BR_XATOL3;
     const double tol2 = 2.0 * tol1;
@@ -417,17 +408,7 @@ __device__ __forceinline__ void brent_step(const Scn& s, const PathK& K, double 
         ix = u_index(*sp, x);
     }
     double kx;
-#if D2D_RECPF
-    if (ix != B.ia) {
-#pragma unroll
-        for (int f = 0; f < REC_N; ++f) rpf[f] = SREC(s, f, ix);
-    }
-    double xx, yy;
-    path_eval_rec(rpf, K, x, ix, xx, yy, kx);
-    const double fu = norm2(xx - px, yy - py);
-#else
     const double fu = path_dist_n(s, K, x, ix, px, py, kx);
-#endif
     B.num += 1;
     const bool le = fu <= fx;
     const bool c1 = !le & ((fu <= B.fnfc) | (nfc == xf));
