@@ -179,7 +179,7 @@ __device__ inline void gen_gradient(const d2d_scn& s, double u, double& gx, doub
 // generate_obstacles_around_path (obstacles.py:58-89): appends up to n circles (the reference's
 // `while num_obstacles < n` with a real-valued n), rejection on |offset| <= size + 10 off the path
 template <typename Rng>
-__device__ inline void gen_obstacles(Rng& R, const Scn& S, d2d_scn& s, double n, double mean, double std, bool on_path) {
+__device__ inline void gen_obstacles(Rng& R, const ScnR& S, d2d_scn& s, double n, double mean, double std, bool on_path) {
     const double L = s.us[s.n_wps - 1];
     int num = 0, tries = 0;
     while ((double)num < n && s.n_circles < D2D_MAX_CIRCLES && tries < 4096) {
@@ -214,7 +214,7 @@ __device__ inline void gen_obstacles(Rng& R, const Scn& S, d2d_scn& s, double n,
 
 // one curriculum reset: writes the ABI record `s` and its device form `S` (both in global memory)
 __device__ inline void gen_curriculum(const d2d_curriculum& c, double W, double H, uint64_t seed, uint32_t gid,
-                                      uint32_t key, double sim, d2d_scn& s, Scn& S) {
+                                      uint32_t key, double sim, d2d_scn& s, ScnR& S) {
     GenRng R;
     R.init(seed, gid, key);
     const int corner = c.random_path_spawn ? R.randint(c.corner_lo, c.corner_hi) : 2;  // 1 DL 2 DR 3 UL 4 UR
@@ -347,12 +347,12 @@ struct GenStream {
 __device__ __forceinline__ double win_u01(const uint32_t* w, int p) { return u53(w[p], w[p + 1]); }
 
 // scn_build with interval n on lane n (the path part: knots, interval records, n_wps) ...
-__device__ inline void scn_build_path_lanes(const d2d_scn& a, Scn& s, int lane) {
+__device__ inline void scn_build_path_lanes(const d2d_scn& a, ScnR& s, int lane) {
     const int nw = a.n_wps, nseg = nw - 2;
     if (lane < D2D_MAX_WPS) {
         const int n = lane;
         s.us_[n] = (n < nw) ? a.us[n] : __builtin_inf();
-        s.rec_[n][REC_N] = 0.0;
+        if (REC_W > REC_N) s.rec_[n][REC_W - 1] = 0.0;
         const int b = (n < nseg - 1) ? n : nseg - 1;
         const int q = (n == 0) ? nseg - 1 : ((n - 1 < nseg - 1) ? n - 1 : nseg - 1);
         const double v[REC_N] = {a.xa[b], a.xb[b], a.xc[b], a.ya[b], a.yb[b], a.yc[b],
@@ -370,7 +370,7 @@ __device__ inline void scn_build_path_lanes(const d2d_scn& a, Scn& s, int lane) 
     if (lane == 0) s.n_wps = nw;
 }
 // ... and the rest: circle k on lane k, the scalars and r_uniform on lane 0
-__device__ inline void scn_build_rest_lanes(const d2d_scn& a, Scn& s, int lane) {
+__device__ inline void scn_build_rest_lanes(const d2d_scn& a, ScnR& s, int lane) {
     if (lane < D2D_MAX_CIRCLES) {
         s.cx[lane] = a.cx[lane];
         s.cy[lane] = a.cy[lane];
@@ -398,7 +398,7 @@ __device__ inline void scn_build_rest_lanes(const d2d_scn& a, Scn& s, int lane) 
 // Per-item LDS of the wave generator.
 struct GenLds {
     d2d_scn a;                 // the ABI record being built
-    Scn s;                     // its device form (obstacle placement, tables)
+    ScnR s;                    // its device form (obstacle placement; the fresh curriculum's layout)
     uint32_t win[GEN_WIN];     // the stream's first GEN_WIN words
     double wx[D2D_MAX_WPS], wy[D2D_MAX_WPS], sa[D2D_MAX_WPS], ca[D2D_MAX_WPS], seg[D2D_MAX_WPS];
     // obstacle placement (gen_obstacles_wave): the trial that starts at stream word w0 + 2 l, per lane l

@@ -55,32 +55,52 @@ constexpr double VEL_MAX = 1330.0;            // drone_2d_env.py:635
 //   RN(1 / (us[n+1] - us[n])), and the blend threshold T: in interval n QPMI2D.__call__ blends the
 //   two quadratics exactly when u < T[n] (below).
 enum { REC_XB = 0, REC_XA = 6, REC_U0 = 12, REC_U1 = 13, REC_IDU = 14, REC_T = 15, REC_N = 16 };
-// Layout (one for every path since round 4): the knots us_[k] contiguous (the knot scan of u_index
-// reads one or two cache lines from global memory, one 16-byte LDS broadcast per two knots) and the
-// interval records record-major with a one-double pad (interval n's 16 fields contiguous, 136 bytes
-// apart): from LDS a wave whose lanes sit in different intervals still reads 16 different banks per
-// field (n x 34 dwords mod 64 is distinct for n < 16), and from global memory (the fresh curriculum's
-// per-lane scenarios) one QPMI2D evaluation touches two cache lines per lane instead of 16.
-// Measured against the field-major rounds 1-3 layout (profiles/r04/layout/): corridor / S_corridor
-// / mixed unchanged, the fresh curriculum's step kernel 179 -> 105 us at 65 536 envs.
-constexpr int REC_W = REC_N + 1;
-struct Scn {
+// Two layouts of the same table, one per way K1 reads it (both in the one library, chosen per
+// handle by where K1 reads the scenarios from; the kernels are templated on the type):
+//   ScnF  field-major rec[f][n] + the knots us[k]: tables K1 stages in LDS (test scenarios, mixed
+//         maps).  Lanes in different knot intervals read different banks.
+//   ScnR  record-major with a one-double pad (interval n's 16 fields contiguous, 136 bytes apart):
+//         tables K1 reads from global memory, one lane per scenario (pools, the fresh curriculum):
+//         one QPMI2D evaluation touches two cache lines per lane instead of 16.
+// Measured (profiles/r04/layout/): ScnR for every path costs the LDS paths 0.6 % (corridor), 3 %
+// (mixed) and 5.6 % (4 096 envs); ScnF for the fresh curriculum's step kernel 179 vs 105 us.
+#ifndef D2D_REC_PAD
+#define D2D_REC_PAD 1  // A/B: ScnR's pad word (136-byte stride: LDS-bank-conflict-free)
+#endif
+constexpr int REC_W = REC_N + D2D_REC_PAD;
+#define D2D_SCN_TAIL                                                                                      \
+    double cx[D2D_MAX_CIRCLES], cy[D2D_MAX_CIRCLES], cr[D2D_MAX_CIRCLES];                               \
+    double wp_last_x, wp_last_y;                                                                          \
+    double spawn_xmin, spawn_xmax, spawn_ymin, spawn_ymax, spawn_amin, spawn_amax;                        \
+    /* the common radius when every circle has the same one (all test scenarios), else NaN (also keeps */ \
+    /* the size a multiple of 16: the probe tables staged after it stay aligned) */                       \
+    double r_uniform;
+struct ScnF {
+    static constexpr bool RM = false;
+    int32_t n_wps, n_circles;
+    double us_[D2D_MAX_WPS];
+    double rec_[REC_N][D2D_MAX_WPS];
+    D2D_SCN_TAIL
+    __host__ __device__ __forceinline__ double& rec(int f, int n) { return rec_[f][n]; }
+    __host__ __device__ __forceinline__ const double& rec(int f, int n) const { return rec_[f][n]; }
+};
+struct ScnR {
+    static constexpr bool RM = true;
     int32_t n_wps, n_circles;
     double us_[D2D_MAX_WPS];
     double rec_[D2D_MAX_WPS][REC_W];
-    double cx[D2D_MAX_CIRCLES], cy[D2D_MAX_CIRCLES], cr[D2D_MAX_CIRCLES];
-    double wp_last_x, wp_last_y;
-    double spawn_xmin, spawn_xmax, spawn_ymin, spawn_ymax, spawn_amin, spawn_amax;
-    double r_uniform;  // the common radius when every circle has the same one (all test scenarios), else NaN
-                       // (also keeps sizeof(Scn) % 16 == 0: the probe tables staged after it stay aligned)
+    D2D_SCN_TAIL
+    __host__ __device__ __forceinline__ double& rec(int f, int n) { return rec_[n][f]; }
+    __host__ __device__ __forceinline__ const double& rec(int f, int n) const { return rec_[n][f]; }
 };
-static_assert(sizeof(Scn) % 16 == 0, "Scn size");
-#define SREC(s, f, n) ((s).rec_[(n)][(f)])
+static_assert(sizeof(ScnF) % 16 == 0 && sizeof(ScnR) % 16 == 0, "Scn size");
+#define SREC(s, f, n) ((s).rec((f), (n)))
 #define SUS(s, k) ((s).us_[(k)])
 
 // Returns false if the table is outside what the record form reproduces exactly: the last-segment
 // window us[nw-2] - 0.001 must not reach back past us[nw-3] (always true for real waypoints).
-__host__ __device__ inline bool scn_build(const d2d_scn& a, Scn& s) {
+template <class S>
+__host__ __device__ inline bool scn_build(const d2d_scn& a, S& s) {
     const int nw = a.n_wps, nseg = nw - 2;
     if (nw >= 4 && !(a.us[nw - 2] - 0.001 > a.us[nw - 3])) return false;
     s.n_wps = nw;
@@ -88,7 +108,9 @@ __host__ __device__ inline bool scn_build(const d2d_scn& a, Scn& s) {
     double us[D2D_MAX_WPS];
     for (int k = 0; k < D2D_MAX_WPS; ++k) us[k] = (k < nw) ? a.us[k] : __builtin_inf();
     for (int k = 0; k < D2D_MAX_WPS; ++k) s.us_[k] = us[k];
-    for (int n = 0; n < D2D_MAX_WPS; ++n) s.rec_[n][REC_N] = 0.0;  // the pad
+    if constexpr (S::RM) {
+        for (int n = 0; n < D2D_MAX_WPS && REC_W > REC_N; ++n) s.rec_[n][REC_W - 1] = 0.0;  // the pad
+    }
     for (int n = 0; n < D2D_MAX_WPS; ++n) {
         const int b = (n < nseg - 1) ? n : nseg - 1;
         const int q = (n == 0) ? nseg - 1 : ((n - 1 < nseg - 1) ? n - 1 : nseg - 1);
@@ -235,7 +257,8 @@ __device__ __forceinline__ int pool_pick(uint64_t seed, uint32_t gid, uint32_t e
     philox(gid, episode, 2u, 0u, (uint32_t)seed, (uint32_t)(seed >> 32), o);
     return (int)(o[0] % (uint32_t)n_scn);
 }
-__device__ __forceinline__ void spawn_draw(const Scn& s, uint64_t seed, uint32_t gid, uint32_t episode,
+template <class S>
+__device__ __forceinline__ void spawn_draw(const S& s, uint64_t seed, uint32_t gid, uint32_t episode,
                                            double& x, double& y, double& th) {
     uint32_t o[4];
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
@@ -253,7 +276,8 @@ __device__ __forceinline__ void spawn_draw(const Scn& s, uint64_t seed, uint32_t
 // the number of knots k >= 1 with !(u <= us[k]) (NaN -> n_wps-1, as the Python loop).
 // (Counting the sign bits of us[k] - u instead of compares gives the same counts and was measured
 // slower in the full kernel.)
-__device__ __forceinline__ int u_index(const Scn& s, double u) {
+template <class S>
+__device__ __forceinline__ int u_index(const S& s, double u) {
     uint32_t c = 0;
 #pragma unroll
     for (int k = 1; k < D2D_MAX_WPS; ++k) c += !(u <= SUS(s, k)) ? 1u : 0u;
@@ -265,7 +289,8 @@ struct PathK {
     double us0, last_lo, L;
     int nw;
 };
-__device__ __forceinline__ PathK path_k(const Scn& s) {
+template <class S>
+__device__ __forceinline__ PathK path_k(const S& s) {
     const int nw = s.n_wps;
     return PathK{SUS(s, 0), SUS(s, nw - 2) - 0.001, SUS(s, nw - 1), nw};
 }
@@ -291,21 +316,25 @@ __device__ __forceinline__ void path_eval_rec(const double r[REC_N], const PathK
     y = blend ? yb : yB;
     u1_out = u1;
 }
-__device__ __forceinline__ void path_eval_n(const Scn& s, const PathK& K, double u, int n, double& x, double& y,
+template <class S>
+__device__ __forceinline__ void path_eval_n(const S& s, const PathK& K, double u, int n, double& x, double& y,
                                             double& u1_out) {
     double r[REC_N];
 #pragma unroll
     for (int f = 0; f < REC_N; ++f) r[f] = SREC(s, f, n);
     path_eval_rec(r, K, u, n, x, y, u1_out);
 }
-__device__ __forceinline__ void path_eval(const Scn& s, const PathK& K, double u, double& x, double& y) {
+template <class S>
+__device__ __forceinline__ void path_eval(const S& s, const PathK& K, double u, double& x, double& y) {
     double u1;
     path_eval_n(s, K, u, u_index(s, u), x, y, u1);
 }
-__device__ __forceinline__ void path_eval(const Scn& s, double u, double& x, double& y) {
+template <class S>
+__device__ __forceinline__ void path_eval(const S& s, double u, double& x, double& y) {
     path_eval(s, path_k(s), u, x, y);
 }
-__device__ __forceinline__ double path_dist_n(const Scn& s, const PathK& K, double u, int n, double px, double py,
+template <class S>
+__device__ __forceinline__ double path_dist_n(const S& s, const PathK& K, double u, int n, double px, double py,
                                               double& u1) {
     double x, y;
     path_eval_n(s, K, u, n, x, y, u1);
@@ -331,7 +360,8 @@ struct Brent {
 constexpr double BR_SQRT_EPS = 1.4832396974191326e-08;  // sqrt(2.2e-16)
 constexpr double BR_GOLDEN = 0.3819660112501051;        // 0.5*(3.0 - sqrt(5.0))
 constexpr double BR_XATOL3 = 1e-6 / 3.0;
-__device__ __forceinline__ void brent_init(const Scn& s, const PathK& K, double px, double py, Brent& B) {
+template <class S>
+__device__ __forceinline__ void brent_init(const S& s, const PathK& K, double px, double py, Brent& B) {
     B.a = 0.0 - 10.0;
     B.b = K.L + 10.0;
     B.fulc = B.a + BR_GOLDEN * (B.b - B.a);
@@ -354,7 +384,8 @@ __device__ __forceinline__ bool brent_active(const Brent& B) {
     const double tol2 = 2.0 * tol1;
     return (fabs(B.xf - xm) > (tol2 - 0.5 * (B.b - B.a))) & (B.num < 500);
 }
-__device__ __forceinline__ void brent_step(const Scn& s, const PathK& K, double px, double py, Brent& B) {
+template <class S>
+__device__ __forceinline__ void brent_step(const S& s, const PathK& K, double px, double py, Brent& B) {
     const double a = B.a, b = B.b, xf = B.xf, fx = B.fx, nfc = B.nfc, fulc = B.fulc;
     // the upper knot of a's interval, for the one-compare interval test.  (Carrying it in the state,
     // or prefetching a's whole record before the candidate is known, measured no faster -- also with
@@ -403,7 +434,7 @@ __device__ __forceinline__ void brent_step(const Scn& s, const PathK& K, double 
     } else {
         // the knot scan re-reads the knots each time (an opaque pointer stops the compiler from
         // keeping all 15 in registers across the loop: the fast path does not need them)
-        const Scn* sp = &s;
+        const S* sp = &s;
         asm volatile("" : "+v"(sp));
         ix = u_index(*sp, x);
     }
@@ -436,7 +467,8 @@ __device__ __forceinline__ void brent_step(const Scn& s, const PathK& K, double 
     B.fx = le ? fu : fx;
 }
 // (iu: the knot interval of the result, u_index(s, result), tracked by the search)
-__device__ __forceinline__ double closest_u(const Scn& s, double px, double py, int& iu) {
+template <class S>
+__device__ __forceinline__ double closest_u(const S& s, double px, double py, int& iu) {
     const PathK K = path_k(s);
     Brent B;
     brent_init(s, K, px, py, B);
@@ -493,7 +525,8 @@ struct BrTab {
 };
 
 // forced run of kind `kind` (one thread per scenario and kind; table generation, not on the step path)
-__device__ __forceinline__ void brtab_build(const Scn& s, int kind, BrTab& T) {
+template <class SC>
+__device__ __forceinline__ void brtab_build(const SC& s, int kind, BrTab& T) {
     const PathK K = path_k(s);
     Brent B;
     B.a = 0.0 - 10.0;
@@ -666,8 +699,8 @@ __device__ __forceinline__ void bt_verify(const BtHot* hot, BtLane& L, int k0, i
 }
 // resume brent_step from the snapshot before step dev (a search that followed the table restores
 // its final state, which is inactive unless the march is longer than BT_K); iu = result's interval
-template <bool LT>
-__device__ __forceinline__ double bt_finish(const Scn& s, const BrTab& T, const BtHot* hot, int kind, int dev,
+template <bool LT, class SC>
+__device__ __forceinline__ double bt_finish(const SC& s, const BrTab& T, const BtHot* hot, int kind, int dev,
                                             double px, double py, int& iu) {
     const BtSnap& S = T.snap[kind][dev];
     Brent B;
@@ -694,8 +727,8 @@ __device__ __forceinline__ double bt_finish(const Scn& s, const BrTab& T, const 
     iu = B.ixf;
     return B.xf;
 }
-template <bool LT>
-__device__ __forceinline__ double closest_u_tab(const Scn& s, const BrTab& T, const BtHot* hot, double px,
+template <bool LT, class S>
+__device__ __forceinline__ double closest_u_tab(const S& s, const BrTab& T, const BtHot* hot, double px,
                                                 double py, int& iu) {
     BtLane L = bt_start<LT>(T, hot, px, py);
     bt_verify<LT>(hot, L, 1, BT_K, px, py);
@@ -804,7 +837,8 @@ __device__ __forceinline__ void advance_position(Body& b) {
     b.py = b.py + (b.vy + 0.0) * DT;
     b.a = b.a + (b.w + 0.0) * DT;
 }
-__device__ __forceinline__ bool frame_hits(const Scn& s, const Body& F, double cs, double sn) {
+template <class S>
+__device__ __forceinline__ bool frame_hits(const S& s, const Body& F, double cs, double sn) {
     bool hit = false;
     for (int k = 0; k < ((D2D_ABLATE & 8) ? 0 : s.n_circles); ++k) {
         const double dx = s.cx[k] - F.px, dy = s.cy[k] - F.py;
@@ -827,7 +861,8 @@ __device__ __forceinline__ bool frame_hits(const Scn& s, const Body& F, double c
     }
     return hit;
 }
-__device__ __forceinline__ bool phys_positions(const Scn& s, Body B[3], double fL, double fR, double cs[3],
+template <class S>
+__device__ __forceinline__ bool phys_positions(const S& s, Body B[3], double fL, double fR, double cs[3],
                                                double sn[3], double& fx, double& fy, double& tq) {
     // forces on the frame at local (-40,0) then (40,0): cpBodyApplyForceAtLocalPoint
     double c0, s0;
@@ -873,7 +908,8 @@ __device__ __forceinline__ bool phys_positions(const Scn& s, Body B[3], double f
 }
 // The frame's post-step position and contact flag from its pre-step state alone (forces only act
 // on velocities): lets the observation waves start without waiting for the physics wave.
-__device__ __forceinline__ bool frame_advance(const Scn& s, Body& F) {
+template <class S>
+__device__ __forceinline__ bool frame_advance(const S& s, Body& F) {
     advance_position(F);
     double sn, cs;
     sincos_d(F.a, sn, cs);
@@ -1003,7 +1039,8 @@ __device__ __forceinline__ void phys_velocities(const Arms& A, const double pos[
 }
 
 // whole step, registers only (reference / diagnostics)
-__device__ __forceinline__ bool space_step(const Scn& s, double damping_dt, Body B[3], double j[12], double fL,
+template <class S>
+__device__ __forceinline__ bool space_step(const S& s, double damping_dt, Body B[3], double j[12], double fL,
                                            double fR) {
     double cs[3], sn[3], fx, fy, tq;
     const bool hit = phys_positions(s, B, fL, fR, cs, sn, fx, fy, tq);
@@ -1062,7 +1099,8 @@ __device__ __forceinline__ void sensor_vel(const Body& F, double o[19]) {
     sincos_d(F.a, sa, ca);
     sensor_vel(F, sa, ca, o);
 }
-__device__ __forceinline__ void sensor_pos(const d2d_cfg& cfg, const Scn& s, double x, double y, double al,
+template <class S>
+__device__ __forceinline__ void sensor_pos(const d2d_cfg& cfg, const S& s, double x, double y, double al,
                                            double o[19]) {
     const double W = cfg.screen_w, H = cfg.screen_h;
     o[3] = al / PI;
@@ -1160,7 +1198,8 @@ __device__ __forceinline__ void sensor_pos(const d2d_cfg& cfg, const Scn& s, dou
         o[10 + 3 * jj] = have ? ca : 0.0;
     }
 }
-__device__ __forceinline__ void sensor_obs(const d2d_cfg& cfg, const Scn& s, const Body& F, double o[19]) {
+template <class S>
+__device__ __forceinline__ void sensor_obs(const d2d_cfg& cfg, const S& s, const Body& F, double o[19]) {
     sensor_vel(F, o);
     sensor_pos(cfg, s, F.px, F.py, F.a, o);
 }
@@ -1170,7 +1209,8 @@ __device__ __forceinline__ void sensor_obs(const d2d_cfg& cfg, const Scn& s, con
 // sticky LA lock in `flags`; returns the closest point (cpx, cpy) for the path-adherence reward.
 // the part after the closest-point search, for a given u
 // (iu: u's knot interval if known, else -1)
-__device__ __forceinline__ void path_obs_u(const d2d_cfg& cfg, const Scn& s, double x, double y, double al,
+template <class S>
+__device__ __forceinline__ void path_obs_u(const d2d_cfg& cfg, const S& s, double x, double y, double al,
                                            double u, uint32_t& flags, double o[8], int iu = -1) {
     const double W = cfg.screen_w, H = cfg.screen_h;
     double cpx, cpy, u1;
@@ -1202,8 +1242,8 @@ __device__ __forceinline__ void path_obs_u(const d2d_cfg& cfg, const Scn& s, dou
 }
 // T: the scenario's golden-march tables (null: plain search); hot: their probe table staged in LDS
 // (LT) or null (read from T in global memory)
-template <bool LT = false>
-__device__ __forceinline__ void path_obs(const d2d_cfg& cfg, const Scn& s, const BrTab* T, double x, double y,
+template <bool LT = false, class S>
+__device__ __forceinline__ void path_obs(const d2d_cfg& cfg, const S& s, const BrTab* T, double x, double y,
                                          double al, uint32_t& flags, double o[8], const BtHot* hot = nullptr) {
     int iu = -1;
     const double u = (D2D_ABLATE & 1) ? clipd(x - 100.0, -10.0, SUS(s, s.n_wps - 1))
@@ -1218,7 +1258,8 @@ __device__ __forceinline__ void path_obs(const d2d_cfg& cfg, const Scn& s, const
 // end conditions that need only the post-physics frame (drone_2d_env.py:543-571): collision,
 // reach-end (decoded target distance), AA (decoded alpha), time-up.  Known before the observation,
 // which lets the cooperative kernel start the auto-reset observation concurrently.
-__device__ __forceinline__ int end_cause(const d2d_cfg& cfg, const Scn& s, const Body& F, bool collided, int t) {
+template <class S>
+__device__ __forceinline__ int end_cause(const d2d_cfg& cfg, const S& s, const Body& F, bool collided, int t) {
     const double W = cfg.screen_w, H = cfg.screen_h;
     const double tdx = invm1to1(m1to1(s.wp_last_x - F.px, 0.0, W), 0.0, W);
     const double tdy = invm1to1(m1to1(s.wp_last_y - F.py, 0.0, H), 0.0, H);
@@ -1243,7 +1284,8 @@ __device__ __forceinline__ int end_cause(const d2d_cfg& cfg, const Scn& s, const
 struct CAStatic {
     double d, os, oc, lpa, lca, rr;   // closest obstacle: distance, bearing (sin, cos) = obs 9, 10
 };
-__device__ __forceinline__ CAStatic ca_static(const d2d_cfg& cfg, const Scn& s, const double* o) {
+template <class S>
+__device__ __forceinline__ CAStatic ca_static(const d2d_cfg& cfg, const S& s, const double* o) {
     const double W = cfg.screen_w, H = cfg.screen_h;
     CAStatic C{__builtin_inf(), 0.0, 1.0, 1.0, 1.0, 0.0};
     if (s.n_circles > 0) {
@@ -1337,7 +1379,8 @@ __device__ __forceinline__ RewardSum reward_sum(const d2d_cfg& cfg, const Reward
 }
 
 // full single-lane observation (reset kernel)
-__device__ __forceinline__ void observe(const d2d_cfg& cfg, const Scn& s, const BrTab* T, const Body& F,
+template <class S>
+__device__ __forceinline__ void observe(const d2d_cfg& cfg, const S& s, const BrTab* T, const Body& F,
                                         uint32_t& flags, double obs[D2D_OBS_DIM]) {
     sensor_obs(cfg, s, F, obs);
     path_obs(cfg, s, T, F.px, F.py, F.a, flags, obs + 19);

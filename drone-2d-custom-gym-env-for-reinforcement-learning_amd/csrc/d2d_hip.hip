@@ -41,7 +41,8 @@ struct d2d_handle {
     double* st = nullptr;
     int32_t* ist = nullptr;
     double* acc = nullptr;
-    d2d::Scn* scn = nullptr;    // device table: ABI scenarios + derived fields
+    void* scn = nullptr;        // device table: ABI scenarios + derived fields, ScnF or ScnR (rm)
+    bool rm = false;            // the table's layout: ScnR where K1 reads it from global memory
     d2d::BrTab* brt = nullptr;  // golden-march tables of the scenarios (d2d_brtab_kernel)
     int32_t* env_scn = nullptr;
     // pool mode: the scenario table has two halves of pool_n entries; resets draw from the half at
@@ -129,7 +130,7 @@ hipError_t fresh_regen(d2d_t* h, hipStream_t stream, bool restore = false, bool 
     f.seed = h->seed;
     f.env_id_base = (uint32_t)h->cfg.env_id_base;
     f.abi = h->abi;
-    f.scn = h->scn;
+    f.scn = static_cast<d2d::ScnR*>(h->scn);  // (fresh mode: h->rm)
     f.tag = h->scn_tag;
     f.gclk = h->gclk;
     f.clock = h->clock;
@@ -152,17 +153,50 @@ hipError_t fresh_regen(d2d_t* h, hipStream_t stream, bool restore = false, bool 
 }
 bool fresh_mode(const d2d_t* h) { return h->cfg.scn_pool == 2; }
 
+// The scenario table's layout (d2d_device.h ScnF / ScnR): ScnR exactly when K1 will read it from
+// global memory -- the fresh curriculum, and tables too big to stage (pools) unless the map is grouped
+// (a grouped workgroup stages only its own scenarios).  d2d_step dispatches on the same rule.
+bool table_rm(bool fresh, bool grouped, size_t n_total) {
+    if (fresh) return true;
+    if (grouped) return false;
+    return sizeof(d2d::ScnF) * n_total + sizeof(K1Shared) > K1_LDS_BUDGET;
+}
+size_t scn_size(bool rm) { return rm ? sizeof(d2d::ScnR) : sizeof(d2d::ScnF); }
+void* scn_at(const d2d_t* h, size_t k) { return static_cast<char*>(h->scn) + k * scn_size(h->rm); }
+// host tables in either layout; entries with use(k) false stay zero.  False: a scenario scn_build refuses
+template <class S>
+bool build_tables_t(const d2d_scn* src, size_t n, std::vector<unsigned char>& out, const std::vector<bool>* use) {
+    out.assign(n * sizeof(S), 0);
+    for (size_t k = 0; k < n; ++k)
+        if ((!use || (*use)[k]) && !d2d::scn_build(src[k], *reinterpret_cast<S*>(out.data() + k * sizeof(S))))
+            return false;
+    return true;
+}
+bool build_tables(bool rm, const d2d_scn* src, size_t n, std::vector<unsigned char>& out,
+                  const std::vector<bool>* use = nullptr) {
+    return rm ? build_tables_t<d2d::ScnR>(src, n, out, use) : build_tables_t<d2d::ScnF>(src, n, out, use);
+}
+void launch_brtab(bool rm, const void* scn, int n, d2d::BrTab* out) {
+    const dim3 grid((2 * n + 63) / 64);
+    if (rm) hipLaunchKernelGGL(d2d_brtab_kernel<d2d::ScnR>, grid, dim3(64), 0, 0, (const d2d::ScnR*)scn, n, out);
+    else hipLaunchKernelGGL(d2d_brtab_kernel<d2d::ScnF>, grid, dim3(64), 0, 0, (const d2d::ScnF*)scn, n, out);
+}
+
 // K4: fill every cache entry that does not belong to its env's current episode, ordered on `stream`
 hipError_t rc_fill(d2d_t* h, hipStream_t stream, bool force = false) {
     StepArgs a = make_args(h);
     a.fill_force = force ? 1 : 0;
     const dim3 grid((h->ns + FILL_SPB - 1) / FILL_SPB);
     // dynamic LDS padded to K1's per-workgroup LDS, so K4 is resident 4 per CU as K1 (d2d_fill_kernel)
-    const size_t pad = sizeof(d2d::Scn) + sizeof(d2d::BtHot) + sizeof(K1Shared) - 2048;
-    if (sizeof(d2d::Scn) * (size_t)h->n_scn <= K2_LDS_BUDGET)
-        hipLaunchKernelGGL(d2d_fill_kernel<true>, grid, dim3(BLOCK), std::max(sizeof(d2d::Scn) * h->n_scn, pad), stream, a);
-    else
-        hipLaunchKernelGGL(d2d_fill_kernel<false>, grid, dim3(BLOCK), pad, stream, a);
+    const size_t pad = sizeof(d2d::ScnF) + sizeof(d2d::BtHot) + sizeof(K1Shared) - 2048;
+    const size_t lds = scn_size(h->rm) * (size_t)h->n_scn;
+    if (lds <= K2_LDS_BUDGET) {
+        if (h->rm) hipLaunchKernelGGL((d2d_fill_kernel<true, true>), grid, dim3(BLOCK), std::max(lds, pad), stream, a);
+        else hipLaunchKernelGGL((d2d_fill_kernel<true, false>), grid, dim3(BLOCK), std::max(lds, pad), stream, a);
+    } else {
+        if (h->rm) hipLaunchKernelGGL((d2d_fill_kernel<false, true>), grid, dim3(BLOCK), pad, stream, a);
+        else hipLaunchKernelGGL((d2d_fill_kernel<false, false>), grid, dim3(BLOCK), pad, stream, a);
+    }
     return hipGetLastError();
 }
 // drop every entry (new seed, counters or scenarios) and refill, ordered on `stream`
@@ -474,14 +508,16 @@ int32_t d2d_set_scenarios(d2d_t* h, const d2d_scn* scns, int32_t n_scn, const in
                 return fail(D2D_E_ARG, "d2d_set_scenarios: env scenario index out of range");
     }
     // validate and build everything before touching the handle: a bad scenario leaves it as it was
-    std::vector<d2d::Scn> tab((size_t)n_scn);
-    for (int k = 0; k < n_scn; ++k) {
-        if (!d2d::scn_build(scns[k], tab[k]))
-            return fail(D2D_E_ARG, "d2d_set_scenarios: us[n_wps-2] - us[n_wps-3] must exceed 0.001");
-    }
+    // pool mode: room for a second pool half (d2d_refresh_pool), zero until the first refresh
+    const size_t T = (size_t)n_scn * (h->cfg.scn_pool ? 2 : 1);
+    const bool grouped = env_scn_host && n_scn > 1 && !h->cfg.scn_pool;
+    const bool rm = table_rm(false, grouped, T);
+    std::vector<unsigned char> tab;
+    if (!build_tables(rm, scns, (size_t)n_scn, tab))
+        return fail(D2D_E_ARG, "d2d_set_scenarios: us[n_wps-2] - us[n_wps-3] must exceed 0.001");
     DeviceGuard g(h->device);
     hipError_t e;
-    d2d::Scn* scn = nullptr;
+    void* scn = nullptr;
     d2d::BrTab* brt = nullptr;
     d2d_scn* abi = nullptr;
     auto drop = [&](hipError_t err, const char* what) {
@@ -490,12 +526,10 @@ int32_t d2d_set_scenarios(d2d_t* h, const d2d_scn* scns, int32_t n_scn, const in
         if (abi) (void)hipFree(abi);
         return hip_fail(err, what);
     };
-    // pool mode: room for a second pool half (d2d_refresh_pool), zero until the first refresh
-    const size_t T = (size_t)n_scn * (h->cfg.scn_pool ? 2 : 1);
-    const size_t bytes = sizeof(d2d::Scn) * (size_t)n_scn;
-    if ((e = hipMalloc(&scn, sizeof(d2d::Scn) * T)) != hipSuccess) return drop(e, "hipMalloc scn");
-    if ((e = hipMemset(scn, 0, sizeof(d2d::Scn) * T)) != hipSuccess) return drop(e, "hipMemset scn");
-    if ((e = hipMemcpy(scn, tab.data(), bytes, hipMemcpyHostToDevice)) != hipSuccess) return drop(e, "hipMemcpy scn");
+    const size_t sz = scn_size(rm);
+    if ((e = hipMalloc(&scn, sz * T)) != hipSuccess) return drop(e, "hipMalloc scn");
+    if ((e = hipMemset(scn, 0, sz * T)) != hipSuccess) return drop(e, "hipMemset scn");
+    if ((e = hipMemcpy(scn, tab.data(), tab.size(), hipMemcpyHostToDevice)) != hipSuccess) return drop(e, "hipMemcpy scn");
     if (h->cfg.scn_pool) {  // pool mode keeps the ABI records for checkpoints / readback
         if ((e = hipMalloc(&abi, sizeof(d2d_scn) * T)) != hipSuccess) return drop(e, "hipMalloc abi");
         if ((e = hipMemset(abi, 0, sizeof(d2d_scn) * T)) != hipSuccess) return drop(e, "hipMemset abi");
@@ -505,14 +539,14 @@ int32_t d2d_set_scenarios(d2d_t* h, const d2d_scn* scns, int32_t n_scn, const in
     // golden-march tables: forced searches on the device (same arithmetic as the step kernels)
     if ((e = hipMalloc(&brt, sizeof(d2d::BrTab) * T)) != hipSuccess) return drop(e, "hipMalloc brt");
     if ((e = hipMemset(brt, 0, sizeof(d2d::BrTab) * T)) != hipSuccess) return drop(e, "hipMemset brt");
-    hipLaunchKernelGGL(d2d_brtab_kernel, dim3((2 * n_scn + 63) / 64), dim3(64), 0, 0, scn, n_scn, brt);
+    launch_brtab(rm, scn, n_scn, brt);
     if ((e = hipGetLastError()) != hipSuccess) return drop(e, "d2d_brtab_kernel launch");
     if ((e = hipMemset(h->pool_dev, 0, sizeof(int32_t))) != hipSuccess) return drop(e, "hipMemset pool");
     if ((e = hipDeviceSynchronize()) != hipSuccess) return drop(e, "d2d_brtab_kernel");
     // slot layout: grouped for a static mixed map (pool mode redraws scenarios at every reset);
     // the current state moves into the new layout
     std::vector<int32_t> lanes, ws;
-    if (env_scn_host && n_scn > 1 && !h->cfg.scn_pool) {
+    if (grouped) {
         make_groups(h->n, env_scn_host, n_scn, lanes, ws);
         if ((int)h->scn_cost.size() == n_scn) balance_groups(h->n_cu, h->scn_cost.data(), n_scn, lanes, ws);
     }
@@ -535,6 +569,7 @@ int32_t d2d_set_scenarios(d2d_t* h, const d2d_scn* scns, int32_t n_scn, const in
     if (h->brt) (void)hipFree(h->brt);
     if (h->abi) (void)hipFree(h->abi);
     h->scn = scn;
+    h->rm = rm;
     h->brt = brt;
     h->abi = abi;
     h->n_scn = (int)T;
@@ -627,10 +662,15 @@ int32_t d2d_reset(d2d_t* h, const uint8_t* mask_dev, uint64_t seed, float* obs_d
     a.obs = obs_dev;
     a.mask = mask_dev;
     const dim3 grid((h->ns + BLOCK - 1) / BLOCK);
-    if (sizeof(d2d::Scn) * (size_t)h->n_scn <= K2_LDS_BUDGET)
-        hipLaunchKernelGGL(d2d_reset_kernel<true>, grid, dim3(BLOCK), sizeof(d2d::Scn) * h->n_scn, (hipStream_t)stream, a);
-    else
-        hipLaunchKernelGGL(d2d_reset_kernel<false>, grid, dim3(BLOCK), 0, (hipStream_t)stream, a);
+    const size_t lds = scn_size(h->rm) * (size_t)h->n_scn;
+    const hipStream_t rs = (hipStream_t)stream;
+    if (lds <= K2_LDS_BUDGET) {
+        if (h->rm) hipLaunchKernelGGL((d2d_reset_kernel<true, true>), grid, dim3(BLOCK), lds, rs, a);
+        else hipLaunchKernelGGL((d2d_reset_kernel<true, false>), grid, dim3(BLOCK), lds, rs, a);
+    } else {
+        if (h->rm) hipLaunchKernelGGL((d2d_reset_kernel<false, true>), grid, dim3(BLOCK), 0, rs, a);
+        else hipLaunchKernelGGL((d2d_reset_kernel<false, false>), grid, dim3(BLOCK), 0, rs, a);
+    }
     e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "d2d_reset launch");
     if (fresh_mode(h) && (e = fresh_regen(h, (hipStream_t)stream)) != hipSuccess)
@@ -660,8 +700,8 @@ int32_t d2d_step(d2d_t* h, const float* act_dev, float* obs_dev, float* rew_dev,
     a.info = info_dev;
     a.tobs = term_obs_dev;
     const dim3 grid((h->n + EPB - 1) / EPB);
-    const size_t lds_scn = sizeof(d2d::Scn) * (size_t)h->n_scn, lds_hot = sizeof(d2d::BtHot) * (size_t)h->n_scn;
-    static_assert(sizeof(d2d::Scn) + sizeof(d2d::BtHot) + sizeof(K1Shared) <= K1_LDS_BUDGET, "grouped K1 LDS");
+    const size_t lds_scn = sizeof(d2d::ScnF) * (size_t)h->n_scn, lds_hot = sizeof(d2d::BtHot) * (size_t)h->n_scn;
+    static_assert(sizeof(d2d::ScnF) + sizeof(d2d::BtHot) + sizeof(K1Shared) <= K1_LDS_BUDGET, "grouped K1 LDS");
     {
         // the three-way table re-check pays when the SIMDs have idle issue slots (at most one K1
         // workgroup per CU: 4 096 / 16 384 envs -4 %), not at full load (65 536 envs +3.6 %)
@@ -671,13 +711,13 @@ int32_t d2d_step(d2d_t* h, const float* act_dev, float* obs_dev, float* rew_dev,
             hipLaunchKernelGGL(kern, g, dim3(K1_THREADS), lds, (hipStream_t)stream, a);
         };
         if (h->lane_env) {
-            const size_t lds = sizeof(d2d::Scn) + sizeof(d2d::BtHot);
+            const size_t lds = sizeof(d2d::ScnF) + sizeof(d2d::BtHot);
             if (s3) launch(d2d_step_grouped_kernel<true>, dim3(h->n_groups), lds);
             else launch(d2d_step_grouped_kernel<false>, dim3(h->n_groups), lds);
-        } else if (a.brt && lds_scn + lds_hot + sizeof(K1Shared) <= K1_LDS_BUDGET) {
+        } else if (!h->rm && a.brt && lds_scn + lds_hot + sizeof(K1Shared) <= K1_LDS_BUDGET) {
             if (s3) launch(d2d_step_kernel<true, true, true>, grid, lds_scn + lds_hot);
             else launch(d2d_step_kernel<true, true, false>, grid, lds_scn + lds_hot);
-        } else if (lds_scn + sizeof(K1Shared) <= K1_LDS_BUDGET) {
+        } else if (!h->rm) {  // (table_rm: a ScnF table fits K1's LDS)
             if (s3) launch(d2d_step_kernel<true, false, true>, grid, lds_scn);
             else launch(d2d_step_kernel<true, false, false>, grid, lds_scn);
         } else {
@@ -758,13 +798,13 @@ int32_t d2d_refresh_pool(d2d_t* h, const d2d_scn* scns, int32_t n_scn) {
     if (h->cfg.scn_pool != 1) return fail(D2D_E_ARG, "d2d_refresh_pool: pool mode only (cfg.scn_pool = 1)");
     if (h->n_scn <= 0) return fail(D2D_E_STATE, "d2d_refresh_pool: call d2d_set_scenarios first");
     if (n_scn != h->pool_n) return fail(D2D_E_ARG, "d2d_refresh_pool: n_scn must equal the pool size");
-    std::vector<d2d::Scn> tab((size_t)n_scn);
     for (int k = 0; k < n_scn; ++k) {
         const d2d_scn& s = scns[k];
-        if (s.n_wps < 3 || s.n_wps > D2D_MAX_WPS || s.n_circles < 0 || s.n_circles > D2D_MAX_CIRCLES ||
-            !d2d::scn_build(s, tab[k]))
+        if (s.n_wps < 3 || s.n_wps > D2D_MAX_WPS || s.n_circles < 0 || s.n_circles > D2D_MAX_CIRCLES)
             return fail(D2D_E_ARG, "d2d_refresh_pool: invalid scenario");
     }
+    std::vector<unsigned char> tab;
+    if (!build_tables(h->rm, scns, (size_t)n_scn, tab)) return fail(D2D_E_ARG, "d2d_refresh_pool: invalid scenario");
     DeviceGuard g(h->device);
     hipError_t e;
     const size_t P = (size_t)n_scn;
@@ -780,11 +820,11 @@ int32_t d2d_refresh_pool(d2d_t* h, const d2d_scn* scns, int32_t n_scn) {
     if (busy)
         return fail(D2D_E_STATE, "d2d_refresh_pool: " + std::to_string(busy) +
                                      " envs still run episodes from the pool before the previous refresh");
-    if ((e = hipMemcpy(h->scn + half, tab.data(), P * sizeof(d2d::Scn), hipMemcpyHostToDevice)) != hipSuccess ||
+    if ((e = hipMemcpy(scn_at(h, half), tab.data(), tab.size(), hipMemcpyHostToDevice)) != hipSuccess ||
         (h->abi && (e = hipMemcpy(h->abi + half, scns, P * sizeof(d2d_scn), hipMemcpyHostToDevice)) != hipSuccess) ||
         (e = hipMemset(h->brt + half, 0, P * sizeof(d2d::BrTab))) != hipSuccess)
         return hip_fail(e, "d2d_refresh_pool: upload");
-    hipLaunchKernelGGL(d2d_brtab_kernel, dim3((2 * n_scn + 63) / 64), dim3(64), 0, 0, h->scn + half, n_scn, h->brt + half);
+    launch_brtab(h->rm, scn_at(h, half), n_scn, h->brt + half);
     if ((e = hipGetLastError()) != hipSuccess || (e = hipDeviceSynchronize()) != hipSuccess)
         return hip_fail(e, "d2d_refresh_pool: d2d_brtab_kernel");
     if ((e = hipMemcpy(h->pool_dev, &half, sizeof(int32_t), hipMemcpyHostToDevice)) != hipSuccess)
@@ -846,31 +886,34 @@ int32_t d2d_restore_pool(d2d_t* h, const d2d_scn* scns, int32_t n_total, int32_t
     if (active_base != 0 && active_base != P) return fail(D2D_E_ARG, "d2d_restore_pool: active_base must be 0 or pool_n");
     if (!(valid_mask & (active_base ? 2 : 1)) || (valid_mask & ~3))
         return fail(D2D_E_ARG, "d2d_restore_pool: the active half must be valid");
-    std::vector<d2d::Scn> tab((size_t)n_total);
+    std::vector<bool> use((size_t)n_total);
     for (int k = 0; k < n_total; ++k) {
-        if (!(valid_mask & (k >= P ? 2 : 1))) continue;
+        use[k] = (valid_mask & (k >= P ? 2 : 1)) != 0;
+        if (!use[k]) continue;
         const d2d_scn& sc = scns[k];
-        if (sc.n_wps < 3 || sc.n_wps > D2D_MAX_WPS || sc.n_circles < 0 || sc.n_circles > D2D_MAX_CIRCLES ||
-            !d2d::scn_build(sc, tab[k]))
+        if (sc.n_wps < 3 || sc.n_wps > D2D_MAX_WPS || sc.n_circles < 0 || sc.n_circles > D2D_MAX_CIRCLES)
             return fail(D2D_E_ARG, "d2d_restore_pool: invalid scenario");
     }
+    std::vector<unsigned char> tab;
+    if (!build_tables(h->rm, scns, (size_t)n_total, tab, &use)) return fail(D2D_E_ARG, "d2d_restore_pool: invalid scenario");
+    const size_t sz = scn_size(h->rm);
     DeviceGuard g(h->device);
     hipError_t e;
     if ((e = hipDeviceSynchronize()) != hipSuccess) return hip_fail(e, "d2d_restore_pool: sync");
     for (int half = 0; half < 2; ++half) {
         const size_t o = (size_t)half * P;
         if (!(valid_mask & (1 << half))) {
-            if ((e = hipMemset(h->scn + o, 0, P * sizeof(d2d::Scn))) != hipSuccess ||
+            if ((e = hipMemset(scn_at(h, o), 0, P * sz)) != hipSuccess ||
                 (e = hipMemset(h->abi + o, 0, P * sizeof(d2d_scn))) != hipSuccess ||
                 (e = hipMemset(h->brt + o, 0, P * sizeof(d2d::BrTab))) != hipSuccess)
                 return hip_fail(e, "d2d_restore_pool: clear");
             continue;
         }
-        if ((e = hipMemcpy(h->scn + o, tab.data() + o, P * sizeof(d2d::Scn), hipMemcpyHostToDevice)) != hipSuccess ||
+        if ((e = hipMemcpy(scn_at(h, o), tab.data() + o * sz, P * sz, hipMemcpyHostToDevice)) != hipSuccess ||
             (e = hipMemcpy(h->abi + o, scns + o, P * sizeof(d2d_scn), hipMemcpyHostToDevice)) != hipSuccess ||
             (e = hipMemset(h->brt + o, 0, P * sizeof(d2d::BrTab))) != hipSuccess)
             return hip_fail(e, "d2d_restore_pool: upload");
-        hipLaunchKernelGGL(d2d_brtab_kernel, dim3((2 * P + 63) / 64), dim3(64), 0, 0, h->scn + o, P, h->brt + o);
+        launch_brtab(h->rm, scn_at(h, o), P, h->brt + o);
         if ((e = hipGetLastError()) != hipSuccess) return hip_fail(e, "d2d_restore_pool: d2d_brtab_kernel");
     }
     if ((e = hipMemcpy(h->pool_dev, &active_base, sizeof(int32_t), hipMemcpyHostToDevice)) != hipSuccess ||
@@ -906,13 +949,14 @@ int32_t d2d_set_curriculum(d2d_t* h, const d2d_curriculum* c) {
         h->gclk = nullptr;
         h->fresh_q = nullptr;
         h->n_scn = 0;
-        if ((e = hipMalloc(&h->scn, sizeof(d2d::Scn) * S)) != hipSuccess ||
+        h->rm = true;  // (the fresh curriculum's tables are read per lane from global memory)
+        if ((e = hipMalloc(&h->scn, sizeof(d2d::ScnR) * S)) != hipSuccess ||
             (e = hipMalloc(&h->abi, sizeof(d2d_scn) * S)) != hipSuccess ||
             (e = hipMalloc(&h->scn_tag, sizeof(int32_t) * S)) != hipSuccess ||
             (e = hipMalloc(&h->gclk, sizeof(int64_t) * S)) != hipSuccess ||
             (e = hipMalloc(&h->fresh_q, sizeof(int32_t) * (S + 2))) != hipSuccess ||
             (e = hipMemset(h->fresh_q, 0, sizeof(int32_t) * (S + 2))) != hipSuccess ||
-            (e = hipMemset(h->scn, 0, sizeof(d2d::Scn) * S)) != hipSuccess ||
+            (e = hipMemset(h->scn, 0, sizeof(d2d::ScnR) * S)) != hipSuccess ||
             (e = hipMemset(h->abi, 0, sizeof(d2d_scn) * S)) != hipSuccess ||
             (e = hipMemset(h->gclk, 0, sizeof(int64_t) * S)) != hipSuccess)
             return hip_fail(e, "d2d_set_curriculum: hipMalloc");

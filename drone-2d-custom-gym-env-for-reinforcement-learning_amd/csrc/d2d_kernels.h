@@ -29,6 +29,8 @@
 // K4 d2d_fill_kernel: fills the auto-reset observation cache (the envs that need it compacted,
 // four waves per 64 of them: fill_split).
 #pragma once
+#include <type_traits>
+
 #include "d2d_curriculum.h"
 #include "d2d_device.h"
 
@@ -62,7 +64,7 @@ struct StepArgs {
     double* st;              // [NSTATE][n]
     int32_t* ist;            // [NISTATE][n]
     double* acc;             // [NSTATS][n]
-    const Scn* scn;          // [n_scn]
+    const void* scn;         // [n_scn] ScnF or ScnR (d2d_t::rm), see scn_tab
     const BrTab* brt;        // [n_scn] golden-march tables (d2d_brtab_kernel), or null
     int32_t* env_scn;        // [n] or null (all scenario 0); rewritten at resets in pool mode
     int32_t* fill_ctl;         // K4's device tick [0] and finished-workgroup count [1]
@@ -104,6 +106,11 @@ struct StepArgs {
     int32_t* fq;              // [2 n] slots
     int32_t* fqc;             // [0]: queue length
 };
+
+// the scenario table in the layout the launch was instantiated for (ScnF: the handle stages its
+// scenarios in LDS; ScnR: K1 reads them from global memory, d2d_hip.hip table_rm)
+template <class S>
+__device__ __forceinline__ const S* scn_tab(const StepArgs& a) { return static_cast<const S*>(a.scn); }
 
 // Auto-reset observation cache.  The observation an env gets when it auto-resets depends only on
 // (seed, env id, episode counter, scenario), so it is computed ahead of time, while the env is still
@@ -179,12 +186,12 @@ __device__ __forceinline__ size_t rc_entry(const StepArgs& a, int i, uint32_t ep
 // Scenarios [first, first + count) into LDS; the returned table is indexed by the global scenario
 // index (a grouped K1 workgroup stages only its own scenario: the base is offset by -first, LDS
 // addresses are 32-bit and wrap back into the staged block for the indices it holds).
-template <bool LDS, int NT>
-__device__ __forceinline__ const Scn* stage_scenarios(const StepArgs& a, Scn* lds, int first = 0, int count = -1) {
-    if (!LDS) return a.scn;
+template <bool LDS, int NT, class S>
+__device__ __forceinline__ const S* stage_scenarios(const StepArgs& a, S* lds, int first = 0, int count = -1) {
+    if (!LDS) return scn_tab<S>(a);
     if (count < 0) count = a.n_scn;
-    const int words = count * (int)(sizeof(Scn) / 8);
-    const double* src = reinterpret_cast<const double*>(a.scn + first);
+    const int words = count * (int)(sizeof(S) / 8);
+    const double* src = reinterpret_cast<const double*>(scn_tab<S>(a) + first);
     double* dst = reinterpret_cast<double*>(lds);
     for (int k = threadIdx.x; k < words; k += NT) dst[k] = src[k];
     return lds - first;
@@ -241,7 +248,8 @@ __device__ __forceinline__ Body load_frame(const StepArgs& a, int i) {
                 fld(a.st, 3, n, i), fld(a.st, 4, n, i), fld(a.st, 5, n, i)};
 }
 // next-episode spawn (test-mode reset, drone_2d_env.py:218-311, Drone.py:20-52)
-__device__ __forceinline__ void spawn_state(const StepArgs& a, const Scn& S, int i, uint32_t ep, double sp[7]) {
+template <class SC>
+__device__ __forceinline__ void spawn_state(const StepArgs& a, const SC& S, int i, uint32_t ep, double sp[7]) {
     double x, y, th;
     spawn_draw(S, a.seed, (uint32_t)a.cfg.env_id_base + (uint32_t)i, ep, x, y, th);
     double sl, cl, sr, cr;
@@ -323,8 +331,8 @@ __device__ __forceinline__ void flag_wait(const uint32_t& f) {
 // LDS, the group is pure and stages only its own scenario.  s_scn: the dynamic LDS (scenario tables
 // [+ probe tables], sized at launch).  Returns the tables indexed by global scenario id and the
 // group's (first) scenario s0.
-template <bool LDS, bool LTAB, bool GRP>
-__device__ __forceinline__ void k1_stage(const StepArgs& a, Scn* s_scn, int wg, const Scn*& scns,
+template <bool LDS, bool LTAB, bool GRP, class S>
+__device__ __forceinline__ void k1_stage(const StepArgs& a, S* s_scn, int wg, const S*& scns,
                                          const BtHot*& hots, int& s0) {
     const int ws = (GRP && LDS) ? a.wg_scn[wg] : 0;
     s0 = ws >= 0 ? ws : -ws - 2;          // a straddling group: its two scenarios s0, s0 + 1
@@ -332,7 +340,7 @@ __device__ __forceinline__ void k1_stage(const StepArgs& a, Scn* s_scn, int wg, 
     hots = nullptr;
     if (LDS && (ncopy == 1 || !LTAB)) {
         // one scenario (+ its probe table) or scenarios only: contiguous sources, LDS-DMA
-        glds_copy<K1_THREADS / 64>(s_scn, a.scn + s0, (int)sizeof(Scn) * ncopy);
+        glds_copy<K1_THREADS / 64>(s_scn, scn_tab<S>(a) + s0, (int)sizeof(S) * ncopy);
         if (LTAB) glds_copy<K1_THREADS / 64>(s_scn + 1, &a.brt[s0].hot, (int)sizeof(BtHot));
         scns = s_scn - s0;
         if (LTAB) hots = reinterpret_cast<const BtHot*>(s_scn + 1) - s0;
@@ -347,8 +355,8 @@ __device__ __forceinline__ void k1_stage(const StepArgs& a, Scn* s_scn, int wg, 
 // tables indexed by global scenario id (LDS when staged: LDS / LTAB), s0 the group's scenario.
 // All 256 threads of the group call it once; the workgroup's barriers are block-wide, so every
 // wave of the block runs k1_body exactly once.
-template <bool LDS, bool LTAB, bool GRP, bool S3 = false>
-__device__ __forceinline__ void k1_body(const StepArgs& a, const Scn* scns, const BtHot* hots, int s0, K1Shared& sh,
+template <bool LDS, bool LTAB, bool GRP, bool S3, class SC>
+__device__ __forceinline__ void k1_body(const StepArgs& a, const SC* scns, const BtHot* hots, int s0, K1Shared& sh,
                                         int wg, int role, int qt) {
     const int wave = role;
     const int lane = threadIdx.x & 63;
@@ -382,7 +390,7 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const Scn* scns, cons
     }
     __syncthreads();
     STAMP(1);
-    const Scn& S = scns[sh.scn[lane]];
+    const SC& S = scns[sh.scn[lane]];
     float* const trow = a.tobs ? a.tobs + (size_t)ie * D2D_OBS_DIM : nullptr;
     float* const orow = &sh.u.p.obs[lane * D2D_OBS_DIM];
 
@@ -557,7 +565,7 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const Scn* scns, cons
                     for (int k = 0; k < 19; ++k) row[k] = c[k];
                 } else {
                     const uint32_t ep = sh.ep[lane];
-                    const Scn& SN = scns[next_scenario(a, ie, ep)];
+                    const SC& SN = scns[next_scenario(a, ie, ep)];
                     double sp[7], so[19];
                     spawn_state(a, SN, ie, ep, sp);
                     sensor_obs(a.cfg, SN, Body{sp[0], sp[1], sp[2], 0.0, 0.0, 0.0}, so);
@@ -692,7 +700,7 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const Scn* scns, cons
             // the next episode: spawn state, reset observation (cached or computed), new state
             const uint32_t ep = sh.ep[lane];
             const int nscn = next_scenario(a, ie, ep);
-            const Scn& SN = scns[nscn];
+            const SC& SN = scns[nscn];
             double sp[7];
             spawn_state(a, SN, ie, ep, sp);
             uint32_t rfl = 0;
@@ -823,21 +831,24 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const Scn* scns, cons
     STAMP(6);
 }
 
-template <bool LDS, bool LTAB, bool GRP, bool S3>
-__device__ __forceinline__ void k1_group(const StepArgs& a, Scn* s_scn, K1Shared& sh, int wg) {
-    const Scn* scns;
+template <bool LDS, bool LTAB, bool GRP, bool S3, class S>
+__device__ __forceinline__ void k1_group(const StepArgs& a, S* s_scn, K1Shared& sh, int wg) {
+    const S* scns;
     const BtHot* hots;
     int s0;
-    k1_stage<LDS, LTAB, GRP>(a, s_scn, wg, scns, hots, s0);
-    k1_body<LDS, LTAB, GRP, S3>(a, scns, hots, s0, sh, wg, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6),
-                                       (int)threadIdx.x);
+    k1_stage<LDS, LTAB, GRP, S>(a, s_scn, wg, scns, hots, s0);
+    k1_body<LDS, LTAB, GRP, S3, S>(a, scns, hots, s0, sh, wg, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6),
+                                   (int)threadIdx.x);
 }
+// the dynamic LDS of every kernel (scenarios [+ probe tables], sized at launch)
+extern __shared__ __attribute__((aligned(16))) uint4 d2d_dyn_lds[];
 // S3: the three-way table re-check (D2D_SPLIT3), chosen at launch
+// (LDS: the handle's tables are ScnF, staged; otherwise ScnR, read per lane from global memory)
 template <bool LDS, bool LTAB, bool S3>
 __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
-    extern __shared__ __attribute__((aligned(16))) Scn s_scn[];
+    using S = std::conditional_t<LDS, ScnF, ScnR>;
     __shared__ __attribute__((aligned(16))) K1Shared sh;
-    k1_group<LDS, LTAB, false, S3>(a, s_scn, sh, blockIdx.x);
+    k1_group<LDS, LTAB, false, S3, S>(a, reinterpret_cast<S*>(d2d_dyn_lds), sh, blockIdx.x);
 }
 // grouped slot layout: a pure group stages its scenario and probe table in LDS; a group that
 // straddles two scenarios (at most n_scn - 1 of them: the layout has no padding between scenarios)
@@ -845,24 +856,25 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {
 // through L1/L2; a group of three or more scenarios reads everything through L1/L2
 template <bool S3>
 __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_grouped_kernel(StepArgs a) {
-    extern __shared__ __attribute__((aligned(16))) Scn s_scn[];
+    ScnF* s_scn = reinterpret_cast<ScnF*>(d2d_dyn_lds);  // (a grouped map's tables are ScnF)
     __shared__ __attribute__((aligned(16))) K1Shared sh;
-    static_assert(2 * sizeof(Scn) <= sizeof(Scn) + sizeof(BtHot), "two staged scenarios");
+    static_assert(2 * sizeof(ScnF) <= sizeof(ScnF) + sizeof(BtHot), "two staged scenarios");
     const int wg = xcd_group(blockIdx.x, gridDim.x);
     const int ws = a.wg_scn[wg];
     if (a.brt && ws >= 0)
-        k1_group<true, true, true, S3>(a, s_scn, sh, wg);
+        k1_group<true, true, true, S3, ScnF>(a, s_scn, sh, wg);
     else if (ws <= -2)
-        k1_group<true, false, true, S3>(a, s_scn, sh, wg);
+        k1_group<true, false, true, S3, ScnF>(a, s_scn, sh, wg);
     else
-        k1_group<false, false, true, S3>(a, s_scn, sh, wg);
+        k1_group<false, false, true, S3, ScnF>(a, s_scn, sh, wg);
 }
 
 // ------------------------------------------------------------------------------------------ K2
-template <bool LDS>
+// LDS: stage every scenario; RM: the handle's layout (ScnR / ScnF)
+template <bool LDS, bool RM>
 __global__ __launch_bounds__(BLOCK) void d2d_reset_kernel(StepArgs a) {
-    extern __shared__ __attribute__((aligned(16))) Scn s_scn[];
-    const Scn* scns = stage_scenarios<LDS, BLOCK>(a, s_scn);
+    using S = std::conditional_t<RM, ScnR, ScnF>;
+    const S* scns = stage_scenarios<LDS, BLOCK>(a, reinterpret_cast<S*>(d2d_dyn_lds));
     __syncthreads();
     const int i = blockIdx.x * BLOCK + threadIdx.x;  // slot
     if (i >= a.ns) return;
@@ -875,7 +887,7 @@ __global__ __launch_bounds__(BLOCK) void d2d_reset_kernel(StepArgs a) {
         si = next_scenario(a, ie, (uint32_t)fld(a.ist, D2D_I_EPISODE, n, i));
         a.env_scn[ie] = si;
     }
-    const Scn& s = scns[si];
+    const S& s = scns[si];
     double sp[7];
     spawn_state(a, s, ie, (uint32_t)fld(a.ist, D2D_I_EPISODE, n, i), sp);
     const double th = sp[2];
@@ -916,7 +928,8 @@ __global__ __launch_bounds__(BLOCK) void d2d_permute_kernel(const T* src, int ss
 // alone on a mostly idle GPU, so its duration is one env's latency chain): wave 0 the spawn-state
 // sensor part, waves 1-3 one third each of the golden-march re-check, then wave 1 the Brent
 // continuation and the path part.  Same operations as the one-lane-per-env path.
-__device__ __forceinline__ void fill_split(const StepArgs& a, const Scn* scns, const int* list, int total) {
+template <class SC>
+__device__ __forceinline__ void fill_split(const StepArgs& a, const SC* scns, const int* list, int total) {
     __shared__ int devp[3][64];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int n = a.ns;
@@ -928,7 +941,7 @@ __device__ __forceinline__ void fill_split(const StepArgs& a, const Scn* scns, c
         const size_t ce = rc_entry(a, i, (uint32_t)ep);
         const int ie = a.lane_env ? a.lane_env[i] : i;
         const int si = next_scenario(a, ie, (uint32_t)ep);
-        const Scn& S = scns[si];
+        const SC& S = scns[si];
         const BrTab* T = brtab(a, si);
         double sp[7];
         spawn_state(a, S, ie, (uint32_t)ep, sp);
@@ -997,13 +1010,12 @@ __device__ __forceinline__ void fill_split(const StepArgs& a, const Scn* scns, c
 // since the last fill need it (~1/5 of them at fill period 16): each workgroup compacts its
 // envs that do into the leading lanes (ballot + popcount), so the long search runs in as few
 // waves as possible instead of one wave per 64 envs with a few active lanes.
-template <bool LDS>
+template <bool LDS, class S>
 __device__ __forceinline__ void fill_work(const StepArgs& a) {
-    extern __shared__ __attribute__((aligned(16))) Scn s_scn[];
     __shared__ int list[BLOCK];
     __shared__ int cnt[BLOCK / 64];
     FSTAMP(0);
-    const Scn* scns = stage_scenarios<LDS, BLOCK>(a, s_scn);
+    const S* scns = stage_scenarios<LDS, BLOCK>(a, reinterpret_cast<S*>(d2d_dyn_lds));
     const int n = a.ns;
     // work items: (slot, which) -- the entry for the env's current episode counter (which = 0) and
     // for the next one (which = 1); thread t takes slot t % FILL_SPB, which t / FILL_SPB
@@ -1047,7 +1059,7 @@ __device__ __forceinline__ void fill_work(const StepArgs& a) {
 // CU, one round).  K4 (1 024 workgroups at 65 536 envs) otherwise ran 3 per CU and left the CUs'
 // wave-placement rotation uneven, and the next K1 then put two path waves of one CU on one SIMD on
 // a few CUs (+7 us on that step, tools/ubench_after_stamps.py).
-template <bool LDS>
+template <bool LDS, bool RM>
 __global__ __launch_bounds__(BLOCK, 4) void d2d_fill_kernel(StepArgs a) {
     const bool ticked = !a.fill_force && a.fill_every > 1;
     bool run = true;
@@ -1058,7 +1070,7 @@ __global__ __launch_bounds__(BLOCK, 4) void d2d_fill_kernel(StepArgs a) {
         if (blockIdx.x == 0 && threadIdx.x == 0)
             __hip_atomic_store(&a.fill_ctl[1], tick + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    if (run) fill_work<LDS>(a);
+    if (run) fill_work<LDS, std::conditional_t<RM, ScnR, ScnF>>(a);
 }
 
 // ------------------------------------------------------------------------ fresh curriculum (K5)
@@ -1085,7 +1097,7 @@ struct FreshArgs {
     uint64_t seed;
     uint32_t env_id_base;
     d2d_scn* abi;            // [2 n] ABI records (read back for the oracle)
-    Scn* scn;                // [2 n]
+    ScnR* scn;               // [2 n] (the fresh curriculum's tables are ScnR)
     int32_t* tag;            // [2 n] episode key of each slot (-1: empty)
     int64_t* gclk;           // [2 n] clock at generation
     const int64_t* clock;    // the step clock (K1 advances it)
@@ -1147,7 +1159,7 @@ __global__ __launch_bounds__(64) void d2d_fresh_gen_kernel(FreshArgs f) {
         // the device table and the ABI record, 8-byte words across the wave
         const double* src = reinterpret_cast<const double*>(&G.s);
         double* dst = reinterpret_cast<double*>(f.scn + slot);
-        for (int k = lane; k < (int)(sizeof(Scn) / 8); k += 64) dst[k] = src[k];
+        for (int k = lane; k < (int)(sizeof(ScnR) / 8); k += 64) dst[k] = src[k];
         static_assert(sizeof(d2d_scn) % 8 == 0, "d2d_scn size");
         const double* sa = reinterpret_cast<const double*>(&G.a);
         double* da = reinterpret_cast<double*>(f.abi + slot);
@@ -1163,7 +1175,8 @@ __global__ __launch_bounds__(64) void d2d_fresh_gen_kernel(FreshArgs f) {
 
 // ------------------------------------------------------------------------- golden-march tables
 // one thread per (scenario, kind): the forced runs of brtab_build (d2d_device.h)
-__global__ __launch_bounds__(64) void d2d_brtab_kernel(const Scn* scn, int n_scn, BrTab* out) {
+template <class S>
+__global__ __launch_bounds__(64) void d2d_brtab_kernel(const S* scn, int n_scn, BrTab* out) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= 2 * n_scn) return;
     brtab_build(scn[t >> 1], t & 1, out[t >> 1]);

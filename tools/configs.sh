@@ -24,3 +24,4 @@ run cfg4_mixed_65536 --scenario mixed
 run cfg2_free_65536 --scenario corridor_free
 run cfg2_corridor_65536_eager --scenario corridor --eager
 run cfg2_corridor_65536_info --scenario corridor --info
+run fresh_curriculum_65536 --scenario curriculum
