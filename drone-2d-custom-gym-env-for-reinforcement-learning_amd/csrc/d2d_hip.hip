@@ -111,6 +111,7 @@ StepArgs make_args(const d2d_t* h) {
     if (D2D_K1_QUEUE && h->cfg.scn_pool == 2 && h->fresh_q) {
         a.fq = h->fresh_q;
         a.fqc = h->fresh_q + 2 * (size_t)h->n;
+        a.fq_cap = 2 * h->n;
     }
     return a;
 }
@@ -148,8 +149,9 @@ hipError_t fresh_regen(d2d_t* h, hipStream_t stream, bool restore = false, bool 
     hipError_t e = hipGetLastError();
     // the queue length back to 0 for the next K1 (a last-workgroup ticket instead costs ~2 048
     // same-address atomics: +14 us per step)
-    if (e == hipSuccess) e = hipMemsetAsync(f.qcount, 0, sizeof(int32_t), stream);
-    return e;
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(d2d_fresh_clear_kernel, dim3(1), dim3(64), 0, stream, f.qcount);
+    return hipGetLastError();
 }
 bool fresh_mode(const d2d_t* h) { return h->cfg.scn_pool == 2; }
 

@@ -103,8 +103,9 @@ struct StepArgs {
     int64_t* clock;           // [1]
     // ... and K5's queue: K1 appends the slot of the episode after next of every env it resets
     // (D2D_K1_QUEUE; null: K5a scans for them)
-    int32_t* fq;              // [2 n] slots
+    int32_t* fq;              // [fq_cap] slots
     int32_t* fqc;             // [0]: queue length
+    int fq_cap;               // 2 n
 };
 
 // the scenario table in the layout the launch was instantiated for (ScnF: the handle stages its
@@ -727,7 +728,8 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const SC* scns, const
             fld(a.ist, D2D_I_EPISODE, n, i) = (int32_t)(ep + 1u);
             if (a.cfg.scn_pool && a.env_scn) a.env_scn[ie] = nscn;
         }
-        if (D2D_K1_QUEUE && a.fq) {
+        if (D2D_K1_QUEUE && !LDS && a.fq) {  // (fresh mode reads its tables from global memory: the LDS
+                                             // instantiations carry no queue code, +0.9 us at 4 096 envs)
             // fresh curriculum: the slot the finished episode ran on now takes the episode after
             // next (key ep + 2 - 1 = the new counter), generated by K5 after this launch
             const bool need = valid && done && auto_reset;
@@ -737,7 +739,8 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const SC* scns, const
                 int base = 0;
                 if (lane == first) base = atomicAdd(a.fqc, __popcll(m));
                 base = __shfl(base, first);
-                if (need) a.fq[base + __popcll(m & ((1ull << lane) - 1ull))] = fresh_slot(ie, sh.ep[lane] + 1u);
+                const int pos = base + __popcll(m & ((1ull << lane) - 1ull));
+                if (need && pos < a.fq_cap) a.fq[pos] = fresh_slot(ie, sh.ep[lane] + 1u);
             }
         }
         STAMP(4);
@@ -1127,7 +1130,8 @@ __global__ __launch_bounds__(256) void d2d_fresh_scan_kernel(FreshArgs f) {
     int base = 0;
     if (lane == first) base = atomicAdd(f.qcount, __popcll(m));
     base = __shfl(base, first);
-    if (need) f.queue[base + __popcll(m & ((1ull << lane) - 1ull))] = slot;
+    const int pos = base + __popcll(m & ((1ull << lane) - 1ull));
+    if (need && pos < 2 * f.n) f.queue[pos] = slot;
 }
 // K5b: one wave per queued slot generates the scenario in LDS (d2d_curriculum.h) and writes the device
 // table and the ABI record.  (No golden-march tables in fresh mode: built per scenario they cost K5b
@@ -1135,7 +1139,8 @@ __global__ __launch_bounds__(256) void d2d_fresh_scan_kernel(FreshArgs f) {
 __global__ __launch_bounds__(64) void d2d_fresh_gen_kernel(FreshArgs f) {
     __shared__ __attribute__((aligned(16))) GenLds G;
     const int lane = threadIdx.x;
-    const int count = __hip_atomic_load(f.qcount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // (at most 2 n slots exist: a count beyond that would mean a lost clear; never read past the queue)
+    const int count = min(__hip_atomic_load(f.qcount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), 2 * f.n);
     for (int it = blockIdx.x; it < count; it += gridDim.x) {
         const int slot = f.queue[it];
         const int i = slot >> 1;
@@ -1171,6 +1176,11 @@ __global__ __launch_bounds__(64) void d2d_fresh_gen_kernel(FreshArgs f) {
         }
         __syncthreads();  // G is reused by the next item
     }
+}
+
+// the queue length back to 0 after K5b (a kernel node: ordered like every other launch of a graph)
+__global__ __launch_bounds__(64) void d2d_fresh_clear_kernel(int32_t* qcount) {
+    if (threadIdx.x == 0) qcount[0] = 0;
 }
 
 // ------------------------------------------------------------------------- golden-march tables
