@@ -61,6 +61,9 @@ def parse():
                         "'curriculum' (the fresh training curriculum: a new device-generated scenario per episode)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget (s)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--clock-warmup-ms", type=float, default=100.0,
+                   help="device clock warm-up before the warmup steps: the step kernels on a separate "
+                        "throwaway batch (the measured envs are untouched); 0 disables")
     p.add_argument("--info", action="store_true",
                    help="also write the per-env info rows (f32 [N, 12], what the SB3 adapter reads): +48 B/env-step")
     p.add_argument("--eager", action="store_true",
@@ -272,6 +275,24 @@ def main():
         torch.cuda.synchronize()
         _upload_graphs([g for g in (graph, tail) if g is not None], stream)
 
+    # Device clock warm-up (not part of the measured run: the measured envs are untouched).  An idle
+    # MI355X starts ~10-13 % below its sustained clock and ramps over tens of ms (GRBM_GUI_ACTIVE per
+    # ns of the first vs the later step launches, profiles/r04/final1/pmc_clk.csv), which a 20-step
+    # run would measure instead of the kernel: 31.4 vs 29.0 us per step (profiles/r04/clock/).  So
+    # the same step kernels first run for --clock-warmup-ms on a separate, throwaway batch of this
+    # rank's size; fp64 GEMMs instead do not raise the clock (31.4 us).
+    if args.clock_warmup_ms > 0:
+        spin = shard.make_shard_venv(n * world, rank, world, device=dev, seed=777, with_info=args.info, **kwargs)
+        spin.reset()
+        torch.cuda.synchronize()
+        t_w = time.perf_counter()
+        k = 0
+        while (time.perf_counter() - t_w) * 1e3 < args.clock_warmup_ms:
+            for _ in range(16):
+                spin.step(bank[k % ACTION_BANK])
+                k += 1
+            torch.cuda.synchronize()
+        spin.close()
     for k in range(args.warmup):
         venv.step(bank[k % ACTION_BANK])
     venv.episode_stats(clear=True)
@@ -343,6 +364,7 @@ def main():
             "n_gpus": world,
             "steps": n_timed,
             "warmup": args.warmup,
+            "clock_warmup_ms": args.clock_warmup_ms,
             "ms_per_step": wall * 1e3 / n_timed,
             "higher_is_better": True,
             "scaling": "weak",
