@@ -32,6 +32,32 @@
 // the product is always built with 0): 1 skip Brent, 2 skip sensing, 4 skip joint iterations,
 // 8 skip collision test, 16 skip the Brent continuation after the golden-march tables, 128 the fresh
 // curriculum generator skips the obstacles.
+#ifndef D2D_RM_CARRY_KA
+#define D2D_RM_CARRY_KA 1  // A/B: brent_step carries ka in the state for global-memory tables (0: reload)
+#endif
+// D2D_BSTAMP (diagnostic builds only, tools/bstamps.py): s_memtime stamps inside the golden-march
+// continuation's Brent steps, per path wave -- [workgroup][step < 64][8] in d2d_bst: entry, candidate
+// computed, interval found, probe evaluated, state updated, the step's B.num, whether the wave took
+// the knot scan, the active lanes.
+#ifdef D2D_BSTAMP
+#define BST_N (1024 * 64 * 8)
+__device__ uint64_t d2d_bst[BST_N];
+#define BST_ARG , uint64_t* bst = nullptr
+// (the stamp waits for `dep`, and volatile asm keeps the stamps in program order)
+#define BST(k, dep)                                                                                      \
+    do {                                                                                                 \
+        if (bst) {                                                                                       \
+            uint64_t bst_v;                                                                              \
+            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(bst_v) : "v"(dep));            \
+            bst_t[k] = bst_v;                                                                            \
+        }                                                                                                \
+    } while (0)
+#else
+#define BST_ARG
+#define BST(k, dep) \
+    do {       \
+    } while (0)
+#endif
 #ifndef D2D_ABLATE
 #define D2D_ABLATE 0
 #endif
@@ -385,12 +411,17 @@ __device__ __forceinline__ bool brent_active(const Brent& B) {
     return (fabs(B.xf - xm) > (tol2 - 0.5 * (B.b - B.a))) & (B.num < 500);
 }
 template <class S>
-__device__ __forceinline__ void brent_step(const S& s, const PathK& K, double px, double py, Brent& B) {
+__device__ __forceinline__ void brent_step(const S& s, const PathK& K, double px, double py, Brent& B BST_ARG) {
+#ifdef D2D_BSTAMP
+    uint64_t bst_t[5];
+#endif
+    BST(0, B.xf);
     const double a = B.a, b = B.b, xf = B.xf, fx = B.fx, nfc = B.nfc, fulc = B.fulc;
-    // the upper knot of a's interval, for the one-compare interval test.  (Carrying it in the state,
-    // or prefetching a's whole record before the candidate is known, measured no faster -- also with
-    // the scenarios in global memory, round 4: 92.4 vs 93.0 us per fresh-curriculum step.)
-    const double ka = SREC(s, REC_U1, B.ia);
+    // the upper knot of a's interval, for the one-compare interval test: re-read from a staged (LDS)
+    // table; carried in the state (B.ka, B.kxf, from the records the probes already read) when the
+    // table is read per lane from global memory (ScnR), where that load sat on every step's chain.
+    // (Prefetching a's whole record before the candidate is known, or xf's, measured no faster.)
+    const double ka = (S::RM && D2D_RM_CARRY_KA) ? B.ka : SREC(s, REC_U1, B.ia);
     const double xm = 0.5 * (a + b);
     const double tol1 = BR_SQRT_EPS * fabs(xf) + BR_XATOL3;
     const double tol2 = 2.0 * tol1;
@@ -426,6 +457,7 @@ __device__ __forceinline__ void brent_step(const S& s, const PathK& K, double px
     // (rat is never -0: e_g = a - xf or b - xf is +0 at worst, the parabolic step is p + 0.0 over
     // |q| or tol1 times a nonzero sign, so copysign gives the same -mx / +mx)
     const double x = xf + copysign(mx, rat);
+    BST(1, x);
     // knot interval of x: one compare once the bracket spans <= 2 intervals (wave-uniform choice)
     const bool fast = (x >= a) & (x <= b) & (B.ib <= B.ia + 1);
     int ix;
@@ -438,8 +470,10 @@ __device__ __forceinline__ void brent_step(const S& s, const PathK& K, double px
         asm volatile("" : "+v"(sp));
         ix = u_index(*sp, x);
     }
+    BST(2, ix);
     double kx;
     const double fu = path_dist_n(s, K, x, ix, px, py, kx);
+    BST(3, fu);
     B.num += 1;
     const bool le = fu <= fx;
     const bool c1 = !le & ((fu <= B.fnfc) | (nfc == xf));
@@ -455,6 +489,11 @@ __device__ __forceinline__ void brent_step(const S& s, const PathK& K, double px
     B.ia = to_a ? ti : B.ia;
     B.ib = to_a ? B.ib : ti;
     B.ixf = le ? ix : B.ixf;
+    if constexpr (S::RM && D2D_RM_CARRY_KA) {  // (the same bookkeeping brtab_build does for its snapshots)
+        const double tk = le ? B.kxf : kx;
+        B.ka = to_a ? tk : B.ka;
+        B.kxf = le ? kx : B.kxf;
+    }
     const double nfulc = (le | c1) ? nfc : (c2 ? x : fulc);
     const double nffulc = (le | c1) ? B.fnfc : (c2 ? fu : B.ffulc);
     const double nnfc = le ? xf : (c1 ? x : nfc);
@@ -465,6 +504,16 @@ __device__ __forceinline__ void brent_step(const S& s, const PathK& K, double px
     B.fnfc = nfnfc;
     B.xf = le ? x : xf;
     B.fx = le ? fu : fx;
+#ifdef D2D_BSTAMP
+    BST(4, B.fx);
+    const uint64_t act = __ballot(1);
+    if (bst && (int)(threadIdx.x & 63) == __ffsll((unsigned long long)act) - 1) {
+        for (int k = 0; k < 5; ++k) bst[k] = bst_t[k];
+        bst[5] = (uint64_t)B.num;
+        bst[6] = (uint64_t)(__ballot(!fast) != 0ull);
+        bst[7] = (uint64_t)__popcll(act);
+    }
+#endif
 }
 // (iu: the knot interval of the result, u_index(s, result), tracked by the search)
 template <class S>
@@ -722,7 +771,17 @@ __device__ __forceinline__ double bt_finish(const SC& s, const BrTab& T, const B
         B.ffulc = bt_dist<LT>(hot, kind, S.j_fulc, px, py);
         B.fnfc = bt_dist<LT>(hot, kind, S.j_nfc, px, py);
         B.fx = bt_dist<LT>(hot, kind, S.j_xf, px, py);
+#ifdef D2D_BSTAMP
+        int it = 0;
+        while (brent_active(B)) {
+            uint64_t* bst = nullptr;
+            if ((threadIdx.x >> 6) == 2 && blockIdx.x < 1024 && it < 64) bst = d2d_bst + ((size_t)blockIdx.x * 64 + it) * 8;
+            brent_step(s, K, px, py, B, bst);
+            ++it;
+        }
+#else
         while (!(D2D_ABLATE & 16) && brent_active(B)) brent_step(s, K, px, py, B);
+#endif
     }
     iu = B.ixf;
     return B.xf;

@@ -70,7 +70,8 @@ struct d2d_handle {
     d2d_curriculum cur{};        // fresh mode: generator parameters
     int32_t* scn_tag = nullptr;  // fresh mode: [2 n] episode key of each slot
     int64_t* gclk = nullptr;     // fresh mode: [2 n] clock at generation
-    int32_t* fresh_q = nullptr;  // fresh mode: [2 n + 2] K5's queue of slots to generate, its length (+1 spare)
+    int32_t* fresh_q = nullptr;  // fresh mode: [fresh_ring + FR_WORDS] K5's ring of slots to generate + its words
+    size_t fresh_ring = 0;       // ring size: the power of two >= 2 n
     int64_t* clock = nullptr;    // [1] the step clock (K1 advances it)
     uint64_t fresh_seed = 0;
     bool fresh_seeded = false;
@@ -110,8 +111,8 @@ StepArgs make_args(const d2d_t* h) {
     a.clock = h->clock;
     if (D2D_K1_QUEUE && h->cfg.scn_pool == 2 && h->fresh_q) {
         a.fq = h->fresh_q;
-        a.fqc = h->fresh_q + 2 * (size_t)h->n;
-        a.fq_cap = 2 * h->n;
+        a.fqc = reinterpret_cast<uint32_t*>(h->fresh_q + h->fresh_ring);
+        a.fq_mask = (uint32_t)h->fresh_ring - 1u;
     }
     return a;
 }
@@ -136,7 +137,9 @@ hipError_t fresh_regen(d2d_t* h, hipStream_t stream, bool restore = false, bool 
     f.gclk = h->gclk;
     f.clock = h->clock;
     f.queue = h->fresh_q;
-    f.qcount = h->fresh_q + 2 * (size_t)h->n;
+    f.ring = reinterpret_cast<uint32_t*>(h->fresh_q + h->fresh_ring);
+    f.mask = (uint32_t)h->fresh_ring - 1u;
+    f.scan = queued ? 0 : 1;
     f.restore = restore ? 1 : 0;
 #ifdef D2D_GEN_STAMPS
     f.stamps = h->stamps;
@@ -147,13 +150,18 @@ hipError_t fresh_regen(d2d_t* h, hipStream_t stream, bool restore = false, bool 
     // of a step all run at once); a reset queues every env (the grid's workgroups then take several)
     hipLaunchKernelGGL(d2d_fresh_gen_kernel, dim3(std::min(items, D2D_GEN_GRID)), dim3(64), 0, stream, f);
     hipError_t e = hipGetLastError();
-    // the queue length back to 0 for the next K1 (a last-workgroup ticket instead costs ~2 048
-    // same-address atomics: +14 us per step)
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(d2d_fresh_clear_kernel, dim3(1), dim3(64), 0, stream, f.qcount);
+    // after a K1, K5b itself leaves the next tail (FreshRing: no launch; the round-4 clear kernel
+    // after every K5b cost 5.5 us per step); after a scan, both tails to the head
+    if (e != hipSuccess || queued) return e;
+    hipLaunchKernelGGL(d2d_fresh_tail_kernel, dim3(1), dim3(64), 0, stream, f.ring);
     return hipGetLastError();
 }
 bool fresh_mode(const d2d_t* h) { return h->cfg.scn_pool == 2; }
+size_t ring_size(size_t slots) {  // FreshRing: a power of two holding every slot
+    size_t r = 64;
+    while (r < slots) r <<= 1;
+    return r;
+}
 
 // The scenario table's layout (d2d_device.h ScnF / ScnR): ScnR exactly when K1 will read it from
 // global memory -- the fresh curriculum, and tables too big to stage (pools) unless the map is grouped
@@ -491,6 +499,18 @@ int32_t d2d_debug_stamps(d2d_t* h, uint64_t* buf) {
     if (!h) return fail(D2D_E_ARG, "d2d_debug_stamps: null handle");
     h->stamps = buf;
     return D2D_OK;
+}
+#endif
+#ifdef D2D_BSTAMP
+// diagnostic builds only: the Brent-step stamps (d2d_device.h, D2D_BSTAMP): clear = 1 zeroes them,
+// else copies [1024][64][8] u64 into out
+int32_t d2d_debug_bstamps(uint64_t* out, int32_t clear) {
+    void* p = nullptr;
+    hipError_t e = hipGetSymbolAddress(&p, HIP_SYMBOL(d2d_bst));
+    if (e == hipSuccess) e = clear ? hipMemset(p, 0, sizeof(uint64_t) * BST_N)
+                                   : hipMemcpy(out, p, sizeof(uint64_t) * BST_N, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    return e == hipSuccess ? D2D_OK : hip_fail(e, "d2d_debug_bstamps");
 }
 #endif
 
@@ -950,14 +970,15 @@ int32_t d2d_set_curriculum(d2d_t* h, const d2d_curriculum* c) {
         h->scn_tag = nullptr;
         h->gclk = nullptr;
         h->fresh_q = nullptr;
+        h->fresh_ring = ring_size(S);
         h->n_scn = 0;
         h->rm = true;  // (the fresh curriculum's tables are read per lane from global memory)
         if ((e = hipMalloc(&h->scn, sizeof(d2d::ScnR) * S)) != hipSuccess ||
             (e = hipMalloc(&h->abi, sizeof(d2d_scn) * S)) != hipSuccess ||
             (e = hipMalloc(&h->scn_tag, sizeof(int32_t) * S)) != hipSuccess ||
             (e = hipMalloc(&h->gclk, sizeof(int64_t) * S)) != hipSuccess ||
-            (e = hipMalloc(&h->fresh_q, sizeof(int32_t) * (S + 2))) != hipSuccess ||
-            (e = hipMemset(h->fresh_q, 0, sizeof(int32_t) * (S + 2))) != hipSuccess ||
+            (e = hipMalloc(&h->fresh_q, sizeof(int32_t) * (ring_size(S) + FR_WORDS))) != hipSuccess ||
+            (e = hipMemset(h->fresh_q, 0, sizeof(int32_t) * (ring_size(S) + FR_WORDS))) != hipSuccess ||
             (e = hipMemset(h->scn, 0, sizeof(d2d::ScnR) * S)) != hipSuccess ||
             (e = hipMemset(h->abi, 0, sizeof(d2d_scn) * S)) != hipSuccess ||
             (e = hipMemset(h->gclk, 0, sizeof(int64_t) * S)) != hipSuccess)
@@ -967,6 +988,7 @@ int32_t d2d_set_curriculum(d2d_t* h, const d2d_curriculum* c) {
     // taken on THIS curriculum, not those since the handle was created
     if ((e = hipMemset(h->scn_tag, 0xFF, sizeof(int32_t) * S)) != hipSuccess ||
         (e = hipMemset(h->clock, 0, sizeof(int64_t))) != hipSuccess ||
+        (e = hipMemset(h->fresh_q + h->fresh_ring, 0, sizeof(int32_t) * FR_WORDS)) != hipSuccess ||  // (FreshRing)
         (e = hipDeviceSynchronize()) != hipSuccess)
         return hip_fail(e, "d2d_set_curriculum: slots");
     h->cur = *c;

@@ -103,9 +103,9 @@ struct StepArgs {
     int64_t* clock;           // [1]
     // ... and K5's queue: K1 appends the slot of the episode after next of every env it resets
     // (D2D_K1_QUEUE; null: K5a scans for them)
-    int32_t* fq;              // [fq_cap] slots
-    int32_t* fqc;             // [0]: queue length
-    int fq_cap;               // 2 n
+    int32_t* fq;              // [fq_mask + 1] slots (a ring, see FreshRing)
+    uint32_t* fqc;            // FreshRing words ([FR_HEAD]: appends so far)
+    uint32_t fq_mask;         // ring size - 1 (a power of two >= 2 n)
 };
 
 // the scenario table in the layout the launch was instantiated for (ScnF: the handle stages its
@@ -278,6 +278,13 @@ __device__ __forceinline__ int pool_scenario(const StepArgs& a, int j, uint32_t 
 // fresh curriculum: env j's two scenario slots alternate by episode key (d2d_fresh_kernel writes
 // the slot of key ep -- the episode the next reset starts -- one step ahead)
 __device__ __forceinline__ int fresh_slot(int j, uint32_t ep) { return 2 * j + (int)(ep & 1u); }
+// FreshRing: the fresh curriculum's slots to generate, in a ring nobody clears.  FR_HEAD counts the
+// appends (K1 at its auto-resets, or K5a), modulo 2^32; K5b drains [tail, head) and leaves the new
+// tail in the word of the next clock parity -- the one the K5b after the next K1 reads -- so no
+// workgroup of a launch writes a word another reads (the step clock, advanced by K1, is stable
+// during K5b).  After a scan (K5a) the tail is the later of the two words, and a one-thread launch
+// sets both to the head.
+enum { FR_HEAD = 0, FR_TAIL0 = 1, FR_TAIL1 = 2, FR_WORDS = 4 };
 __device__ __forceinline__ int next_scenario(const StepArgs& a, int j, uint32_t ep) {
     if (a.cfg.scn_pool == 2) return fresh_slot(j, ep);
     if (a.cfg.scn_pool) return pool_scenario(a, j, ep);
@@ -736,11 +743,11 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const SC* scns, const
             const uint64_t m = __ballot(need);
             if (m != 0ull) {
                 const int first = __ffsll((unsigned long long)m) - 1;
-                int base = 0;
-                if (lane == first) base = atomicAdd(a.fqc, __popcll(m));
+                uint32_t base = 0;
+                if (lane == first) base = atomicAdd(&a.fqc[FR_HEAD], (uint32_t)__popcll(m));
                 base = __shfl(base, first);
-                const int pos = base + __popcll(m & ((1ull << lane) - 1ull));
-                if (need && pos < a.fq_cap) a.fq[pos] = fresh_slot(ie, sh.ep[lane] + 1u);
+                const uint32_t pos = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+                if (need) a.fq[pos & a.fq_mask] = fresh_slot(ie, sh.ep[lane] + 1u);
             }
         }
         STAMP(4);
@@ -1104,8 +1111,10 @@ struct FreshArgs {
     int32_t* tag;            // [2 n] episode key of each slot (-1: empty)
     int64_t* gclk;           // [2 n] clock at generation
     const int64_t* clock;    // the step clock (K1 advances it)
-    int32_t* queue;          // [2 n] slots to generate (K5a -> K5b)
-    int32_t* qcount;         // [1] queue length (cleared by a memset after K5b)
+    int32_t* queue;          // [mask + 1] slots to generate (K1 / K5a -> K5b), a ring (FreshRing)
+    uint32_t* ring;          // FreshRing words: head, the two tails
+    uint32_t mask;           // ring size - 1
+    int scan;                // 1: K5a appended (the tail is the later of the two words)
     uint64_t* stamps;        // diagnostic builds only (D2D_GEN_STAMPS): [queue position][8]
     int restore;
 };
@@ -1127,22 +1136,32 @@ __global__ __launch_bounds__(256) void d2d_fresh_scan_kernel(FreshArgs f) {
     const uint64_t m = __ballot(need);
     if (m == 0ull) return;
     const int lane = threadIdx.x & 63, first = __ffsll((unsigned long long)m) - 1;
-    int base = 0;
-    if (lane == first) base = atomicAdd(f.qcount, __popcll(m));
+    uint32_t base = 0;
+    if (lane == first) base = atomicAdd(&f.ring[FR_HEAD], (uint32_t)__popcll(m));
     base = __shfl(base, first);
-    const int pos = base + __popcll(m & ((1ull << lane) - 1ull));
-    if (need && pos < 2 * f.n) f.queue[pos] = slot;
+    const uint32_t pos = base + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    if (need) f.queue[pos & f.mask] = slot;
 }
 // K5b: one wave per queued slot generates the scenario in LDS (d2d_curriculum.h) and writes the device
 // table and the ABI record.  (No golden-march tables in fresh mode: built per scenario they cost K5b
-// more than they save K1, DESIGN.md "Round 4".)  The host clears the queue length after the launch.
+// more than they save K1, DESIGN.md "Round 4".)  It drains the ring from the tail to the head
+// (FreshRing) and, after a K1, leaves the head as the next tail.
 __global__ __launch_bounds__(64) void d2d_fresh_gen_kernel(FreshArgs f) {
     __shared__ __attribute__((aligned(16))) GenLds G;
     const int lane = threadIdx.x;
-    // (at most 2 n slots exist: a count beyond that would mean a lost clear; never read past the queue)
-    const int count = min(__hip_atomic_load(f.qcount, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), 2 * f.n);
+    const uint32_t head = f.ring[FR_HEAD];  // (K1 / K5a have finished: stable)
+    uint32_t tail;
+    if (f.scan) {  // the later of the two tails (both are at or behind the head, modulo 2^32)
+        tail = head - min(head - f.ring[FR_TAIL0], head - f.ring[FR_TAIL1]);
+    } else {  // after K1: its clock parity picks the word; the other one is the next K5b's
+        const int64_t clk = *f.clock;
+        tail = f.ring[FR_TAIL0 + (int)(clk & 1)];
+        if (blockIdx.x == 0 && lane == 0) f.ring[FR_TAIL0 + (int)((clk + 1) & 1)] = head;
+    }
+    // (at most 2 n slots exist, and the ring holds them; never read more than the ring)
+    const int count = (int)min(head - tail, f.mask + 1u);
     for (int it = blockIdx.x; it < count; it += gridDim.x) {
-        const int slot = f.queue[it];
+        const int slot = f.queue[(tail + (uint32_t)it) & f.mask];
         const int i = slot >> 1;
         int key;
         int64_t clk;
@@ -1155,7 +1174,7 @@ __global__ __launch_bounds__(64) void d2d_fresh_gen_kernel(FreshArgs f) {
         }
         uint64_t* st = nullptr;
 #ifdef D2D_GEN_STAMPS
-        if (f.stamps) st = f.stamps + (size_t)it * 8;
+        if (f.stamps && it < 2 * f.n) st = f.stamps + (size_t)it * 8;
 #endif
         const double sim = f.cur.sim_num0 + (double)clk * f.cur.envs_total;
         const uint32_t gid = f.env_id_base + (uint32_t)i;
@@ -1178,9 +1197,10 @@ __global__ __launch_bounds__(64) void d2d_fresh_gen_kernel(FreshArgs f) {
     }
 }
 
-// the queue length back to 0 after K5b (a kernel node: ordered like every other launch of a graph)
-__global__ __launch_bounds__(64) void d2d_fresh_clear_kernel(int32_t* qcount) {
-    if (threadIdx.x == 0) qcount[0] = 0;
+// after a scan's K5b: both tails to the head (FreshRing; a kernel node, ordered like every other
+// launch of a graph)
+__global__ __launch_bounds__(64) void d2d_fresh_tail_kernel(uint32_t* ring) {
+    if (threadIdx.x == 0) ring[FR_TAIL0] = ring[FR_TAIL1] = ring[FR_HEAD];
 }
 
 // ------------------------------------------------------------------------- golden-march tables
