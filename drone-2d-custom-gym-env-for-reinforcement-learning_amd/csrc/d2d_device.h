@@ -32,6 +32,9 @@
 // the product is always built with 0): 1 skip Brent, 2 skip sensing, 4 skip joint iterations,
 // 8 skip collision test, 16 skip the Brent continuation after the golden-march tables, 128 the fresh
 // curriculum generator skips the obstacles.
+#ifndef D2D_KS_OFF
+#define D2D_KS_OFF 0  // A/B: the knot scan keeps the table's address space (opaque offset, not pointer)
+#endif
 #ifndef D2D_RM_CARRY_KA
 #define D2D_RM_CARRY_KA 1  // A/B: brent_step carries ka in the state for global-memory tables (0: reload)
 #endif
@@ -310,6 +313,16 @@ __device__ __forceinline__ int u_index(const S& s, double u) {
     const int nw1 = s.n_wps - 1;
     return (u != u) ? nw1 : min((int)c, nw1);
 }
+// the same with the knots read at an opaque offset z (= 0): keeps the table's address space (LDS
+// loads for a staged table) while stopping the compiler from keeping the knots in registers
+template <class S>
+__device__ __forceinline__ int u_index_at(const S& s, double u, int z) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 1; k < D2D_MAX_WPS; ++k) c += !(u <= SUS(s, k + z)) ? 1u : 0u;
+    const int nw1 = s.n_wps - 1;
+    return (u != u) ? nw1 : min((int)c, nw1);
+}
 // loop invariants of path_eval (hoisted out of the Brent loop)
 struct PathK {
     double us0, last_lo, L;
@@ -466,9 +479,15 @@ __device__ __forceinline__ void brent_step(const S& s, const PathK& K, double px
     } else {
         // the knot scan re-reads the knots each time (an opaque pointer stops the compiler from
         // keeping all 15 in registers across the loop: the fast path does not need them)
+#if D2D_KS_OFF
+        int z = 0;
+        asm volatile("" : "+v"(z));
+        ix = u_index_at(s, x, z);
+#else
         const S* sp = &s;
         asm volatile("" : "+v"(sp));
         ix = u_index(*sp, x);
+#endif
     }
     BST(2, ix);
     double kx;

@@ -15,3 +15,8 @@ tail -2 $O/ppo_fresh.jsonl | cut -c1-300
 timeout -k 10 200 python -u tools/bstamps.py run --scenario corridor_free --envs 4096 --out $O/bstamps_corridor_free_4096.json > $O/bstamps_4096.log 2>&1 || { echo STOP bst; exit 1; }
 timeout -k 10 200 python -u tools/bstamps.py run --scenario corridor --envs 65536 --out $O/bstamps_corridor_65536.json > $O/bstamps_65536.log 2>&1 || { echo STOP bst2; exit 1; }
 tail -1 $O/bstamps_4096.log; tail -1 $O/bstamps_65536.log
+# knot-scan address-space A/B (D2D_KS_OFF)
+timeout -k 10 300 python -u tools/variants.py run base ks --envs 65536 --rounds 3 > $O/var_ks_65536.log 2>&1 || { echo STOP var; exit 1; }
+timeout -k 10 200 python -u tools/variants.py run base ks --envs 4096 --scenario corridor_free --rounds 3 > $O/var_ks_4096.log 2>&1 || { echo STOP var2; exit 1; }
+grep -A3 '"base"\|"ks"' $O/var_ks_65536.log | grep min; grep -A3 '"base"\|"ks"' $O/var_ks_4096.log | grep min
+bash tools/gpu_fresh.sh ${TAG}ks tools/_abl/libd2d_var_ks.so || exit 1
