@@ -32,9 +32,6 @@
 // the product is always built with 0): 1 skip Brent, 2 skip sensing, 4 skip joint iterations,
 // 8 skip collision test, 16 skip the Brent continuation after the golden-march tables, 128 the fresh
 // curriculum generator skips the obstacles.
-#ifndef D2D_KS_OFF
-#define D2D_KS_OFF 0  // A/B: the knot scan keeps the table's address space (opaque offset, not pointer)
-#endif
 #ifndef D2D_RM_CARRY_KA
 #define D2D_RM_CARRY_KA 1  // A/B: brent_step carries ka in the state for global-memory tables (0: reload)
 #endif
@@ -477,17 +474,20 @@ __device__ __forceinline__ void brent_step(const S& s, const PathK& K, double px
     if (__ballot(!fast) == 0ull) {
         ix = min(B.ia + ((x <= ka) ? 0 : 1), K.nw - 1);
     } else {
-        // the knot scan re-reads the knots each time (an opaque pointer stops the compiler from
-        // keeping all 15 in registers across the loop: the fast path does not need them)
-#if D2D_KS_OFF
-        int z = 0;
-        asm volatile("" : "+v"(z));
-        ix = u_index_at(s, x, z);
-#else
-        const S* sp = &s;
-        asm volatile("" : "+v"(sp));
-        ix = u_index(*sp, x);
-#endif
+        // the knot scan re-reads the knots each time (an opaque pointer or offset stops the compiler
+        // from keeping all 15 in registers across the loop: the fast path does not need them).  With
+        // the table in global memory (ScnR) an opaque offset keeps global loads where the opaque
+        // pointer made flat ones (fresh curriculum K1 88.9 -> 85.4 us); for a staged (LDS) table the
+        // offset form measured 1.3 % slower at 4 096 envs (profiles/r04/ring/), so the flat loads stay.
+        if constexpr (S::RM) {
+            int z = 0;
+            asm volatile("" : "+v"(z));
+            ix = u_index_at(s, x, z);
+        } else {
+            const S* sp = &s;
+            asm volatile("" : "+v"(sp));
+            ix = u_index(*sp, x);
+        }
     }
     BST(2, ix);
     double kx;
