@@ -9,8 +9,10 @@ R=$(pwd)
 OUT=$R/gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
+SKIP=" ${SKIP:-} "  # names of steps to skip, e.g. SKIP="profile ppo_corridor"
 run() {  # run <name> <timeout-s> <cmd...>: allow 0/1 (test failures), stop on anything else
   local name=$1 lim=$2; shift 2
+  case "$SKIP" in *" $name "*) echo "=== $name skipped"; return 0;; esac
   echo "=== $name ($(date +%T))"
   timeout -k 10 "$lim" "$@" > "$OUT/$name.log" 2>&1
   local rc=$?
@@ -27,6 +29,6 @@ run configs 900 bash tools/configs.sh "$TAG"
 run profile 1100 bash tools/profile.sh "$TAG"
 run fresh 600 bash tools/gpu_fresh.sh "$TAG" drone-2d-custom-gym-env-for-reinforcement-learning_amd/_lib/libdrone2d_hip.so
 run ppo_corridor 600 python tools/train_ppo.py --updates 60
-cp gpurun_out/ppo.jsonl "$OUT/ppo_corridor_60.jsonl"
+case "$SKIP" in *" ppo_corridor "*) ;; *) cp gpurun_out/ppo.jsonl "$OUT/ppo_corridor_60.jsonl";; esac
 run ppo_fresh 600 python tools/train_ppo.py --curriculum --pool 0 --updates 100
 cp gpurun_out/ppo.jsonl "$OUT/ppo_fresh_100.jsonl"
