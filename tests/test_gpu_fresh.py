@@ -192,8 +192,9 @@ def test_masked_fresh_reset_keeps_seed(d2):
 def test_fresh_graph_replay_keeps_every_slot(d2):
     """The fresh curriculum inside a captured HIP graph with other kernels between the steps (as PPO's
     rollout graph has them): after every replay each env's running and next slots hold its current
-    and next episode's scenario (the slot queue K1 fills and K5 drains lost nothing), and a handle
-    restored from the recipes regenerates the same tables byte for byte."""
+    and next episode's scenario (the slot ring K1 fills and K5 drains lost nothing, also after its
+    indices wrapped: more than 2 n appends, FreshRing in d2d_kernels.h), and a handle restored from the
+    recipes regenerates the same tables byte for byte."""
     n = 4096
     venv = d2.Drone2dVecEnv(n, seed=3, **_kw(sim_num=1950000))  # stage 4 -> 5 during the replays
     venv.reset()
@@ -211,7 +212,7 @@ def test_fresh_graph_replay_keeps_every_slot(d2):
             _, rew, _, _, _ = venv.step(act)
             acc += rew.double().sum()
     dones = 0
-    for _ in range(6):
+    for _ in range(10):
         gr.replay()
         torch.cuda.synchronize()
         dones += int(venv.episode_stats()[1].item())
@@ -220,7 +221,9 @@ def test_fresh_graph_replay_keeps_every_slot(d2):
         slot = 2 * np.arange(n)
         np.testing.assert_array_equal(keys[slot + ((ep - 1) & 1)], ep - 1)
         np.testing.assert_array_equal(keys[slot + (ep & 1)], ep)
-    assert dones > n // 2  # thousands of auto-resets inside the replays (3 880 measured)
+    # thousands of auto-resets inside the replays (~650 per replay); the reset's scan appended n, so
+    # more than n resets have wrapped the ring of 2 n slots
+    assert dones > n + 256
     b = d2.Drone2dVecEnv(n, seed=1, **_kw(sim_num=1950000))
     b.load_state_dict(venv.state_dict())
     assert bytes(venv.scenario_table()) == bytes(b.scenario_table())
