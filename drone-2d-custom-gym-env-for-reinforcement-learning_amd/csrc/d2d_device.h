@@ -320,6 +320,16 @@ __device__ __forceinline__ int u_index_at(const S& s, double u, int z) {
     const int nw1 = s.n_wps - 1;
     return (u != u) ? nw1 : min((int)c, nw1);
 }
+// the same over a lane's knots staged in LDS, knot k at kn[64 k + lane] (conflict-free), read at an
+// opaque offset z (= 0) so the compiler keeps them in LDS
+__device__ __forceinline__ int u_index_kn(const double* kn, int nw, double u, int z) {
+    const int lane = (int)(threadIdx.x & 63) + z;
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 1; k < D2D_MAX_WPS; ++k) c += !(u <= kn[64 * k + lane]) ? 1u : 0u;
+    const int nw1 = nw - 1;
+    return (u != u) ? nw1 : min((int)c, nw1);
+}
 // loop invariants of path_eval (hoisted out of the Brent loop)
 struct PathK {
     double us0, last_lo, L;
@@ -420,8 +430,10 @@ __device__ __forceinline__ bool brent_active(const Brent& B) {
     const double tol2 = 2.0 * tol1;
     return (fabs(B.xf - xm) > (tol2 - 0.5 * (B.b - B.a))) & (B.num < 500);
 }
-template <class S>
-__device__ __forceinline__ void brent_step(const S& s, const PathK& K, double px, double py, Brent& B BST_ARG) {
+// KN: the knot scan reads the lane's knots staged in LDS at kn (global-memory tables, closest_u)
+template <bool KN = false, class S>
+__device__ __forceinline__ void brent_step(const S& s, const PathK& K, double px, double py, Brent& B,
+                                           const double* kn = nullptr BST_ARG) {
 #ifdef D2D_BSTAMP
     uint64_t bst_t[5];
 #endif
@@ -482,7 +494,8 @@ __device__ __forceinline__ void brent_step(const S& s, const PathK& K, double px
         if constexpr (S::RM) {
             int z = 0;
             asm volatile("" : "+v"(z));
-            ix = u_index_at(s, x, z);
+            if constexpr (KN) ix = u_index_kn(kn, K.nw, x, z);
+            else ix = u_index_at(s, x, z);
         } else {
             const S* sp = &s;
             asm volatile("" : "+v"(sp));
@@ -535,12 +548,29 @@ __device__ __forceinline__ void brent_step(const S& s, const PathK& K, double px
 #endif
 }
 // (iu: the knot interval of the result, u_index(s, result), tracked by the search)
-template <class S>
-__device__ __forceinline__ double closest_u(const S& s, double px, double py, int& iu) {
+// kn (global-memory tables only, K1's path wave): LDS for the lane's knots, which the knot scans
+// then read instead of global memory (16 x 64 doubles)
+template <bool KN = false, class S>
+__device__ __forceinline__ double closest_u(const S& s, double px, double py, int& iu, double* kn = nullptr) {
+    static_assert(!KN || S::RM, "staged knots: global-memory tables only");
     const PathK K = path_k(s);
+    if constexpr (KN) {
+#pragma unroll
+        for (int k = 0; k < D2D_MAX_WPS; ++k) kn[64 * k + (threadIdx.x & 63)] = SUS(s, k);
+    }
     Brent B;
     brent_init(s, K, px, py, B);
-    while (brent_active(B)) brent_step(s, K, px, py, B);
+#ifdef D2D_BSTAMP
+    int it = 0;
+    while (brent_active(B)) {
+        uint64_t* bst = nullptr;
+        if ((threadIdx.x >> 6) == 2 && blockIdx.x < 1024 && it < 64) bst = d2d_bst + ((size_t)blockIdx.x * 64 + it) * 8;
+        brent_step<KN>(s, K, px, py, B, kn, bst);
+        ++it;
+    }
+#else
+    while (brent_active(B)) brent_step<KN>(s, K, px, py, B, kn);
+#endif
     iu = B.ixf;
     return B.xf;
 }
@@ -795,7 +825,7 @@ __device__ __forceinline__ double bt_finish(const SC& s, const BrTab& T, const B
         while (brent_active(B)) {
             uint64_t* bst = nullptr;
             if ((threadIdx.x >> 6) == 2 && blockIdx.x < 1024 && it < 64) bst = d2d_bst + ((size_t)blockIdx.x * 64 + it) * 8;
-            brent_step(s, K, px, py, B, bst);
+            brent_step(s, K, px, py, B, nullptr, bst);
             ++it;
         }
 #else
@@ -1320,14 +1350,16 @@ __device__ __forceinline__ void path_obs_u(const d2d_cfg& cfg, const S& s, doubl
 }
 // T: the scenario's golden-march tables (null: plain search); hot: their probe table staged in LDS
 // (LT) or null (read from T in global memory)
-template <bool LT = false, class S>
+// KN: kn is LDS for the plain search's staged knots (closest_u; global-memory tables)
+template <bool LT = false, bool KN = false, class S>
 __device__ __forceinline__ void path_obs(const d2d_cfg& cfg, const S& s, const BrTab* T, double x, double y,
-                                         double al, uint32_t& flags, double o[8], const BtHot* hot = nullptr) {
+                                         double al, uint32_t& flags, double o[8], const BtHot* hot = nullptr,
+                                         double* kn = nullptr) {
     int iu = -1;
     const double u = (D2D_ABLATE & 1) ? clipd(x - 100.0, -10.0, SUS(s, s.n_wps - 1))
                      : (T ? (LT ? closest_u_tab<true>(s, *T, hot, x, y, iu)
                                 : closest_u_tab<false>(s, *T, &T->hot, x, y, iu))
-                          : closest_u(s, x, y, iu));
+                          : closest_u<KN>(s, x, y, iu, kn));
     path_obs_u(cfg, s, x, y, al, u, flags, o, iu);
 }
 

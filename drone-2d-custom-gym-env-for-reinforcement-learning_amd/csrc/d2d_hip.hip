@@ -743,8 +743,8 @@ int32_t d2d_step(d2d_t* h, const float* act_dev, float* obs_dev, float* rew_dev,
             if (s3) launch(d2d_step_kernel<true, false, true>, grid, lds_scn);
             else launch(d2d_step_kernel<true, false, false>, grid, lds_scn);
         } else {
-            if (s3) launch(d2d_step_kernel<false, false, true>, grid, 0);
-            else launch(d2d_step_kernel<false, false, false>, grid, 0);
+            if (s3) launch(d2d_step_kernel<false, false, true>, grid, K1_KN_BYTES);
+            else launch(d2d_step_kernel<false, false, false>, grid, K1_KN_BYTES);
         }
     }
     e = hipGetLastError();

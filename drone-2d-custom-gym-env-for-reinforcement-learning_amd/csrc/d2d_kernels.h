@@ -358,6 +358,10 @@ __device__ __forceinline__ void k1_stage(const StepArgs& a, S* s_scn, int wg, co
     }
 }
 
+// the dynamic LDS of every kernel (scenarios [+ probe tables]; global-memory tables: the path wave's
+// staged knots, K1_KN_BYTES), sized at launch
+extern __shared__ __attribute__((aligned(16))) uint4 d2d_dyn_lds[];
+constexpr int K1_KN_BYTES = D2D_MAX_WPS * 64 * 8;
 // One env step for the 64 envs of group wg (slots [64 wg, 64 wg + 64)) by the calling wave in role `role` (0..3, wave-uniform); qt =
 // 64 role + lane, the thread's index among the group's 256.  scns / hots: the scenario and probe
 // tables indexed by global scenario id (LDS when staged: LDS / LTAB), s0 the group's scenario.
@@ -619,7 +623,9 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const SC* scns, const
                 const double u = bt_finish<LTAB>(S, *T, hot, L.kind, L.dev, F.px, F.py, iu);
                 path_obs_u(a.cfg, S, F.px, F.py, F.a, u, f, po, iu);
             } else {
-                path_obs<LTAB>(a.cfg, S, T, F.px, F.py, F.a, f, po, LTAB ? hots + sh.scn[lane] : nullptr);
+                // (global-memory tables: the plain search scans the lane's knots staged in LDS)
+                path_obs<LTAB, SC::RM>(a.cfg, S, T, F.px, F.py, F.a, f, po, LTAB ? hots + sh.scn[lane] : nullptr,
+                                       SC::RM ? reinterpret_cast<double*>(d2d_dyn_lds) : nullptr);
             }
             sh.pflags[lane] = f & D2D_FLAG_LA_LOCK;
         }
@@ -850,8 +856,6 @@ __device__ __forceinline__ void k1_group(const StepArgs& a, S* s_scn, K1Shared& 
     k1_body<LDS, LTAB, GRP, S3, S>(a, scns, hots, s0, sh, wg, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6),
                                    (int)threadIdx.x);
 }
-// the dynamic LDS of every kernel (scenarios [+ probe tables], sized at launch)
-extern __shared__ __attribute__((aligned(16))) uint4 d2d_dyn_lds[];
 // S3: the three-way table re-check (D2D_SPLIT3), chosen at launch
 // (LDS: the handle's tables are ScnF, staged; otherwise ScnR, read per lane from global memory)
 template <bool LDS, bool LTAB, bool S3>

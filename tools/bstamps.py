@@ -5,7 +5,8 @@
     python tools/bstamps.py run [--scenario S] [--envs N] [--out F] # GPU box
 
 The D2D_BSTAMP build (d2d_device.h) stamps s_memtime five times inside each continuation
-`brent_step` of every path wave (wave 2): entry, candidate computed (parabolic / golden arithmetic),
+`brent_step` of every path wave (wave 2; with `--scenario curriculum`, every step of the plain
+search, whose tables are read per lane from global memory): entry, candidate computed (parabolic / golden arithmetic),
 interval found (one compare, or the knot scan), probe evaluated (the interval's record from LDS +
 the cubic's value, distance), state updated (scipy's compares and selects; the compiler schedules
 them after the last stamp, so they are reported with the loop's own overhead).  Per phase the cycles
@@ -91,7 +92,10 @@ def run(scenario, n, warm, reps, out):
     import drone2d_amd as d2
     from drone2d_amd.config import ENV_TRAIN_CONFIG
 
-    venv = d2.Drone2dVecEnv(n, seed=3, with_info=False, native_lib=LIB, **dict(ENV_TRAIN_CONFIG, scenario=scenario))
+    kw = dict(ENV_TRAIN_CONFIG, scenario=scenario)
+    if scenario == "curriculum":  # the fresh curriculum: the plain search over global-memory tables
+        kw.update(mode="curriculum", sim_num=0)
+    venv = d2.Drone2dVecEnv(n, seed=3, with_info=False, native_lib=LIB, **kw)
     lib = venv._lib
     lib.d2d_debug_bstamps.argtypes = [C.c_void_p, C.c_int32]
     lib.d2d_debug_bstamps.restype = C.c_int32
