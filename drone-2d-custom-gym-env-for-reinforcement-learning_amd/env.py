@@ -206,7 +206,8 @@ class Drone2dVecEnv:
         """Regenerate the curriculum pool (explicit ``stage`` or the reference's ``sim_num``
         schedule), upload it and reset every env; returns the reset observations.  Fresh
         curriculum: the schedule restarts at ``sim_num`` (the device step clock is zeroed, so
-        sim_num = sim_num + steps taken from here x envs_total)."""
+        sim_num = sim_num + steps taken from here x envs_total); with neither ``stage`` nor
+        ``sim_num`` (e.g. ``seed=`` only) it continues from the progress the clock holds."""
         if not self.cfg.scn_pool:
             raise ValueError("set_curriculum needs an env created in curriculum mode (mode='curriculum')")
         if pool is not None and self.fresh:
@@ -217,6 +218,11 @@ class Drone2dVecEnv:
         elif sim_num is not None:
             self.kwargs["scenario"] = "curriculum"
             self.kwargs["sim_num"] = int(sim_num)
+        elif self.fresh and self.kwargs.get("scenario") == "curriculum":
+            # neither given: the schedule carries on where the device clock has it (the library
+            # zeroes the clock, so sim_num0 takes the progress: sim_num + clock x envs_total)
+            clock = self.fresh_recipes()[2]
+            self.kwargs["sim_num"] = int(self.kwargs.get("sim_num", 0)) + clock * self.envs_total
         self.kwargs["mode"] = "curriculum"
         if pool is not None and not self.fresh:
             self.kwargs["curriculum_pool"] = int(pool)
@@ -272,14 +278,16 @@ class Drone2dVecEnv:
     # ------------------------------------------------------------------ API
     def reset(self, seed: int | None = None, mask: torch.Tensor | None = None) -> torch.Tensor:
         """Reset all envs (or those with ``mask`` set); returns obs [N, 27] float32."""
-        if seed is not None:
-            self.seed_value = int(seed)
+        sv = int(seed) if seed is not None else self.seed_value
         b = self._bufs[self._k]
         m = None
         if mask is not None:
             m = mask.to(device=self.device, dtype=torch.uint8).contiguous()
-        self._check(self._lib.d2d_reset(self._h, self._ptr(m), C.c_uint64(self.seed_value & (2 ** 64 - 1)),
+        self._check(self._lib.d2d_reset(self._h, self._ptr(m), C.c_uint64(sv & (2 ** 64 - 1)),
                                   self._ptr(b["obs"]), self._stream()), "d2d_reset")
+        # only a reset the library accepted installs the seed (a refused masked fresh-curriculum
+        # reset with a new seed leaves the library on the old one, and so must state_dict())
+        self.seed_value = sv
         return b["obs"]
 
     def _prep_actions(self, actions) -> torch.Tensor:

@@ -168,6 +168,25 @@ def test_set_curriculum_restarts_schedule(d2):
     venv.close()
 
 
+def test_set_curriculum_seed_only_keeps_progress(d2):
+    """set_curriculum(seed=...) alone on a fresh env carries the schedule's progress (the
+    library zeroes its clock, the wrapper moves it into sim_num0): 690 000 + 50 x 1 024 = 741 200 is
+    stage 2 (the random spawn box), where restarting at 690 000 would be stage 1."""
+    n = 1024
+    venv = d2.Drone2dVecEnv(n, seed=5, **_kw(sim_num=690000))
+    venv.reset()
+    for _ in range(50):
+        venv.step(torch.rand(n, 2, device=venv.device) * 2 - 1)
+    venv.set_curriculum(seed=7)
+    assert venv.kwargs["sim_num"] == 690000 + 50 * n
+    keys, _, clock = venv.fresh_recipes()
+    assert clock == 0
+    tab = venv.scenario_table(0, 2 * n)
+    for s in np.flatnonzero(keys >= 0):
+        assert (tab[s].spawn_xmin, tab[s].spawn_xmax) == (100.0, 1200.0), s
+    venv.close()
+
+
 def test_masked_fresh_reset_keeps_seed(d2):
     """a masked fresh reset with a new seed is refused (the envs it leaves running would
     keep old-seed scenarios that no checkpoint recipe regenerates); with the same seed it works."""
@@ -180,7 +199,8 @@ def test_masked_fresh_reset_keeps_seed(d2):
     mask[::3] = True
     with pytest.raises(RuntimeError, match="masked reset"):
         venv.reset(seed=99, mask=mask)
-    venv.seed_value = 5
+    assert venv.seed_value == 5  # the refused seed is not installed: state_dict() saves 5
+    assert venv.state_dict()["seed"] == 5
     venv.reset(mask=mask)
     keys = venv.fresh_recipes()[0]
     ep = venv.get_state()[1][2].cpu().numpy()

@@ -309,7 +309,14 @@ def _oracle_run(scn, n, seed):
 def test_test_loop_hip_matches_oracle(d2, scn):
     """the reference's test loop (main.py:258-327) run by ``run_first_episodes``
     on the HIP batch and on the CPU oracle, same seed / scenario / env ids, the shipped agent 17_90
-    evaluated on the host for both (so both see one action stream): every record identical."""
+    evaluated on the host for both (so both see one action stream).  The contract is statistical,
+    not per record (the kernel's bearings, obs 9-18 / 23-26, are rotated unit vectors a few ulp
+    from the reference's atan2 / ssa / sincos, so an occasional f32 observation rounds one ulp
+    apart and that closed-loop episode drifts; DESIGN.md "Round 4" item 2).  ``_records_equal``
+    asserts: >= 98 % of episodes end at the same step with the same collision flag; success / fail
+    counts within max(2, 1 %); on the episodes that end alike, flight paths within 1 px on >= 97 %,
+    and |APE_hip - APE_oracle| <= that flight's own maximum deviation + 1e-3 px on >= 99 %; total
+    reward to rtol 1e-6 where the two flights are identical at every step."""
     from drone2d_amd import harness
     from drone2d_amd.config import ENV_TEST_CONFIG
 

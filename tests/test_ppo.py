@@ -173,28 +173,40 @@ def test_manual_step_hip_matches_autograd(d2, M):
 
 
 @pytest.mark.gpu
-def test_rollout_graph_matches_eager(d2):
+@pytest.mark.parametrize("scn", ["corridor", "fresh_curriculum"])
+def test_rollout_graph_matches_eager(d2, scn):
     """The captured rollout (policy + env step + GAE replayed as one HIP graph) fills the same
-    buffers as the eager loop, bit for bit, over three consecutive rollouts."""
+    buffers as the eager loop, bit for bit, over five consecutive rollouts (the first eager, the
+    second captured and replayed, then three more replays).  ``fresh_curriculum`` is the
+    configuration of profiles/r04/ppo/crash_fresh_graph_memset.err (an illegal address at the second
+    rollout-graph replay): the device scenario generator K5 and K1's FreshRing
+    appends inside PPO's rollout graph with the policy kernels between the steps; stage 4 -> 5 of
+    the schedule during the rollouts."""
     from drone2d_amd.ppo import PPO, PPOConfig
 
+    kw = _kw(scenario="corridor") if scn == "corridor" else _kw(mode="curriculum", scenario="curriculum",
+                                                                 sim_num=1990000)
     outs = []
     for graph in (False, True):
-        venv = d2.Drone2dVecEnv(2048, seed=4, with_info=True, **_kw(scenario="corridor"))
+        venv = d2.Drone2dVecEnv(2048, seed=4, with_info=True, **kw)
+        assert venv.fresh == (scn != "corridor")
         cfg = PPOConfig.gpu_defaults(n_steps=16, batch_size=4096)
         cfg.graph = graph
         algo = PPO(venv, cfg, seed=2)
         rec = []
-        for _ in range(3):
+        for _ in range(5):
             st = algo.collect_rollouts()
             rec.append(([t.clone() for t in algo._flat], st))
         assert (algo._ro_graph is not None) == graph
+        if venv.fresh:
+            rec.append(([torch.as_tensor(np.frombuffer(bytes(venv.scenario_table()), np.uint8))], {"episodes": 0}))
         outs.append(rec)
         venv.close()
     for (fa, sa), (fb, sb) in zip(*outs):
         for a, b in zip(fa, fb):
             assert torch.equal(a, b)
         assert sa["episodes"] == sb["episodes"]
+    assert sum(s["episodes"] for _, s in outs[1]) > 0
 
 
 @pytest.mark.gpu

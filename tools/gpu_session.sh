@@ -1,10 +1,10 @@
 #!/bin/bash
-# Round-4 final GPU session: parity suite, smoke, benches (driver's 20/5, steady state, every
-# BASELINE config + the fresh curriculum), rocprofv3 kernel trace + PMC passes of the headline,
-# the fresh curriculum's kernel split, PPO on corridor and on the fresh curriculum.
+# GPU session (bash tools/gpu_session.sh TAG): parity suite, smoke, benches (driver's 20/5, steady
+# state, every BASELINE config + the fresh curriculum), rocprofv3 kernel trace + PMC passes of the
+# headline, the fresh curriculum's kernel split, PPO on corridor and on the fresh curriculum.
 # Every GPU step has its own time limit; a crash / fault / timeout ends the script (no retries).
 set -u
-TAG=${1:-r04final}
+TAG=${1:-r05}
 R=$(pwd)
 OUT=$R/gpurun_out/$TAG
 mkdir -p "$OUT"
