@@ -35,6 +35,13 @@
 #ifndef D2D_RM_CARRY_KA
 #define D2D_RM_CARRY_KA 1  // A/B: brent_step carries ka in the state for global-memory tables (0: reload)
 #endif
+#ifndef D2D_RCACHE
+#define D2D_RCACHE 0  // A/B: 1 = K1's plain search over global-memory tables caches the probe's
+                      // interval record in LDS instead of staging the lane's knots there.  Measured
+                      // slower (fresh K1 80.5 vs 77.7 us, profiles/r05/a): 68 % of probes hit the
+                      // cached interval, but some lane of the wave misses on most early steps, so the
+                      // wave still waits for a global record load on nearly every step of its chain
+#endif
 // D2D_BSTAMP (diagnostic builds only, tools/bstamps.py): s_memtime stamps inside the golden-march
 // continuation's Brent steps, per path wave -- [workgroup][step < 64][8] in d2d_bst: entry, candidate
 // computed, interval found, probe evaluated, state updated, the step's B.num, whether the wave took
@@ -190,7 +197,7 @@ __device__ __forceinline__ double div_by_recip(double a, double b, double y) {
 // (rsq estimate + Goldschmidt/Newton refinement) without its range-scaling steps, which only act
 // below 2^-767.  Squared distances between fp64 points are 0 or far above that.  Checked bitwise
 // against sqrt() by d2d_selftest.
-__device__ __forceinline__ double sqrt_nz(double x) {
+__device__ __forceinline__ double sqrt_refine(double x) {
     const double y = __builtin_amdgcn_rsq(x);
     double g = x * y;
     double h = 0.5 * y;
@@ -200,12 +207,31 @@ __device__ __forceinline__ double sqrt_nz(double x) {
     double d = fma(-g, g, x);
     g = fma(d, h, g);
     d = fma(-g, g, x);
-    g = fma(d, h, g);
-    // +-0 and +inf return themselves (the refinement would give NaN for inf), NaN propagates
-    return __builtin_amdgcn_class(x, 0x260) ? x : g;
+    return fma(d, h, g);
 }
-// distances: the range-limited sqrt (squared fp64 distances are 0 or >= 2^-767)
-__device__ __forceinline__ double sqrt_dist(double x) { return sqrt_nz(x); }
+__device__ __forceinline__ double sqrt_nz(double x) {
+    // +-0 and +inf return themselves (the refinement would give NaN for inf), NaN propagates
+    return __builtin_amdgcn_class(x, 0x260) ? x : sqrt_refine(x);
+}
+// distances: the range-limited sqrt (squared fp64 distances are 0 or >= 2^-767).  The +-0 / inf /
+// NaN fix-up is a wave-uniform branch taken only when some lane needs it (a probe exactly on the
+// drone's position): one compare per distance instead of a compare and two selects.  The same
+// results as sqrt_nz bit for bit (d2d_selftest checks it against sqrt()).
+__device__ __forceinline__ double sqrt_dist(double x) {
+    double g = sqrt_refine(x);
+    if (__builtin_expect(__ballot(__builtin_amdgcn_class(x, 0x260)) != 0ull, 0)) {
+        asm volatile("" ::: "memory");  // keeps the branch (no if-conversion into selects)
+        g = __builtin_amdgcn_class(x, 0x260) ? x : g;
+    }
+    return g;
+}
+// max(|r|, t) for finite r and t > 0: one v_max_f64 with the abs modifier (fmax first quiets both
+// operands for its NaN rule, two more v_max_f64, and no operand here can be NaN)
+__device__ __forceinline__ double max_abs_fin(double r, double t) {
+    double m;
+    asm("v_max_f64 %0, |%1|, %2" : "=v"(m) : "v"(r), "v"(t));
+    return m;
+}
 // Correctly rounded a / b for normal operands with a normal quotient (no div_scale / div_fixup
 // range handling: results for zero / inf / NaN / extreme-exponent operands are unspecified).
 // Checked bitwise against '/' by d2d_selftest.
@@ -402,10 +428,12 @@ struct Brent {
     double a, b, fulc, ffulc, nfc, fnfc, xf, fx, rat, e;
     double ka, kxf;
     int num, ia, ib, ixf;
+    int rci;  // record cache (D2D_RCACHE, global-memory tables): interval whose record the lane holds in LDS, -1: none
 };
 constexpr double BR_SQRT_EPS = 1.4832396974191326e-08;  // sqrt(2.2e-16)
 constexpr double BR_GOLDEN = 0.3819660112501051;        // 0.5*(3.0 - sqrt(5.0))
 constexpr double BR_XATOL3 = 1e-6 / 3.0;
+constexpr int BT_K_MAX = 48;  // = BT_K (golden-march table steps): a snapshot's num is at most BT_K + 1
 template <class S>
 __device__ __forceinline__ void brent_init(const S& s, const PathK& K, double px, double py, Brent& B) {
     B.a = 0.0 - 10.0;
@@ -423,17 +451,20 @@ __device__ __forceinline__ void brent_init(const S& s, const PathK& K, double px
     B.num = 1;
     B.ffulc = B.fx;
     B.fnfc = B.fx;
+    B.rci = -1;
 }
-__device__ __forceinline__ bool brent_active(const Brent& B) {
+// scipy's loop condition without maxfun: |xf - xm| > tol2 - (b - a) / 2
+__device__ __forceinline__ bool brent_open(const Brent& B) {
     const double xm = 0.5 * (B.a + B.b);
     const double tol1 = BR_SQRT_EPS * fabs(B.xf) + BR_XATOL3;
     const double tol2 = 2.0 * tol1;
-    return (fabs(B.xf - xm) > (tol2 - 0.5 * (B.b - B.a))) & (B.num < 500);
+    return fabs(B.xf - xm) > (tol2 - 0.5 * (B.b - B.a));
 }
+__device__ __forceinline__ bool brent_active(const Brent& B) { return brent_open(B) & (B.num < 500); }
 // KN: the knot scan reads the lane's knots staged in LDS at kn (global-memory tables, closest_u)
 template <bool KN = false, class S>
 __device__ __forceinline__ void brent_step(const S& s, const PathK& K, double px, double py, Brent& B,
-                                           const double* kn = nullptr BST_ARG) {
+                                           double* kn = nullptr BST_ARG) {
 #ifdef D2D_BSTAMP
     uint64_t bst_t[5];
 #endif
@@ -475,7 +506,7 @@ __device__ __forceinline__ void brent_step(const S& s, const PathK& K, double px
     // x = xf + (sign(rat) + (rat == 0)) * max(|rat|, tol1).  rat is finite (a, b, xf are, and the
     // parabolic step is taken only when |p/q| < |e|/2), so np.max's NaN rule never applies and the
     // product is exactly -mx for rat < 0 and +mx otherwise
-    const double mx = fmax(fabs(rat), tol1);
+    const double mx = max_abs_fin(rat, tol1);
     // (rat is never -0: e_g = a - xf or b - xf is +0 at worst, the parabolic step is p + 0.0 over
     // |q| or tol1 times a nonzero sign, so copysign gives the same -mx / +mx)
     const double x = xf + copysign(mx, rat);
@@ -494,8 +525,22 @@ __device__ __forceinline__ void brent_step(const S& s, const PathK& K, double px
         if constexpr (S::RM) {
             int z = 0;
             asm volatile("" : "+v"(z));
-            if constexpr (KN) ix = u_index_kn(kn, K.nw, x, z);
-            else ix = u_index_at(s, x, z);
+            if constexpr (KN && D2D_RCACHE) {
+                // the cached record's interval first: u_index(x) == n exactly when us[n] < x <= us[n+1]
+                // (n >= 1; n = 0: x <= us[1]), the knots being non-decreasing (NaN fails both)
+                const int lane = (int)(threadIdx.x & 63);
+                const double c0 = kn[64 * REC_U0 + lane], c1 = kn[64 * REC_U1 + lane];
+                const bool inc = (B.rci >= 0) & (x <= c1) & ((B.rci == 0) | (c0 < x));
+                ix = B.rci;
+                if (__ballot(!inc) != 0ull) {
+                    const int iscan = u_index_at(s, x, z);
+                    ix = inc ? ix : iscan;
+                }
+            } else if constexpr (KN) {
+                ix = u_index_kn(kn, K.nw, x, z);
+            } else {
+                ix = u_index_at(s, x, z);
+            }
         } else {
             const S* sp = &s;
             asm volatile("" : "+v"(sp));
@@ -504,9 +549,32 @@ __device__ __forceinline__ void brent_step(const S& s, const PathK& K, double px
     }
     BST(2, ix);
     double kx;
-    const double fu = path_dist_n(s, K, x, ix, px, py, kx);
+    double fu;
+    if constexpr (KN && D2D_RCACHE) {
+        // global-memory tables (one scenario per lane, fresh curriculum): the interval's record from the
+        // lane's LDS cache when it is the interval of the previous probe (most probes once the bracket
+        // has closed in), else from global memory into the cache -- one record load per interval
+        // change instead of one per probe
+        const int lane = (int)(threadIdx.x & 63);
+        const bool hit = ix == B.rci;
+        if (__ballot(!hit) != 0ull) {
+            if (!hit) {
+#pragma unroll
+                for (int f = 0; f < REC_N; ++f) kn[64 * f + lane] = SREC(s, f, ix);
+                B.rci = ix;
+            }
+        }
+        double r[REC_N];
+#pragma unroll
+        for (int f = 0; f < REC_N; ++f) r[f] = kn[64 * f + lane];
+        double xq, yq;
+        path_eval_rec(r, K, x, ix, xq, yq, kx);
+        fu = norm2(xq - px, yq - py);
+    } else {
+        fu = path_dist_n(s, K, x, ix, px, py, kx);
+    }
     BST(3, fu);
-    B.num += 1;
+    // (num, scipy's maxfun count, is not advanced here: brent_run derives it from its pass count)
     const bool le = fu <= fx;
     const bool c1 = !le & ((fu <= B.fnfc) | (nfc == xf));
     const bool c2 = !le & !c1 & ((fu <= B.ffulc) | (fulc == xf) | (fulc == nfc));
@@ -541,36 +609,53 @@ __device__ __forceinline__ void brent_step(const S& s, const PathK& K, double px
     const uint64_t act = __ballot(1);
     if (bst && (int)(threadIdx.x & 63) == __ffsll((unsigned long long)act) - 1) {
         for (int k = 0; k < 5; ++k) bst[k] = bst_t[k];
-        bst[5] = (uint64_t)B.num;
+        bst[5] = 0;
         bst[6] = (uint64_t)(__ballot(!fast) != 0ull);
         bst[7] = (uint64_t)__popcll(act);
     }
 #endif
+}
+// scipy's `while` loop (maxfun = 500 included).  A lane takes one step per pass of the wave's loop
+// until it is inactive (a finished search stays finished), so at pass `it` an active lane's num is
+// its entry num + it; entry nums are at most BT_K + 1 (a golden-march snapshot), so num < 500 holds
+// for every active lane while it + BT_K + 1 < 500 and the per-lane count is only tested past that
+// (never reached by a search over a finite bracket: the golden steps alone shrink it below xtol in
+// ~60 passes).  brent_step does not advance num; B.num stays the entry count.
+template <bool KN = false, class S>
+__device__ __forceinline__ void brent_run(const S& s, const PathK& K, double px, double py, Brent& B,
+                                          double* kn = nullptr) {
+    constexpr int IT_FREE = 500 - (BT_K_MAX + 1);
+    for (int it = 0;; ++it) {
+        bool act = brent_open(B);
+        if (__builtin_expect(it >= IT_FREE, 0)) {
+            asm volatile("" ::: "memory");  // a scalar branch, not a per-pass compare
+            act = act & (B.num + it < 500);
+        }
+        if (!act) break;
+#ifdef D2D_BSTAMP
+        uint64_t* bst = nullptr;
+        if ((threadIdx.x >> 6) == 2 && blockIdx.x < 1024 && it < 64) bst = d2d_bst + ((size_t)blockIdx.x * 64 + it) * 8;
+        brent_step<KN>(s, K, px, py, B, kn, bst);
+#else
+        brent_step<KN>(s, K, px, py, B, kn);
+#endif
+    }
 }
 // (iu: the knot interval of the result, u_index(s, result), tracked by the search)
 // kn (global-memory tables only, K1's path wave): LDS for the lane's knots, which the knot scans
 // then read instead of global memory (16 x 64 doubles)
 template <bool KN = false, class S>
 __device__ __forceinline__ double closest_u(const S& s, double px, double py, int& iu, double* kn = nullptr) {
-    static_assert(!KN || S::RM, "staged knots: global-memory tables only");
+    static_assert(!KN || S::RM, "staged knots / record cache: global-memory tables only");
+    static_assert(REC_N <= D2D_MAX_WPS, "the record cache reuses the knot staging's LDS (K1_KN_BYTES)");
     const PathK K = path_k(s);
-    if constexpr (KN) {
+    if constexpr (KN && !D2D_RCACHE) {
 #pragma unroll
         for (int k = 0; k < D2D_MAX_WPS; ++k) kn[64 * k + (threadIdx.x & 63)] = SUS(s, k);
     }
     Brent B;
     brent_init(s, K, px, py, B);
-#ifdef D2D_BSTAMP
-    int it = 0;
-    while (brent_active(B)) {
-        uint64_t* bst = nullptr;
-        if ((threadIdx.x >> 6) == 2 && blockIdx.x < 1024 && it < 64) bst = d2d_bst + ((size_t)blockIdx.x * 64 + it) * 8;
-        brent_step<KN>(s, K, px, py, B, kn, bst);
-        ++it;
-    }
-#else
-    while (brent_active(B)) brent_step<KN>(s, K, px, py, B, kn);
-#endif
+    brent_run<KN>(s, K, px, py, B, kn);
     iu = B.ixf;
     return B.xf;
 }
@@ -596,7 +681,7 @@ __device__ __forceinline__ double closest_u(const S& s, double px, double py, in
 #ifndef D2D_BT_MASK
 #define D2D_BT_MASK 1  // exec-masked table loads in the re-check (global-memory tables only; A/B: 0)
 #endif
-constexpr int BT_K = 48;    // recorded steps per kind (longer marches continue in brent_step)
+constexpr int BT_K = BT_K_MAX;  // recorded steps per kind (longer marches continue in brent_step)
 constexpr int BT_HOT = BT_K + 3;  // probe entries per kind: 0..BT_K, plus zero entries the 3-step
                                   // unrolled check may read past a table's end
 struct BtIt {             // probe j (0: the initial point; k + 1: the probe of step k) + step k's operands
@@ -663,7 +748,7 @@ __device__ __forceinline__ void brtab_build(const SC& s, int kind, BrTab& T) {
         const double rat = BR_GOLDEN * e_g;
         B.e = e_g;
         B.rat = rat;
-        const double mx = fmax(fabs(rat), tol1);
+        const double mx = max_abs_fin(rat, tol1);
         const double x = xf + ((rat < 0.0) ? -mx : mx);
         const int ix = u_index(s, x);
         double kx;
@@ -815,22 +900,13 @@ __device__ __forceinline__ double bt_finish(const SC& s, const BrTab& T, const B
     B.ia = S.ia;
     B.ib = S.ib;
     B.ixf = S.ixf;
+    B.rci = -1;
     if (__ballot(brent_active(B)) != 0ull) {
         const PathK K = path_k(s);
         B.ffulc = bt_dist<LT>(hot, kind, S.j_fulc, px, py);
         B.fnfc = bt_dist<LT>(hot, kind, S.j_nfc, px, py);
         B.fx = bt_dist<LT>(hot, kind, S.j_xf, px, py);
-#ifdef D2D_BSTAMP
-        int it = 0;
-        while (brent_active(B)) {
-            uint64_t* bst = nullptr;
-            if ((threadIdx.x >> 6) == 2 && blockIdx.x < 1024 && it < 64) bst = d2d_bst + ((size_t)blockIdx.x * 64 + it) * 8;
-            brent_step(s, K, px, py, B, nullptr, bst);
-            ++it;
-        }
-#else
-        while (!(D2D_ABLATE & 16) && brent_active(B)) brent_step(s, K, px, py, B);
-#endif
+        if (!(D2D_ABLATE & 16)) brent_run(s, K, px, py, B);
     }
     iu = B.ixf;
     return B.xf;

@@ -743,8 +743,12 @@ int32_t d2d_step(d2d_t* h, const float* act_dev, float* obs_dev, float* rew_dev,
             if (s3) launch(d2d_step_kernel<true, false, true>, grid, lds_scn);
             else launch(d2d_step_kernel<true, false, false>, grid, lds_scn);
         } else {
-            if (s3) launch(d2d_step_kernel<false, false, true>, grid, K1_KN_BYTES);
-            else launch(d2d_step_kernel<false, false, false>, grid, K1_KN_BYTES);
+            // the plain search's staged knots only without golden-march tables (fresh curriculum);
+            // a pool's tables (a.brt) take the table path, which never reads them
+            const size_t kn = a.brt ? 0 : K1_KN_BYTES;
+            static_assert(sizeof(K1Shared) + K1_KN_BYTES <= K1_LDS_BUDGET, "K1 LDS with the staged knots");
+            if (s3) launch(d2d_step_kernel<false, false, true>, grid, kn);
+            else launch(d2d_step_kernel<false, false, false>, grid, kn);
         }
     }
     e = hipGetLastError();

@@ -1236,7 +1236,9 @@ __global__ __launch_bounds__(256) void d2d_selftest_kernel(int which, long long 
         if (which == D2D_SELFTEST_SQRT) {
             const uint32_t sel = p[0] & 63u;  // 1/64 zeros, 1/64 +inf, the rest in [2^-767, max]
             const double x = (sel == 0u) ? 0.0 : ((sel == 1u) ? __builtin_inf() : st_rand(o[0], o[1], 1023 - 767, 2046, 0u));
-            got = sqrt_nz(x);
+            // odd indices through sqrt_dist (the wave-uniform fix-up branch: waves with a zero or an
+            // infinity among their lanes take it), even ones through sqrt_nz
+            got = (k & 1) ? sqrt_dist(x) : sqrt_nz(x);
             want = sqrt(x);
         } else {
             const double a = st_rand(o[0], o[1], 1023 - 400, 1023 + 400, o[2]);
