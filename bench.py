@@ -68,6 +68,9 @@ def parse():
                    help="also write the per-env info rows (f32 [N, 12], what the SB3 adapter reads): +48 B/env-step")
     p.add_argument("--eager", action="store_true",
                    help="launch every step from Python instead of replaying the captured hipGraph")
+    p.add_argument("--exact-trig", action="store_true",
+                   help="the exact-trig library build (Drone2dVecEnv(exact_trig=True): fdlibm sin / cos / "
+                        "atan2, the reference's bearing sequence; bit-identical to the oracle's exact build)")
     return p.parse_args()
 
 
@@ -244,7 +247,8 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
     n = args.envs
     # this rank's block of a global batch of world x n envs (global env ids, no step collective)
-    venv = shard.make_shard_venv(n * world, rank, world, device=dev, seed=12345, with_info=args.info, **kwargs)
+    venv = shard.make_shard_venv(n * world, rank, world, device=dev, seed=12345, with_info=args.info,
+                                 exact_trig=args.exact_trig, **kwargs)
     # one global action bank (seed 1000) sliced by rank: a run of world x n envs in one process
     # steps exactly the same envs with exactly the same actions (global env ids below)
     g = torch.Generator(device=dev).manual_seed(1000)

@@ -19,6 +19,9 @@ def env_headers() -> list:
 
 HDRS = env_headers()
 OUT = os.path.join(PKG_DIR, "_lib", "libdrone2d_hip.so")
+# the same source with -DD2D_EXACT_TRIG=1: sin / cos / atan2 from d2d_pmath.h and the reference's
+# bearing sequence (Drone2dVecEnv(exact_trig=True); bit-identical to the oracle's exact build)
+EXACT_OUT = os.path.join(PKG_DIR, "_lib", "libdrone2d_hip_exact.so")
 # the PPO update's fused element-wise kernels (include/d2d_ppo.h)
 PPO_SRC = os.path.join(PKG_DIR, "csrc", "d2d_ppo.hip")
 PPO_HDRS = [os.path.join(REPO, "include", "d2d_ppo.h")]
@@ -62,13 +65,15 @@ def _compile(src: str, out: str, verbose: bool, flags=None):
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
-    """The in-tree libraries: the env (libdrone2d_hip.so: every mode, one scenario layout) and the PPO
-    update kernels (libd2d_ppo.so)."""
+    """The in-tree libraries: the env (libdrone2d_hip.so: every mode, one scenario layout), its
+    exact-trig build (libdrone2d_hip_exact.so) and the PPO update kernels (libd2d_ppo.so)."""
     stale = os.path.join(PKG_DIR, "_lib", "libdrone2d_hip_rm.so")  # rounds 1-3's second layout build
     if os.path.exists(stale):
         os.remove(stale)
     if force or needs_build():
         _compile(SRC, OUT, verbose)
+    if force or needs_build(EXACT_OUT):
+        _compile(SRC, EXACT_OUT, verbose, HIPCC_FLAGS + ["-DD2D_EXACT_TRIG=1"])
     if force or needs_build(PPO_OUT, PPO_SRC, PPO_HDRS):
         _compile(PPO_SRC, PPO_OUT, verbose, PPO_FLAGS)
     return OUT

@@ -14,6 +14,8 @@ from . import abi
 LIB_NAME = "libdrone2d_hip.so"
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib")
 LIB_PATH = os.path.join(LIB_DIR, LIB_NAME)
+# the exact-trig build of the same source (d2d_device.h D2D_EXACT_TRIG)
+EXACT_LIB_PATH = os.path.join(LIB_DIR, "libdrone2d_hip_exact.so")
 
 # every entry point of include/drone2d.h: name -> (restype, argtypes)
 _VP = C.c_void_p

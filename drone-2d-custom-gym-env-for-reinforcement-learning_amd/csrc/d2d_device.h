@@ -24,6 +24,7 @@
 #include <stdint.h>
 
 #include "../../include/drone2d.h"
+#include "d2d_pmath.h"
 
 // bool conditions are combined with & / | on purpose (selects instead of short-circuit branches)
 #pragma clang diagnostic ignored "-Wbitwise-instead-of-logical"
@@ -283,7 +284,31 @@ __device__ __forceinline__ double sgn_nz(double x) {
     const double s = (x < 0.0) ? -1.0 : 1.0;
     return (x != x) ? x : s;
 }
-__device__ __forceinline__ void sincos_d(double x, double& s, double& c) { sincos(x, &s, &c); }
+// D2D_EXACT_TRIG (a second build of the library, libdrone2d_hip_exact.so, exact_trig=True in the
+// Python facade): every sine / cosine / arctangent the state or the observation depends on is
+// d2d_pmath.h's fdlibm restatement, which the CPU oracle's exact build (libd2d_oracle_exact.so)
+// uses too, and the bearings take the reference sequence (atan2 -> ssa -> sincos) instead of the
+// rotated unit vectors: state and observation are then bit-identical to that oracle's, so a closed
+// loop (a policy acting on the observations) stays identical to it, episode for episode
+// (tests/test_harness.py).  The default build uses the device library and the cheaper sequences
+// (a few ulp apart; DESIGN.md "Round 5").
+#ifndef D2D_EXACT_TRIG
+#define D2D_EXACT_TRIG 0
+#endif
+__device__ __forceinline__ void sincos_d(double x, double& s, double& c) {
+#if D2D_EXACT_TRIG
+    d2d_pm_sincos(x, &s, &c);
+#else
+    sincos(x, &s, &c);
+#endif
+}
+__device__ __forceinline__ double atan2_d(double y, double x) {
+#if D2D_EXACT_TRIG
+    return d2d_pm_atan2(y, x);
+#else
+    return atan2(y, x);
+#endif
+}
 
 // ------------------------------------------------------------------------------ Philox4x32-10
 __device__ __forceinline__ void philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
@@ -1077,7 +1102,7 @@ __device__ __forceinline__ bool phys_positions(const S& s, Body B[3], double fL,
 #pragma unroll
     for (int i = 1; i < 3; ++i) {
         const double d = B[i].a - B[0].a;
-        if (fabs(d) < 1e-2) {
+        if (!D2D_EXACT_TRIG && fabs(d) < 1e-2) {
             const double d2 = d * d;
             const double sd = d * fma(d2, fma(d2, fma(d2, -1.0 / 5040.0, 1.0 / 120.0), -1.0 / 6.0), 1.0);
             const double cdm1 = d2 * fma(d2, fma(d2, fma(d2, 1.0 / 40320.0, -1.0 / 720.0), 1.0 / 24.0), -0.5);
@@ -1259,7 +1284,7 @@ template <typename Ref>
 __device__ __forceinline__ void rel_dir(double y, double x, double sa, double ca, double& s, double& c,
                                         const Ref& ref) {
     const double r2 = fma(y, y, x * x);
-    if ((r2 > 1e-200) & (r2 < 1e300)) {
+    if (!D2D_EXACT_TRIG && (r2 > 1e-200) & (r2 < 1e300)) {
         const double ir = 1.0 / sqrt_nz(r2);
         const double ux = x * ir, uy = y * ir;
         s = uy * ca - ux * sa;  // sin(phi - al)
@@ -1274,7 +1299,7 @@ __device__ __forceinline__ void sensor_vel(const Body& F, double sa, double ca, 
     o[1] = m1to1(F.vy, -VEL_MAX, VEL_MAX);
     o[2] = clipd(F.w / 11.7, -1.0, 1.0);
     rel_dir(F.vy, F.vx, sa, ca, o[17], o[18], [&](double& s, double& c) {
-        const double vab = ssa(atan2(F.vy, F.vx) - F.a);
+        const double vab = ssa(atan2_d(F.vy, F.vx) - F.a);
         sincos_d(vab, s, c);
     });
 }
@@ -1369,7 +1394,7 @@ __device__ __forceinline__ void sensor_pos(const d2d_cfg& cfg, const S& s, doubl
         double sa, ca;
         // ssa(atan2(dy, dx) - al - pi): the rotated unit vector, negated
         rel_dir(dy, dx, sal, cal, sa, ca, [&](double& rs, double& rc) {
-            const double ang = ssa(atan2(dy, dx) - al - PI);
+            const double ang = ssa(atan2_d(dy, dx) - al - PI);
             sincos_d(ang, rs, rc);
             rs = -rs;
             rc = -rc;
@@ -1418,7 +1443,7 @@ __device__ __forceinline__ void path_obs_u(const d2d_cfg& cfg, const S& s, doubl
         double sa, ca;
         sincos_d(al, sa, ca);
         const double bx = fma(ca, dx, (-sa) * dy), by = fma(sa, dx, ca * dy);
-        sincos_d(ssa(atan2(by, bx) - al), rs, rc);
+        sincos_d(ssa(atan2_d(by, bx) - al), rs, rc);
     };
     const double ldx = lax - x, ldy = lay - y, cdx = cpx - x, cdy = cpy - y;
     rel_dir(ldy, ldx, 0.0, 1.0, o[4], o[5], [&](double& rs, double& rc) { ref(ldx, ldy, rs, rc); });
@@ -1528,7 +1553,7 @@ __device__ __forceinline__ RewardVel reward_vel(const d2d_cfg& cfg, const double
     if (C.d < cfg.danger_range) {
         const double A = cfg.danger_angle, k = cfg.abs_inv_ca_min_rew;
         // |wrap(obstacle angle - velocity angle)| in degrees
-        const double adiff = fabs(atan2(C.os * R.vc - C.oc * R.vs, C.oc * R.vc + C.os * R.vs) * (180.0 / PI));
+        const double adiff = fabs(atan2_d(C.os * R.vc - C.oc * R.vs, C.oc * R.vc + C.os * R.vs) * (180.0 / PI));
         double ar = -(((A + k * A) / (adiff + k * A)) - 1.0);
         ar = (ar > 0.0) ? 0.0 : ar;
         ca = C.rr + ar;

@@ -91,4 +91,108 @@ D2D_PM_FN double d2d_pm_log(double x) {
     const double R = t2 + t1, hfsq = 0.5 * f * f;
     return dk * LN2_HI - ((hfsq - (s * (hfsq + R) + dk * LN2_LO)) - f);
 }
+/* fdlibm s_atan.c: atan(x), |error| < 1 ulp; the same operations on host and device */
+D2D_PM_FN double d2d_pm_atan(double x) {
+    static const double atanhi[4] = {4.63647609000806093515e-01, 7.85398163397448278999e-01,
+                                     9.82793723247329054082e-01, 1.57079632679489655800e+00};
+    static const double atanlo[4] = {2.26987774529616870924e-17, 3.06161699786838301793e-17,
+                                     1.39033110312309984516e-17, 6.12323399573676603587e-17};
+    const double aT0 = 3.33333333333329318027e-01, aT1 = -1.99999999998764832476e-01,
+                 aT2 = 1.42857142725034663711e-01, aT3 = -1.11111104054623557880e-01,
+                 aT4 = 9.09088713343650656196e-02, aT5 = -7.69187620504482999495e-02,
+                 aT6 = 6.66107313738753120669e-02, aT7 = -5.83357013379057348645e-02,
+                 aT8 = 4.97687799461593236017e-02, aT9 = -3.65315727442169155270e-02,
+                 aT10 = 1.62858201153657823623e-02;
+    const uint64_t b = d2d_pm_d2bits(x);
+    const int32_t hx = (int32_t)(b >> 32);
+    const int32_t ix = hx & 0x7fffffff;
+    int id;
+    if (ix >= 0x44100000) { /* |x| >= 2^66 */
+        if (ix > 0x7ff00000 || (ix == 0x7ff00000 && (uint32_t)b != 0u)) return x + x; /* NaN */
+        return hx > 0 ? atanhi[3] + atanlo[3] : -atanhi[3] - atanlo[3];
+    }
+    if (ix < 0x3fdc0000) { /* |x| < 0.4375 */
+        if (ix < 0x3e400000) return x; /* |x| < 2^-27 (fdlibm: huge + x > one, inexact) */
+        id = -1;
+    } else {
+        x = x < 0.0 ? -x : x;
+        if (ix < 0x3ff30000) {     /* |x| < 1.1875 */
+            if (ix < 0x3fe60000) { /* 7/16 <= |x| < 11/16 */
+                id = 0;
+                x = (2.0 * x - 1.0) / (2.0 + x);
+            } else { /* 11/16 <= |x| < 19/16 */
+                id = 1;
+                x = (x - 1.0) / (x + 1.0);
+            }
+        } else {
+            if (ix < 0x40038000) { /* |x| < 2.4375 */
+                id = 2;
+                x = (x - 1.5) / (1.0 + 1.5 * x);
+            } else { /* 2.4375 <= |x| < 2^66 */
+                id = 3;
+                x = -1.0 / x;
+            }
+        }
+    }
+    const double z = x * x, w = z * z;
+    const double s1 = z * (aT0 + w * (aT2 + w * (aT4 + w * (aT6 + w * (aT8 + w * aT10)))));
+    const double s2 = w * (aT1 + w * (aT3 + w * (aT5 + w * (aT7 + w * aT9))));
+    if (id < 0) return x - x * (s1 + s2);
+    const double r = atanhi[id] - ((x * (s1 + s2) - atanlo[id]) - x);
+    return hx < 0 ? -r : r;
+}
+/* fdlibm e_atan2.c: atan2(y, x) with its signed-zero / infinity cases */
+D2D_PM_FN double d2d_pm_atan2(double y, double x) {
+    const double pi_o_4 = 7.8539816339744827900E-01, pi_o_2 = 1.5707963267948965580E+00,
+                 pi = 3.1415926535897931160E+00, pi_lo = 1.2246467991473531772E-16;
+    const uint64_t bx = d2d_pm_d2bits(x), by = d2d_pm_d2bits(y);
+    const int32_t hx = (int32_t)(bx >> 32), hy = (int32_t)(by >> 32);
+    const uint32_t lx = (uint32_t)bx, ly = (uint32_t)by;
+    const int32_t ix = hx & 0x7fffffff, iy = hy & 0x7fffffff;
+    if (((uint32_t)ix | ((lx | (0u - lx)) >> 31)) > 0x7ff00000u ||
+        ((uint32_t)iy | ((ly | (0u - ly)) >> 31)) > 0x7ff00000u)
+        return x + y; /* NaN */
+    if (hx == 0x3ff00000 && lx == 0u) return d2d_pm_atan(y); /* x = 1.0 */
+    const int m = (int)(((uint32_t)hy >> 31) & 1u) | (int)(((uint32_t)hx >> 30) & 2u); /* 2 sign(x) + sign(y) */
+    if ((iy | (int32_t)ly) == 0) { /* y = +-0 */
+        switch (m) {
+            case 0:
+            case 1: return y;
+            case 2: return pi;
+            default: return -pi;
+        }
+    }
+    if ((ix | (int32_t)lx) == 0) return hy < 0 ? -pi_o_2 : pi_o_2; /* x = +-0 */
+    if (ix == 0x7ff00000) {
+        if (iy == 0x7ff00000) {
+            switch (m) {
+                case 0: return pi_o_4;
+                case 1: return -pi_o_4;
+                case 2: return 3.0 * pi_o_4;
+                default: return -3.0 * pi_o_4;
+            }
+        }
+        switch (m) {
+            case 0: return 0.0;
+            case 1: return -0.0;
+            case 2: return pi;
+            default: return -pi;
+        }
+    }
+    if (iy == 0x7ff00000) return hy < 0 ? -pi_o_2 : pi_o_2;
+    const int k = (iy - ix) >> 20;
+    double z;
+    if (k > 60) z = pi_o_2 + 0.5 * pi_lo; /* |y / x| > 2^60 */
+    else if (hx < 0 && k < -60) z = 0.0;  /* |y| / x < -2^60 */
+    else {
+        const double q = y / x;
+        z = d2d_pm_atan(q < 0.0 ? -q : q);
+    }
+    switch (m) {
+        case 0: return z;
+        case 1: return -z;
+        case 2: return pi - (z - pi_lo);
+        default: return (z - pi_lo) - pi;
+    }
+}
 #endif /* D2D_PMATH_H */

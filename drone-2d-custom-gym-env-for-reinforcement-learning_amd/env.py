@@ -135,10 +135,20 @@ class Drone2dVecEnv:
     def __init__(self, num_envs: int, device=None, seed: int = 0, *,
                  env_scenario: Sequence[int] | None = None, auto_reset: bool = True,
                  timeup_truncates: bool = False, with_info: bool = True, env_id_offset: int = 0,
-                 native_lib: str | None = None, envs_total: int | None = None, **kwargs):
+                 native_lib: str | None = None, envs_total: int | None = None, exact_trig: bool = False,
+                 **kwargs):
         self.kwargs = dict(kwargs)
         self.fresh = is_fresh_curriculum(self.kwargs)
-        # native_lib: an alternative build of the same source (diagnostic A/B builds only)
+        # exact_trig: the library build whose sin / cos / atan2 are d2d_pmath.h's restatements and whose
+        # bearings follow the reference's atan2 -> ssa -> sincos sequence; its states and observations
+        # are bit-identical to the CPU oracle's exact build, so closed loops match it episode for
+        # episode (default: the faster build, a few ulp apart).  native_lib: an alternative build of
+        # the same source (diagnostic A/B builds only).
+        self.exact_trig = bool(exact_trig)
+        if exact_trig and native_lib is None:
+            from ._native import EXACT_LIB_PATH
+
+            native_lib = EXACT_LIB_PATH
         self._lib = load(native_lib)
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device())

@@ -65,16 +65,18 @@ def allreduce_stats(stats: torch.Tensor, group=None) -> torch.Tensor:
     return stats
 
 
-def make_shard_venv(n_total: int, rank: int, world: int, *, device=None, seed: int = 0, **kwargs):
+def make_shard_venv(n_total: int, rank: int, world: int, *, device=None, seed: int = 0, with_info: bool = True,
+                    exact_trig: bool = False, **kwargs):
     """This rank's Drone2dVecEnv of a global batch of n_total envs (scenario i mod n_scenarios
     for global env i, as one unsharded batch would assign it)."""
     from .env import Drone2dVecEnv, build_scenarios, is_fresh_curriculum
 
     offset, count = shard_range(n_total, world, rank)
+    opt = dict(device=device, seed=seed, env_id_offset=offset, with_info=with_info, exact_trig=exact_trig)
     if is_fresh_curriculum(kwargs):  # per-episode device scenarios; the stage clock counts all ranks' envs
-        return Drone2dVecEnv(count, device=device, seed=seed, env_id_offset=offset, envs_total=n_total, **kwargs)
+        return Drone2dVecEnv(count, envs_total=n_total, **opt, **kwargs)
     es = shard_env_scenario(global_env_scenario(n_total, len(build_scenarios(kwargs))), offset, count)
-    return Drone2dVecEnv(count, device=device, seed=seed, env_id_offset=offset, env_scenario=es, **kwargs)
+    return Drone2dVecEnv(count, env_scenario=es, **opt, **kwargs)
 
 
 __all__ = ["shard_range", "global_env_scenario", "shard_env_scenario", "init_process_group_from_env",

@@ -33,6 +33,18 @@
 #include <stdlib.h>
 #include <string.h>
 
+#ifdef D2D_ORACLE_EXACT_TRIG
+/* the exact-trig build (libd2d_oracle_exact.so): every sin / cos / atan2 is d2d_pmath.h's fdlibm
+ * restatement, the functions libdrone2d_hip_exact.so calls on the device, so the two agree bit for
+ * bit (each a few ulp from glibc at most; the default build keeps glibc, pinned to the golden vectors) */
+#include "../drone-2d-custom-gym-env-for-reinforcement-learning_amd/csrc/d2d_pmath.h"
+static double ox_sin(double x) { double s, c; d2d_pm_sincos(x, &s, &c); return s; }
+static double ox_cos(double x) { double s, c; d2d_pm_sincos(x, &s, &c); return c; }
+#define sin ox_sin
+#define cos ox_cos
+#define atan2 d2d_pm_atan2
+#endif
+
 /* ------------------------------------------------------------------------------------------ */
 /* Python / NumPy scalar helpers                                                               */
 /* ------------------------------------------------------------------------------------------ */

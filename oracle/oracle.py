@@ -14,12 +14,16 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "libd2d_oracle.so")
+# sin / cos / atan2 from d2d_pmath.h: the oracle of the HIP library's exact-trig build
+LIB_EXACT = os.path.join(HERE, "libd2d_oracle_exact.so")
 
 
 def build(force: bool = False) -> str:
     src = [os.path.join(HERE, f) for f in ("d2d_oracle.c", "d2d_oracle.h", "Makefile")]
     src.append(os.path.join(HERE, "..", "include", "drone2d.h"))
-    if force or not os.path.exists(LIB) or any(os.path.getmtime(s) > os.path.getmtime(LIB) for s in src):
+    src.append(os.path.join(HERE, "..", "drone-2d-custom-gym-env-for-reinforcement-learning_amd", "csrc", "d2d_pmath.h"))
+    if force or any(not os.path.exists(o) or any(os.path.getmtime(s) > os.path.getmtime(o) for s in src)
+                    for o in (LIB, LIB_EXACT)):
         subprocess.run(["make", "-s", "-C", HERE, "-B" if force else "all"], check=True)
     return LIB
 
@@ -30,16 +34,16 @@ def _abi():
     return abi
 
 
-_lib = None
+_libs = {}
 
 
-def load() -> C.CDLL:
-    global _lib
-    if _lib is None:
-        if not os.path.exists(LIB):
+def load(exact_trig: bool = False) -> C.CDLL:
+    path = LIB_EXACT if exact_trig else LIB
+    if path not in _libs:
+        if not os.path.exists(path):
             build()
         abi = _abi()
-        lib = C.CDLL(LIB)
+        lib = C.CDLL(path)
         P, VP, I32, D = C.POINTER, C.c_void_p, C.c_int32, C.c_double
         sigs = {
             "d2dcpu_create": (VP, [P(abi.D2DCfg), I32]),
@@ -70,8 +74,8 @@ def load() -> C.CDLL:
             f = getattr(lib, name)
             f.restype = res
             f.argtypes = args
-        _lib = lib
-    return _lib
+        _libs[path] = lib
+    return _libs[path]
 
 
 def _p(a):
@@ -81,9 +85,10 @@ def _p(a):
 class OracleBatch:
     """Host-side batch with the same call shapes as the HIP library (numpy buffers)."""
 
-    def __init__(self, cfg, scenarios_c, n_envs: int, env_scenario=None, curriculum=None):
-        """``curriculum``: a D2DCurriculum for the fresh curriculum (cfg.scn_pool = 2; no scenarios)."""
-        self.lib = load()
+    def __init__(self, cfg, scenarios_c, n_envs: int, env_scenario=None, curriculum=None, exact_trig: bool = False):
+        """``curriculum``: a D2DCurriculum for the fresh curriculum (cfg.scn_pool = 2; no scenarios).
+        ``exact_trig``: the exact-trig build (the oracle of ``Drone2dVecEnv(exact_trig=True)``)."""
+        self.lib = load(exact_trig)
         abi = _abi()
         self.abi = abi
         self.n = int(n_envs)

@@ -6,7 +6,7 @@ import torch
 
 class OracleVecBackend:
     def __init__(self, num_envs, seed=0, env_scenario=None, timeup_truncates=False, env_id_offset=0,
-                 envs_total=None, **kwargs):
+                 envs_total=None, exact_trig=False, **kwargs):
         import oracle
 
         import drone2d_amd  # noqa: F401
@@ -27,7 +27,7 @@ class OracleVecBackend:
         self.cfg.scn_pool = (2 if fresh else 1) if is_curriculum(self.kwargs) else 0
         cur = make_curriculum(self.kwargs, envs_total or self.num_envs) if fresh else None
         self.orc = oracle.OracleBatch(self.cfg, [s.to_c() for s in self.scenarios], self.num_envs,
-                                      env_scenario=self.env_scenario, curriculum=cur)
+                                      env_scenario=self.env_scenario, curriculum=cur, exact_trig=exact_trig)
         self.seed_value = int(seed)
         self.action_space = _make_box(-np.ones(2), np.ones(2))
         self.observation_space = _make_box(-np.ones(27), np.ones(27))

@@ -293,11 +293,11 @@ def _records_equal(h, o):
     assert rew_ok[ident].all(), (h["rewards"][ident & ~rew_ok], o["rewards"][ident & ~rew_ok])
 
 
-def _oracle_run(scn, n, seed):
+def _oracle_run(scn, n, seed, exact_trig=False):
     from drone2d_amd import harness
     from drone2d_amd.config import ENV_TEST_CONFIG
 
-    be = OracleVecBackend(n, seed=seed, **dict(ENV_TEST_CONFIG, scenario=scn))
+    be = OracleVecBackend(n, seed=seed, exact_trig=exact_trig, **dict(ENV_TEST_CONFIG, scenario=scn))
     pol = harness.MlpActor.from_npz(os.path.join(GOLD, "agent_17_90.npz"), batch_invariant=True)
     m = harness.run_first_episodes(be, pol, seed=seed, flight_paths=True, policy_device="cpu")
     be.close()
@@ -333,6 +333,36 @@ def test_test_loop_hip_matches_oracle(d2, scn):
         assert abs(sh[k] - so[k]) <= 0.01, k
     for k in ("Average APE", "Average flight time"):
         assert sh[k] == pytest.approx(so[k], rel=1e-2), k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scn", ["corridor", "S_corridor"])
+def test_test_loop_exact_trig_identical(d2, scn):
+    """The exactness question of VERDICT r04 item 4, answered by a build: with exact_trig=True the
+    library computes every sin / cos / atan2 the state and observation depend on with d2d_pmath.h's
+    restatements (the physics' body rotations, the spawn, the bearings through the reference's
+    atan2 -> ssa -> sincos sequence), as the oracle's exact build does, so the reference's test loop
+    (main.py:258-327) on the HIP batch and on that oracle gives IDENTICAL records: every episode's
+    length, collision flag, flight path and APE bit for bit, successes / fails equal.  (Rewards are
+    compared to rtol 1e-12: the kernel's reward evaluates the decoded angles by an equivalent but
+    different sequence; they do not feed back into the loop.)"""
+    from drone2d_amd import harness
+    from drone2d_amd.config import ENV_TEST_CONFIG
+
+    n, seed = PARITY_ENVS, 11
+    venv = d2.Drone2dVecEnv(n, device=torch.device("cuda", 0), seed=seed, exact_trig=True,
+                            **dict(ENV_TEST_CONFIG, scenario=scn))
+    pol = harness.MlpActor.from_npz(os.path.join(GOLD, "agent_17_90.npz"), batch_invariant=True)
+    h = harness.run_first_episodes(venv, pol, seed=seed, flight_paths=True, policy_device="cpu")
+    venv.close()
+    o = _oracle_run(scn, n, seed, exact_trig=True)
+    assert h["unfinished"] == o["unfinished"] == 0
+    assert (h["successes"], h["fails"]) == (o["successes"], o["fails"])
+    np.testing.assert_array_equal(h["time_spent"], o["time_spent"])
+    np.testing.assert_array_equal(h["collisions"], o["collisions"])
+    np.testing.assert_array_equal(h["flight_xy"], o["flight_xy"])
+    np.testing.assert_array_equal(h["apes"], o["apes"])
+    np.testing.assert_allclose(h["rewards"], o["rewards"], rtol=1e-12, atol=0)
 
 
 def _hip_parity_worker(rank, world, port, out_path, scn, n, seed):
