@@ -50,7 +50,6 @@ struct d2d_handle {
     int pool_base = 0, pool_n = 0;
     int32_t* pool_dev = nullptr;
     int32_t* fill_ctl = nullptr;  // [2] K4's tick and finished-workgroup count
-    uint32_t* pair_ctr = nullptr; // [PAIR_CTRS] two-group K1's per-CU placement counters
     uint64_t seed = 0;
     bool reset_done = false;
     uint64_t* stamps = nullptr;  // diagnostic builds (D2D_STAMPS) only
@@ -83,15 +82,6 @@ struct d2d_handle {
 
 namespace {
 
-// two-group K1 (d2d_step_pair_kernel): D2D_K1_PAIR=1 in the environment (A/B while it is measured)
-bool k1_pair_enabled() {
-    static const bool on = [] {
-        const char* v = std::getenv("D2D_K1_PAIR");
-        return v && v[0] == '1';
-    }();
-    return on;
-}
-
 StepArgs make_args(const d2d_t* h) {
     StepArgs a{};
     a.n = h->n;
@@ -106,7 +96,6 @@ StepArgs make_args(const d2d_t* h) {
     a.pool_base = h->pool_dev;
     a.pool_n = h->pool_n;
     a.fill_ctl = h->fill_ctl;
-    a.pair_ctr = h->pair_ctr;
     a.fill_every = FILL_EVERY;
     a.fill_force = 0;
     a.cfg = h->cfg;
@@ -468,8 +457,6 @@ int32_t d2d_create(const d2d_cfg* cfg, int32_t n_envs, int32_t device, d2d_t** o
         (e = hipMemset(h->pool_dev, 0, sizeof(int32_t))) != hipSuccess ||
         (e = hipMalloc(&h->fill_ctl, 2 * sizeof(int32_t))) != hipSuccess ||
         (e = hipMemset(h->fill_ctl, 0, 2 * sizeof(int32_t))) != hipSuccess ||
-        (e = hipMalloc(&h->pair_ctr, PAIR_CTRS * sizeof(uint32_t))) != hipSuccess ||
-        (e = hipMemset(h->pair_ctr, 0, PAIR_CTRS * sizeof(uint32_t))) != hipSuccess ||
         (e = hipMalloc(&h->clock, sizeof(int64_t))) != hipSuccess ||
         (e = hipMemset(h->clock, 0, sizeof(int64_t))) != hipSuccess ||
         (e = alloc_layout(L, n_envs, {}, {})) != hipSuccess) {
@@ -496,7 +483,6 @@ void d2d_destroy(d2d_t* h) {
     if (h->env_scn) (void)hipFree(h->env_scn);
     if (h->pool_dev) (void)hipFree(h->pool_dev);
     if (h->fill_ctl) (void)hipFree(h->fill_ctl);
-    if (h->pair_ctr) (void)hipFree(h->pair_ctr);
     if (h->clock) (void)hipFree(h->clock);
     if (h->abi) (void)hipFree(h->abi);
     if (h->scn_tag) (void)hipFree(h->scn_tag);
@@ -743,14 +729,10 @@ int32_t d2d_step(d2d_t* h, const float* act_dev, float* obs_dev, float* rew_dev,
         // workgroup per CU: 4 096 / 16 384 envs -4 %), not at full load (65 536 envs +3.6 %)
         const int nwg = h->lane_env ? h->n_groups : (int)grid.x;
         const bool s3 = D2D_SPLIT3 > 0 || (D2D_SPLIT3 < 0 && nwg <= std::max(h->n_cu, 1));
-        auto launch = [&](auto kern, dim3 g, size_t lds, int threads = K1_THREADS) {
-            hipLaunchKernelGGL(kern, g, dim3(threads), lds, (hipStream_t)stream, a);
+        auto launch = [&](auto kern, dim3 g, size_t lds) {
+            hipLaunchKernelGGL(kern, g, dim3(K1_THREADS), lds, (hipStream_t)stream, a);
         };
-        static_assert(2 * sizeof(K1Shared) + sizeof(PairShared) + sizeof(d2d::ScnF) + sizeof(d2d::BtHot) <=
-                          2 * K1_LDS_BUDGET, "two-group K1 LDS (two workgroups per CU)");
-        if (k1_pair_enabled() && !h->lane_env && !h->rm && a.brt && h->n_scn == 1 && !s3) {
-            launch(d2d_step_pair_kernel, dim3(((int)grid.x + 1) / 2), sizeof(d2d::ScnF) + sizeof(d2d::BtHot), PAIR_THREADS);
-        } else if (h->lane_env) {
+        if (h->lane_env) {
             const size_t lds = sizeof(d2d::ScnF) + sizeof(d2d::BtHot);
             if (s3) launch(d2d_step_grouped_kernel<true>, dim3(h->n_groups), lds);
             else launch(d2d_step_grouped_kernel<false>, dim3(h->n_groups), lds);

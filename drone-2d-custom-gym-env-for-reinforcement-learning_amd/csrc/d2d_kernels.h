@@ -106,10 +106,6 @@ struct StepArgs {
     int32_t* fq;              // [fq_mask + 1] slots (a ring, see FreshRing)
     uint32_t* fqc;            // FreshRing words ([FR_HEAD]: appends so far)
     uint32_t fq_mask;         // ring size - 1 (a power of two >= 2 n)
-    // two-group K1 (d2d_step_pair_kernel): one counter per CU (HW_ID CU / SH / SE + XCC_ID); the two
-    // workgroups a CU holds at once draw consecutive values, whose parities pick complementary role
-    // placements
-    uint32_t* pair_ctr;       // [PAIR_CTRS]
 };
 
 // the scenario table in the layout the launch was instantiated for (ScnF: the handle stages its
@@ -362,36 +358,6 @@ __device__ __forceinline__ void k1_stage(const StepArgs& a, S* s_scn, int wg, co
     }
 }
 
-// Two-group K1 (d2d_step_pair_kernel, one scenario staged in LDS): a 512-thread workgroup steps two
-// 64-env groups, each with the four roles of k1_body, and pools their Brent continuations: after
-// both groups' golden-march re-checks, ONE wave (group 0's path wave, "C") resumes every search
-// that continues -- ~19 of 64 lanes per group at 65 536 corridor envs (tools/brent_lanes.py), so
-// the pooled set usually fits one wave -- instead of two path waves each iterating for the longest
-// of its ~19 searches at ~15 % lane occupancy.  The continuation is the same bt_finish on the same
-// operands, so every result is bit-identical.  The pooled wave is the heavy one, so roles are
-// placed per SIMD at run time (HW_ID) with the two workgroups of a CU taking complementary patterns
-// (pair_ctr parity): VALU per SIMD ~10.8 k instead of 12.1 k on corridor (DESIGN.md "Round 5").
-constexpr int PAIR_THREADS = 2 * K1_THREADS;
-constexpr int PAIR_CTRS = 8 * 256;  // XCC (3 bits) x SE / SH / CU (8 bits)
-struct PairShared {
-    double px[2][EPB], py[2][EPB];  // the post-step frame position of every lane (the searches' point)
-    double u[2][EPB];               // result of every lane's search (bt_finish)
-    int32_t iu[2][EPB];             // ... and its knot interval
-    int32_t kind[2][EPB];           // golden-march kind (-1: no search on this lane)
-    int32_t dev[2][EPB];            // first differing step
-    int32_t item[2 * EPB];          // the pooled searches: group << 6 | lane
-    uint32_t f_tab[2], f_cont;      // group g's table re-check done; pooled continuation done
-    int32_t simd[PAIR_THREADS / 64];
-    int32_t parity;
-};
-// role placement of a two-group workgroup: [parity][SIMD][rank of the wave among this workgroup's
-// two waves on that SIMD] -> group << 2 | role (0 physics, 1 sensing, 2 path, 3 reset).  Group 0's
-// path wave carries the pooled continuation; the patterns put it, in each workgroup of the CU, on a
-// different SIMD, with the light roles (reset, sensing) beside it and the physics waves elsewhere.
-__device__ constexpr int8_t PAIR_PAT[2][4][2] = {
-    {{0 << 2 | 2, 0 << 2 | 3}, {0 << 2 | 1, 1 << 2 | 3}, {0 << 2 | 0, 1 << 2 | 2}, {1 << 2 | 0, 1 << 2 | 1}},
-    {{0 << 2 | 1, 0 << 2 | 3}, {0 << 2 | 2, 1 << 2 | 3}, {0 << 2 | 0, 1 << 2 | 1}, {1 << 2 | 0, 1 << 2 | 2}}};
-
 // the dynamic LDS of every kernel (scenarios [+ probe tables]; global-memory tables: the path wave's
 // staged knots, K1_KN_BYTES), sized at launch
 extern __shared__ __attribute__((aligned(16))) uint4 d2d_dyn_lds[];
@@ -401,10 +367,9 @@ constexpr int K1_KN_BYTES = D2D_MAX_WPS * 64 * 8;
 // tables indexed by global scenario id (LDS when staged: LDS / LTAB), s0 the group's scenario.
 // All 256 threads of the group call it once; the workgroup's barriers are block-wide, so every
 // wave of the block runs k1_body exactly once.
-// PAIR: two-group workgroup (ps: its shared pool, g: this wave's group; see PairShared)
-template <bool LDS, bool LTAB, bool GRP, bool S3, class SC, bool PAIR = false>
+template <bool LDS, bool LTAB, bool GRP, bool S3, class SC>
 __device__ __forceinline__ void k1_body(const StepArgs& a, const SC* scns, const BtHot* hots, int s0, K1Shared& sh,
-                                        int wg, int role, int qt, PairShared* ps = nullptr, int g = 0) {
+                                        int wg, int role, int qt) {
     const int wave = role;
     const int lane = threadIdx.x & 63;
     const bool gvalid = wg >= 0;
@@ -640,81 +605,7 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const SC* scns, const
         __builtin_amdgcn_s_setprio(PRIO_W2);
         double po[8];
         Body F{};
-        if constexpr (PAIR) {
-            // two-group workgroup: every wave of the pair runs this block whole (its flags must be
-            // raised even by a group without envs)
-            const bool tab = valid && !(D2D_ABL & 4) && !(D2D_ABLATE & 1);
-            uint32_t f = 0;
-            BtLane L{};
-            L.kind = -1;
-            const BrTab& T = a.brt[s0];
-            const BtHot* hot = hots + s0;
-            if (valid && !(D2D_ABL & 4)) {
-                F = PF;
-                advance_position(F);
-                f = (uint32_t)fld(a.ist, D2D_I_FLAGS, n, i);
-            }
-            if (tab) {
-                L = bt_start<LTAB>(T, hot, F.px, F.py);
-                bt_verify<LTAB>(hot, L, 1, bt_split(T), F.px, F.py);
-            }
-            flag_wait(sh.f_ver);
-            if (tab) L.dev = min(L.dev, (int)sh.pflags[lane]);
-            ps->kind[g][lane] = tab ? L.kind : -1;
-            ps->dev[g][lane] = L.dev;
-            ps->px[g][lane] = F.px;
-            ps->py[g][lane] = F.py;
-            flag_raise(ps->f_tab[g]);
-            if (g == 0) {
-                // the pooled continuation of both groups (this wave, "C")
-                flag_wait(ps->f_tab[1]);
-                int cnt = 0;
-                const uint64_t below = (1ull << lane) - 1ull;
-#pragma unroll
-                for (int gg = 0; gg < 2; ++gg) {
-                    const int kd = ps->kind[gg][lane];
-                    bool act = false;
-                    if (kd >= 0) {
-                        // bt_finish's own test: is the search still open at the snapshot before dev?
-                        const BtSnap& W = T.snap[kd][ps->dev[gg][lane]];
-                        Brent B;
-                        B.a = W.a;
-                        B.b = W.b;
-                        B.xf = W.xf;
-                        B.num = W.num;
-                        act = brent_active(B);
-                        if (!act) {
-                            ps->u[gg][lane] = W.xf;
-                            ps->iu[gg][lane] = W.ixf;
-                        }
-                    }
-                    const uint64_t m = __ballot(act);
-                    if (act) ps->item[cnt + __popcll(m & below)] = gg * EPB + lane;
-                    cnt += __popcll(m);
-                }
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                for (int r0 = 0; r0 < cnt; r0 += 64) {
-                    if (r0 + lane < cnt) {
-                        const int it = ps->item[r0 + lane];
-                        const int gg = it >> 6, l = it & 63;
-                        int iu;
-                        const double u = bt_finish<LTAB>(scns[s0], T, hot, ps->kind[gg][l], ps->dev[gg][l],
-                                                         ps->px[gg][l], ps->py[gg][l], iu);
-                        ps->u[gg][l] = u;
-                        ps->iu[gg][l] = iu;
-                    }
-                }
-                flag_raise(ps->f_cont);
-            } else {
-                flag_wait(ps->f_cont);
-            }
-            if (tab) {
-                path_obs_u(a.cfg, S, F.px, F.py, F.a, ps->u[g][lane], f, po, ps->iu[g][lane]);
-                sh.pflags[lane] = f & D2D_FLAG_LA_LOCK;
-            }
-        } else if (valid && !(D2D_ABL & 4)) {
+        if (valid && !(D2D_ABL & 4)) {
             F = PF;
             advance_position(F);
             uint32_t f = (uint32_t)fld(a.ist, D2D_I_FLAGS, n, i);
@@ -990,42 +881,6 @@ __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_grouped_kernel(StepArg
         k1_group<true, false, true, S3, ScnF>(a, s_scn, sh, wg);
     else
         k1_group<false, false, true, S3, ScnF>(a, s_scn, sh, wg);
-}
-
-// Two-group K1 (see PairShared): 512 threads, two 64-env groups (2 b, 2 b + 1), one scenario and its
-// probe table staged once.  Roles by SIMD: every wave reads its SIMD from HW_ID; when the workgroup
-// has exactly two waves on each SIMD (the dispatcher's placement, tools/ubench_place2.hip), wave w
-// takes PAIR_PAT[parity][its SIMD][its rank there], else the fixed map (group w / 4, role w % 4).
-// The parity comes from a per-CU counter (two workgroups resident on a CU draw consecutive values).
-__global__ __launch_bounds__(PAIR_THREADS, 4) void d2d_step_pair_kernel(StepArgs a) {
-    __shared__ __attribute__((aligned(16))) K1Shared shp[2];
-    __shared__ __attribute__((aligned(16))) PairShared ps;
-    ScnF* s_scn = reinterpret_cast<ScnF*>(d2d_dyn_lds);
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-    const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_REG_HW_ID
-    if (lane == 0) ps.simd[w] = (int)((hw >> 4) & 3u);
-    if (threadIdx.x == 0) {
-        const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u;  // HW_REG_XCC_ID
-        const uint32_t cu = ((hw >> 8) & 15u) | (((hw >> 12) & 1u) << 4) | (((hw >> 13) & 7u) << 5);
-        ps.parity = (int)(atomicAdd(&a.pair_ctr[(xcc << 8) | cu], 1u) & 1u);
-        ps.f_tab[0] = ps.f_tab[1] = ps.f_cont = 0u;
-    }
-    glds_copy<PAIR_THREADS / 64>(s_scn, scn_tab<ScnF>(a), (int)sizeof(ScnF));
-    glds_copy<PAIR_THREADS / 64>(s_scn + 1, &a.brt[0].hot, (int)sizeof(BtHot));
-    __syncthreads();
-    int mine = ps.simd[w], rank = 0, cnt[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int v = 0; v < PAIR_THREADS / 64; ++v) {
-        const int sv = ps.simd[v];
-        cnt[sv] += 1;
-        rank += (v < w && sv == mine) ? 1 : 0;
-    }
-    const bool placed = cnt[0] == 2 && cnt[1] == 2 && cnt[2] == 2 && cnt[3] == 2;
-    const int code = __builtin_amdgcn_readfirstlane(placed ? (int)PAIR_PAT[ps.parity & 1][mine][rank] : w);
-    const int g = code >> 2, role = code & 3;
-    const BtHot* hots = reinterpret_cast<const BtHot*>(s_scn + 1);
-    k1_body<true, true, false, false, ScnF, true>(a, s_scn, hots, 0, shp[g], 2 * (int)blockIdx.x + g, role,
-                                                  role * 64 + lane, &ps, g);
 }
 
 // ------------------------------------------------------------------------------------------ K2
