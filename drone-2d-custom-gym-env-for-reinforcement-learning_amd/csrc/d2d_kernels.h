@@ -298,7 +298,8 @@ __device__ __forceinline__ int next_scenario(const StepArgs& a, int j, uint32_t 
 //   f_done  W0 -> W1,W2,W3  which envs end this step, cache readiness (right after the positions)
 //   f_ca    W1 -> W0,W2     CA inputs from obs 8..10 (CAStatic)
 //   f_gs    W0 -> W1,W2,W3  joint sweep finished: the jb region becomes the obs tile
-//   f_pre   W0 -> W2        velocity part of the reward (RewardVel)
+//   f_rp    W2 -> W0        the position / path terms of the reward (W0 sums the reward: the physics
+//                           wave ends last at full load, so the sum waits for no other wave)
 //   f_ver   W3 -> W2        first differing step in the second half of the table re-check
 struct K1Shared {
     double cas[6][EPB];       // W1 -> W0, W2: CAStatic (d, os, oc, lpa, lca, rr)
@@ -309,7 +310,7 @@ struct K1Shared {
                               // then W2 -> W0: LA-lock bit after the path role
     uint32_t ep[EPB];         // W0 -> W1, W3: episode counter (the state's copy changes at a reset)
     double sina[EPB];         // W0 -> W2: sin of the post-step frame angle (AA reward)
-    uint32_t f_done, f_ca, f_gs, f_pre, f_ver, f_ver1;
+    uint32_t f_done, f_ca, f_gs, f_rp, f_ver, f_ver1;
     double pe[2][EPB];        // W3 -> W0: path_err, total_reward (prefetched for the epilogue)
     double acc[D2D_NSTATS][EPB];  // W3 -> W0: episode accumulators of envs that end (prefetched)
     union {
@@ -318,8 +319,7 @@ struct K1Shared {
             double arms[ARMS_N][EPB];          // ... and the rotated anchor arms
         } g;
         struct {
-            double pre[4][EPB];            // W0 -> W2: RewardVel
-            double post[7][EPB];           // W2 -> W0: reward, pa, pp, dist, aa, coll, reach
+            double post[7][EPB];           // W2 -> W0: LA bearing (sin, cos), pa, dist, aa, coll, reach
             alignas(16) float obs[EPB * D2D_OBS_DIM];  // the workgroup's obs rows (16-B aligned: float4 stores)
         } p;                               // after f_gs
     } u;
@@ -396,7 +396,7 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const SC* scns, const
         sh.f_done = 0u;
         sh.f_ca = 0u;
         sh.f_gs = 0u;
-        sh.f_pre = 0u;
+        sh.f_rp = 0u;
         sh.f_ver = 0u;
         sh.f_ver1 = 0u;
     }
@@ -412,7 +412,7 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const SC* scns, const
     int t = 0, cause = 0;
     uint32_t flags = 0;
     RewardVel RV{};
-    double dclose = 0.0;
+    double dclose = 0.0, rew_sum = 0.0, rew_pp = 0.0;
     bool done = false;
     if (wave == 0) {
         // ---------------------------------------------------------------- physics
@@ -512,13 +512,23 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const SC* scns, const
             C.lca = sh.cas[4][lane];
             C.rr = sh.cas[5][lane];
             RV = reward_vel(a.cfg, ov, C);
-            sh.u.p.pre[0][lane] = RV.sv;
-            sh.u.p.pre[1][lane] = RV.vs;
-            sh.u.p.pre[2][lane] = RV.vc;
-            sh.u.p.pre[3][lane] = RV.cal;
             dclose = C.d;
         }
-        flag_raise(sh.f_pre);
+        // the reward: W2's position / path terms (usually long ready: the physics chain ends last)
+        flag_wait(sh.f_rp);
+        if (valid) {
+            RewardPos RP{};
+            RP.aa = sh.u.p.post[4][lane];
+            RP.coll = sh.u.p.post[5][lane];
+            RP.reach = sh.u.p.post[6][lane];
+            RewardPath RQ{};
+            RQ.ls = sh.u.p.post[0][lane];
+            RQ.lc = sh.u.p.post[1][lane];
+            RQ.pa = sh.u.p.post[2][lane];
+            const RewardSum Q = reward_sum(a.cfg, RP, RV, RQ);
+            rew_sum = Q.reward;
+            rew_pp = Q.pp;
+        }
     } else if (wave == 1) {
         // ---------------------------------------------------------------- sensing
         float row[19];
@@ -656,23 +666,18 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const SC* scns, const
                 for (int k = 0; k < 8; ++k) trow[19 + k] = (float)po[k];
             }
         }
-        flag_wait(sh.f_pre);
-        STAMP(5);
         if (valid) {
-            RewardVel V;
-            V.sv = sh.u.p.pre[0][lane];
-            V.vs = sh.u.p.pre[1][lane];
-            V.vc = sh.u.p.pre[2][lane];
-            V.cal = sh.u.p.pre[3][lane];
-            const RewardSum Q = reward_sum(a.cfg, RP, V, RQ);
-            sh.u.p.post[0][lane] = Q.reward;
-            sh.u.p.post[1][lane] = RQ.pa;
-            sh.u.p.post[2][lane] = Q.pp;
+            // the position / path terms for W0's sum (u.p is the obs-tile region: after f_gs)
+            sh.u.p.post[0][lane] = RQ.ls;
+            sh.u.p.post[1][lane] = RQ.lc;
+            sh.u.p.post[2][lane] = RQ.pa;
             sh.u.p.post[3][lane] = RQ.dist;
             sh.u.p.post[4][lane] = RP.aa;
             sh.u.p.post[5][lane] = RP.coll;
             sh.u.p.post[6][lane] = RP.reach;
         }
+        flag_raise(sh.f_rp);
+        STAMP(5);
     } else {
         // ---------------------------------------------------------------- auto-reset observation
         __builtin_amdgcn_s_setprio(PRIO_W2);  // the re-check below is on W2's critical path
@@ -796,7 +801,7 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const SC* scns, const
         path_err = sh.pe[0][lane];
         tot_rew = sh.pe[1][lane];
         flags = (flags & ~D2D_FLAG_LA_LOCK) | sh.pflags[lane];
-        const double reward = sh.u.p.post[0][lane];
+        const double reward = rew_sum;
         path_err += sh.u.p.post[3][lane];
         const double ape = path_err / (double)t;
         tot_rew += reward;
@@ -812,8 +817,8 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const SC* scns, const
         if (a.info) {
             float* r = a.info + (size_t)ie * D2D_INFO_DIM;
             r[D2D_INFO_CA] = (float)RV.cal;
-            r[D2D_INFO_PA] = (float)sh.u.p.post[1][lane];
-            r[D2D_INFO_PP] = (float)sh.u.p.post[2][lane];
+            r[D2D_INFO_PA] = (float)sh.u.p.post[2][lane];
+            r[D2D_INFO_PP] = (float)rew_pp;
             r[D2D_INFO_COLL] = (float)sh.u.p.post[5][lane];
             r[D2D_INFO_REACH] = (float)sh.u.p.post[6][lane];
             r[D2D_INFO_AA] = (float)sh.u.p.post[4][lane];

@@ -62,7 +62,7 @@ def run(scenario, n, steps_warm, lib=LIB):
     # cumulative times from the wave's stamp 1 (after staging): [median, p95, max]
     marks = {0: {"physics_done": 4, "ca_received": 5},
              1: {"sensing_done": 4, "gs_received": 5},
-             2: {"search_done": 4, "pre_received": 5},
+             2: {"search_done": 4, "rp_raised": 5},
              3: {"reset_part_done": 4, "gs_received": 5}}
     for w in range(4):
         r = {"stage": [int(np.median(s[:, w, 1] - s[:, w, 0]))]}

@@ -58,8 +58,10 @@ def main():
         out["fp64_flops_per_env_step_issued"] = f64 * per_env  # (2 FMA + ADD + MUL) x 64 lanes / env
         out["fp64_trans_per_env_step"] = mix["TRANS_F64"] * per_env
         if "SQ_INSTS_VALU_FLOPS_FP64" in med:
-            # the hardware's own flop counter (exec-masked lanes)
-            out["fp64_flops_per_env_step_counter"] = med["SQ_INSTS_VALU_FLOPS_FP64"] * SIMDS / a.envs
+            # the hardware's own fp64 flop counter counts per wave-instruction (FMA = 2), like the
+            # SQ_INSTS_VALU_* classes above, not per lane: x 64 lanes per env-step, it agrees with the
+            # instruction-derived figure (round 4 printed it without the x 64: "123")
+            out["fp64_flops_per_env_step_counter"] = med["SQ_INSTS_VALU_FLOPS_FP64"] * per_env
         out["salu_per_simd"] = med.get("SQ_INSTS_SALU")
         out["mix_sources"] = a.mix
     json.dump(out, open(a.out, "w"), indent=1)
