@@ -401,30 +401,39 @@ struct GenLds {
     ScnR s;                    // its device form (obstacle placement; the fresh curriculum's layout)
     uint32_t win[GEN_WIN];     // the stream's first GEN_WIN words
     double wx[D2D_MAX_WPS], wy[D2D_MAX_WPS], sa[D2D_MAX_WPS], ca[D2D_MAX_WPS], seg[D2D_MAX_WPS];
-    // obstacle placement (gen_obstacles_wave): the trial that starts at stream word w0 + 2 l, per lane l
-    double ox[64], oy[64], osz[64], px[64], py[64];
-    int32_t ook[64], ocons[64];
     int32_t wpos;            // the stream position after the obstacle calls
 };
 
 // generate_obstacles_around_path (gen_obstacles) with the wave: one rejection trial is a pure function
 // of the stream word it starts at (every draw consumes an even number of words), so lane l evaluates
-// the trial starting at word w0 + 2 l and lane 0 then walks the chain of trials the serial loop would
-// run (w -> w + words consumed), appending the accepted circles in order; a chain that leaves the 64
-// evaluated starts continues from a new w0.  Same trials, same order, same arithmetic as gen_obstacles.
+// the trial starting at word w0 + 2 l and the wave then walks the chain of trials the serial loop would
+// run (w -> w + words consumed) in scalar registers, reading each visited trial from its lane, and
+// appends the accepted circles in order; a chain that leaves the 64 evaluated starts continues from
+// a new w0.  Same trials, same order, same arithmetic as gen_obstacles.
 // then_on_path: the reference's next call, generate_obstacles_around_path(1, mean 0, std 0, on_path)
 // (stage 5), is folded in.  Its trial at a word consumes the same draws as this call's trial there and
 // is always accepted (on the path: the circle sits at the trial's path point), so once this call's
 // chain ends at word w, the next call's one obstacle is the trial evaluated at w -- no second round of
 // trials (unless w left the evaluated window).  Same trials, same order as the two separate calls.
+// lane t's value as a wave-uniform scalar (v_readlane: t uniform)
+__device__ __forceinline__ int gen_rl(int v, int t) { return __builtin_amdgcn_readlane(v, t); }
+__device__ __forceinline__ double gen_rl(double v, int t) {
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), t),
+                            __builtin_amdgcn_readlane(__double2loint(v), t));
+}
 __device__ inline void gen_obstacles_wave(GenLds& G, uint64_t seed, uint32_t gid, uint32_t key, double n, double mean,
                                           double std, bool on_path, int lane, bool then_on_path = false) {
     d2d_scn& s = G.a;
     const double L = s.us[s.n_wps - 1];
-    int num = 0, tries = 0, w = G.wpos;
-    int phase = 0;  // (lane 0) 0: this call's chain, 1: the folded on-path call, 2: done
-    bool more = true;
-    while (more) {  // (wave-uniform: the walk below runs on lane 0, its state goes through LDS)
+    // the walk's state is wave-uniform (scalar registers) and reads the trials' results from the lanes
+    // that evaluated them (v_readlane): no LDS round trip per visited trial (round 4 kept the trials in
+    // LDS and walked them on lane 0: ~2 dependent LDS reads per trial on the generator's serial chain)
+    int num = 0, tries = 0, w = __builtin_amdgcn_readfirstlane(G.wpos);
+    int nc = __builtin_amdgcn_readfirstlane(s.n_circles);
+    int phase = 0;  // 0: this call's chain, 1: the folded on-path call, 2: done
+    while (phase != 2) {
+        double tox, toy, tpx, tpy, tsz;
+        int tok, tcons;
         {
             GenStream R;
             R.init(G.win, seed, gid, key, w + 2 * lane);
@@ -439,60 +448,59 @@ __device__ inline void gen_obstacles_wave(GenLds& G, uint64_t seed, uint32_t gid
             const double size = R.uniform(10.0, 50.0);
             const double dx = ox - x, dy = oy - y;
             const double off = sqrt(dx * dx + dy * dy);
-            const bool ok = on_path || off > size + 10.0;
-            G.ox[lane] = on_path ? x : ox;
-            G.oy[lane] = on_path ? y : oy;
-            G.px[lane] = x;
-            G.py[lane] = y;
-            G.osz[lane] = size;
-            G.ook[lane] = ok ? 1 : 0;
-            G.ocons[lane] = R.pos - (w + 2 * lane);
+            tok = (on_path || off > size + 10.0) ? 1 : 0;
+            tox = on_path ? x : ox;
+            toy = on_path ? y : oy;
+            tpx = x;
+            tpy = y;
+            tsz = size;
+            tcons = R.pos - (w + 2 * lane);
         }
-        wave_sync();
-        if (lane == 0) {
-            const int w0 = w;
-            if (phase == 0) {
-                while ((double)num < n && s.n_circles < D2D_MAX_CIRCLES && tries < 4096 && w < w0 + 128) {
-                    const int t = (w - w0) >> 1;
-                    ++tries;
-                    if (G.ook[t]) {
-                        s.cx[s.n_circles] = G.ox[t];
-                        s.cy[s.n_circles] = G.oy[t];
-                        s.cr[s.n_circles] = G.osz[t];
-                        s.n_circles += 1;
-                        ++num;
+        const int w0 = w;
+        if (phase == 0) {
+            while ((double)num < n && nc < D2D_MAX_CIRCLES && tries < 4096 && w < w0 + 128) {
+                const int t = (w - w0) >> 1;
+                ++tries;
+                if (gen_rl(tok, t)) {
+                    const double cx = gen_rl(tox, t), cy = gen_rl(toy, t), cr = gen_rl(tsz, t);
+                    if (lane == 0) {
+                        s.cx[nc] = cx;
+                        s.cy[nc] = cy;
+                        s.cr[nc] = cr;
                     }
-                    w += G.ocons[t];
+                    nc += 1;
+                    ++num;
                 }
-                if (!((double)num < n && s.n_circles < D2D_MAX_CIRCLES && tries < 4096)) {
-                    phase = then_on_path ? 1 : 2;
-                    num = 0;
-                    tries = 0;
-                }
+                w += gen_rl(tcons, t);
             }
-            if (phase == 1) {
-                // generate_obstacles_around_path(1.0, 0.0, 0.0, on_path=True): one trial, accepted
-                if (s.n_circles >= D2D_MAX_CIRCLES) {
-                    phase = 2;
-                } else if (w < w0 + 128) {
-                    const int t = (w - w0) >> 1;
-                    s.cx[s.n_circles] = G.px[t];
-                    s.cy[s.n_circles] = G.py[t];
-                    s.cr[s.n_circles] = G.osz[t];
-                    s.n_circles += 1;
-                    w += G.ocons[t];
-                    phase = 2;
-                }
+            if (!((double)num < n && nc < D2D_MAX_CIRCLES && tries < 4096)) {
+                phase = then_on_path ? 1 : 2;
+                num = 0;
+                tries = 0;
             }
-            G.ook[0] = (phase != 2) ? 1 : 0;
-            G.ocons[0] = w;
         }
-        wave_sync();
-        more = G.ook[0] != 0;
-        w = G.ocons[0];
-        wave_sync();  // (G.ook / G.ocons are rewritten by the next round)
+        if (phase == 1) {
+            // generate_obstacles_around_path(1.0, 0.0, 0.0, on_path=True): one trial, accepted
+            if (nc >= D2D_MAX_CIRCLES) {
+                phase = 2;
+            } else if (w < w0 + 128) {
+                const int t = (w - w0) >> 1;
+                const double cx = gen_rl(tpx, t), cy = gen_rl(tpy, t), cr = gen_rl(tsz, t);
+                if (lane == 0) {
+                    s.cx[nc] = cx;
+                    s.cy[nc] = cy;
+                    s.cr[nc] = cr;
+                }
+                nc += 1;
+                w += gen_rl(tcons, t);
+                phase = 2;
+            }
+        }
     }
-    if (lane == 0) G.wpos = w;
+    if (lane == 0) {
+        s.n_circles = nc;
+        G.wpos = w;
+    }
     wave_sync();
 }
 
