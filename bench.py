@@ -417,6 +417,14 @@ def main():
                     "note": "flops = (2 FMA + ADD + MUL) f64 wave-instructions x 64 lanes per env-step "
                             "(issued lanes); the kernel is bound by VALU issue, of which fp64 arithmetic "
                             "is the mix_frac share"}
+                if v.get("valu_lane_util"):
+                    # the same over active lanes only (SQ_THREAD_CYCLES_VALU / 64 x SQ_ACTIVE_INST_VALU):
+                    # the Brent continuation issues with few lanes active
+                    ua = float(v["valu_lane_util"])
+                    line["roofline"]["fp64"].update({
+                        "valu_lane_util": ua, "achieved_active_lanes": tfs * ua,
+                        "frac_active_lanes": tfs * ua / FP64_PEAK_TFS,
+                        "flops_per_env_step_active_est": v.get("fp64_flops_per_env_step_active_est")})
         if args.scenario == "curriculum":
             line["config"]["workload"] = (f"fresh training curriculum (a new device-generated scenario per episode, "
                                           f"stage from the device step clock), {n} envs per GPU, U(-1,1) f32 "

@@ -218,7 +218,17 @@ __device__ __forceinline__ double sqrt_nz(double x) {
 // NaN fix-up is a wave-uniform branch taken only when some lane needs it (a probe exactly on the
 // drone's position): one compare per distance instead of a compare and two selects.  The same
 // results as sqrt_nz bit for bit (d2d_selftest checks it against sqrt()).
+#ifndef D2D_FAST_EARLY
+#define D2D_FAST_EARLY 0  // A/B: 1 = the one-compare interval test decided from the bracket alone
+#endif
+#ifndef D2D_PAR_NOBRANCH
+#define D2D_PAR_NOBRANCH 0  // A/B: 1 = the parabolic step's division on every Brent step (no ballot branch)
+#endif
+#ifndef D2D_SQRT_SEL
+#define D2D_SQRT_SEL 0  // A/B: 1 = the fix-up by selects (sqrt_nz) in every distance
+#endif
 __device__ __forceinline__ double sqrt_dist(double x) {
+    if (D2D_SQRT_SEL) return sqrt_nz(x);
     double g = sqrt_refine(x);
     if (__builtin_expect(__ballot(__builtin_amdgcn_class(x, 0x260)) != 0ull, 0)) {
         asm volatile("" ::: "memory");  // keeps the branch (no if-conversion into selects)
@@ -514,7 +524,7 @@ __device__ __forceinline__ void brent_step(const S& s, const PathK& K, double px
     // only used when `par` holds: then q > 0 and |p / q| < |e| / 2, a normal quotient.  Skipped
     // when no lane of the wave takes the parabolic step (the golden tails of long searches)
     double rat_p = 0.0;
-    if (__ballot(par) != 0ull) {
+    if (D2D_PAR_NOBRANCH || __ballot(par) != 0ull) {
         rat_p = div_normal(p + 0.0, q);
         const double xp = xf + rat_p;
         // tol1 * (np.sign(d) + (d == 0)) for d = xm - xf: a, b and xf are finite (the initial
@@ -536,8 +546,10 @@ __device__ __forceinline__ void brent_step(const S& s, const PathK& K, double px
     // |q| or tol1 times a nonzero sign, so copysign gives the same -mx / +mx)
     const double x = xf + copysign(mx, rat);
     BST(1, x);
-    // knot interval of x: one compare once the bracket spans <= 2 intervals (wave-uniform choice)
-    const bool fast = (x >= a) & (x <= b) & (B.ib <= B.ia + 1);
+    // knot interval of x: one compare once the bracket spans <= 2 intervals (wave-uniform choice).
+    // (D2D_FAST_EARLY: the bracket test alone, known from the state at the step's start; x is in
+    // [a, b] on every step -- see brent_x_in_bracket in the oracle)
+    const bool fast = D2D_FAST_EARLY ? (B.ib <= B.ia + 1) : ((x >= a) & (x <= b) & (B.ib <= B.ia + 1));
     int ix;
     if (__ballot(!fast) == 0ull) {
         ix = min(B.ia + ((x <= ka) ? 0 : 1), K.nw - 1);

@@ -304,12 +304,13 @@ __device__ __forceinline__ int next_scenario(const StepArgs& a, int j, uint32_t 
 struct K1Shared {
     double cas[6][EPB];       // W1 -> W0, W2: CAStatic (d, os, oc, lpa, lca, rr)
     int scn[EPB];             // scenario index per env
-    uint32_t cause[EPB];      // W0 -> W1, W2, W3: end cause (0: the env keeps running)
-    uint32_t cvalid[EPB];     // W0 -> W1, W3: the env's reset-cache entry is ready
+    uint8_t cause[EPB];       // W0 -> W1, W2, W3: end cause (0: the env keeps running)
+    uint8_t cvalid[EPB];      // W0 -> W1, W3: the env's reset-cache entry is ready
     uint32_t pflags[EPB];     // W3 -> W2: first differing step of the second half of the table re-check;
                               // then W2 -> W0: LA-lock bit after the path role
     uint32_t ep[EPB];         // W0 -> W1, W3: episode counter (the state's copy changes at a reset)
     double sina[EPB];         // W0 -> W2: sin of the post-step frame angle (AA reward)
+    uint32_t w0t[EPB], w0fl[EPB];  // W0 -> W0: the step counter t and the flags, for after the joint sweep
     uint32_t f_done, f_ca, f_gs, f_rp, f_ver, f_ver1;
     double pe[2][EPB];        // W3 -> W0: path_err, total_reward (prefetched for the epilogue)
     double acc[D2D_NSTATS][EPB];  // W3 -> W0: episode accumulators of envs that end (prefetched)
@@ -325,6 +326,13 @@ struct K1Shared {
     } u;
 };
 
+// the lane index by instructions the compiler cannot merge with threadIdx.x, so that a wave can
+// drop the index across a register-bound region and recompute it after
+__device__ __forceinline__ int lane_fresh() {
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
 __device__ __forceinline__ void flag_raise(uint32_t& f) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     if ((threadIdx.x & 63) == 0) *(volatile LdsU32*)&f = 1u;
@@ -447,9 +455,11 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const SC* scns, const
             const int32_t ep = fld(a.ist, D2D_I_EPISODE, n, i);
             const bool cv = done && auto_reset && ((D2D_ABL & 16) != 0 || a.rc_tag[rc_entry(a, i, (uint32_t)ep)] == ep);
             sh.ep[lane] = (uint32_t)ep;
-            sh.cause[lane] = (uint32_t)cause;
+            sh.cause[lane] = (uint8_t)cause;
             sh.sina[lane] = sn[0];
             sh.cvalid[lane] = cv ? 1u : 0u;
+            sh.w0t[lane] = (uint32_t)t;
+            sh.w0fl[lane] = flags;
             // positions and angles are final now (the sweep changes velocities only); envs that
             // auto-reset get their spawn state from W3 instead
             if (!(done && auto_reset)) {
@@ -468,63 +478,76 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const SC* scns, const
             double vel[9] = {B[0].vx, B[0].vy, B[0].w, B[1].vx, B[1].vy, B[1].w, B[2].vx, B[2].vy, B[2].w};
             phys_velocities<true>(A, pos, a.damping_dt, fx, fy, tq, vel, j, &sh.u.g.jb[0][lane], EPB,
                                   &sh.u.g.arms[0][lane]);
+            // the lane index, t, flags and the end cause are re-read from LDS or recomputed from here
+            // on (kept live across the sweep they were spilled to scratch: 40 B per lane each way)
+            asm volatile("" ::: "memory");
+            const int ln = lane_fresh(), iw = e0 + ln;
+            const uint32_t cw = sh.cause[ln];
+            cause = (int)cw;
+            done = cw != 0u;
+            t = (int)sh.w0t[ln];
+            flags = sh.w0fl[ln];
             if (!(done && auto_reset)) {
 #pragma unroll
             for (int b = 0; b < 3; ++b) {
-                fld(a.st, 6 * b + 3, n, i) = vel[3 * b + 0];
-                fld(a.st, 6 * b + 4, n, i) = vel[3 * b + 1];
-                fld(a.st, 6 * b + 5, n, i) = vel[3 * b + 2];
+                fld(a.st, 6 * b + 3, n, iw) = vel[3 * b + 0];
+                fld(a.st, 6 * b + 4, n, iw) = vel[3 * b + 1];
+                fld(a.st, 6 * b + 5, n, iw) = vel[3 * b + 2];
             }
 #pragma unroll
-            for (int k = 0; k < 12; ++k) fld(a.st, D2D_S_J + k, n, i) = j[k];
+            for (int k = 0; k < 12; ++k) fld(a.st, D2D_S_J + k, n, iw) = j[k];
             }
-            F0 = Body{B[0].px, B[0].py, B[0].a, vel[0], vel[1], vel[2]};
+            F0 = Body{0.0, 0.0, B[0].a, vel[0], vel[1], vel[2]};
         }
         flag_raise(sh.f_gs);
         STAMP(4);
+        const int ln = lane_fresh(), iw = e0 + ln, iew = GRP ? ie : iw;
+        const bool vw = gvalid && (GRP ? iew >= 0 : iw < a.n);
         // velocity part of the observation (obs 0-2, 17-18) into the tile / terminal obs
-        if (valid) {
-            sensor_vel(F0, sn[0], cs[0], ov);
+        if (vw) {
+            float* const orw = &sh.u.p.obs[ln * D2D_OBS_DIM];
+            float* const trw = a.tobs ? a.tobs + (size_t)iew * D2D_OBS_DIM : nullptr;
+            sensor_vel(F0, sh.sina[ln], cs[0], ov);
             if (!(done && auto_reset)) {
-                orow[0] = (float)ov[0];
-                orow[1] = (float)ov[1];
-                orow[2] = (float)ov[2];
-                orow[17] = (float)ov[17];
-                orow[18] = (float)ov[18];
+                orw[0] = (float)ov[0];
+                orw[1] = (float)ov[1];
+                orw[2] = (float)ov[2];
+                orw[17] = (float)ov[17];
+                orw[18] = (float)ov[18];
             }
-            if (done && trow) {
-                trow[0] = (float)ov[0];
-                trow[1] = (float)ov[1];
-                trow[2] = (float)ov[2];
-                trow[17] = (float)ov[17];
-                trow[18] = (float)ov[18];
+            if (done && trw) {
+                trw[0] = (float)ov[0];
+                trw[1] = (float)ov[1];
+                trw[2] = (float)ov[2];
+                trw[17] = (float)ov[17];
+                trw[18] = (float)ov[18];
             }
         }
         // velocity part of the reward (speed, velocity angle, CA total), for W2
         flag_wait(sh.f_ca);
         STAMP(5);
-        if (valid) {
+        if (vw) {
             CAStatic C;
-            C.d = sh.cas[0][lane];
-            C.os = sh.cas[1][lane];
-            C.oc = sh.cas[2][lane];
-            C.lpa = sh.cas[3][lane];
-            C.lca = sh.cas[4][lane];
-            C.rr = sh.cas[5][lane];
+            C.d = sh.cas[0][ln];
+            C.os = sh.cas[1][ln];
+            C.oc = sh.cas[2][ln];
+            C.lpa = sh.cas[3][ln];
+            C.lca = sh.cas[4][ln];
+            C.rr = sh.cas[5][ln];
             RV = reward_vel(a.cfg, ov, C);
             dclose = C.d;
         }
         // the reward: W2's position / path terms (usually long ready: the physics chain ends last)
         flag_wait(sh.f_rp);
-        if (valid) {
+        if (vw) {
             RewardPos RP{};
-            RP.aa = sh.u.p.post[4][lane];
-            RP.coll = sh.u.p.post[5][lane];
-            RP.reach = sh.u.p.post[6][lane];
+            RP.aa = sh.u.p.post[4][ln];
+            RP.coll = sh.u.p.post[5][ln];
+            RP.reach = sh.u.p.post[6][ln];
             RewardPath RQ{};
-            RQ.ls = sh.u.p.post[0][lane];
-            RQ.lc = sh.u.p.post[1][lane];
-            RQ.pa = sh.u.p.post[2][lane];
+            RQ.ls = sh.u.p.post[0][ln];
+            RQ.lc = sh.u.p.post[1][ln];
+            RQ.pa = sh.u.p.post[2][ln];
             const RewardSum Q = reward_sum(a.cfg, RP, RV, RQ);
             rew_sum = Q.reward;
             rew_pp = Q.pp;
@@ -797,7 +820,10 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const SC* scns, const
         }
         for (int k = k0 + qt; k < words; k += K1_THREADS) dst[k] = sh.u.p.obs[k];
     }
-    if (wave == 0 && valid) {
+    const int lne = lane_fresh(), ile = e0 + lne, iee = GRP ? ie : ile;
+    const bool vle = gvalid && (GRP ? iee >= 0 : ile < a.n);
+    if (wave == 0 && vle) {
+        const int lane = lne, i = ile, ie = iee;
         path_err = sh.pe[0][lane];
         tot_rew = sh.pe[1][lane];
         flags = (flags & ~D2D_FLAG_LA_LOCK) | sh.pflags[lane];

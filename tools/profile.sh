@@ -32,6 +32,8 @@ step pmc_sq 600 rocprofv3 $KR -T --output-format csv -d "$OUT/pmc_sq" -o sq --pm
 # counters: the fp64 co-roofline of the bench line (tools/valu.py --mix)
 step pmc_mix 600 rocprofv3 $KR -T --output-format csv -d "$OUT/pmc_mix" -o mix --pmc SQ_INSTS_VALU SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT -- $B --eager --steps 40 --warmup 300
 step pmc_mix2 600 rocprofv3 $KR -T --output-format csv -d "$OUT/pmc_mix2" -o mix2 --pmc SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_FLOPS_FP64_TRANS SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_SALU SQ_WAVES -- $B --eager --steps 40 --warmup 300
+# VALU lane utilisation (thread-cycles over 64 x VALU-issue cycles): the fp64 flops over active lanes
+step pmc_util 600 rocprofv3 $KR -T --output-format csv -d "$OUT/pmc_util" -o util --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAVES -- $B --eager --steps 40 --warmup 300
 step pmc_clk 600 rocprofv3 $KR -T --output-format csv -d "$OUT/pmc_clk" -o clk --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES -- $B --eager --steps 40 --warmup 300
 python3 "$R/tools/traffic.py" "$OUT" --out "$OUT/traffic.json"
-python3 "$R/tools/valu.py" "$OUT"/pmc_sq/sq_counter_collection.csv --mix "$OUT"/pmc_mix/mix_counter_collection.csv "$OUT"/pmc_mix2/mix2_counter_collection.csv --out "$OUT/valu.json"
+python3 "$R/tools/valu.py" "$OUT"/pmc_sq/sq_counter_collection.csv --mix "$OUT"/pmc_mix/mix_counter_collection.csv "$OUT"/pmc_mix2/mix2_counter_collection.csv --util "$OUT"/pmc_util/util_counter_collection.csv --out "$OUT/valu.json"

@@ -38,11 +38,36 @@ def per_step(rows):
     return (step_b + fill_b) * 1024.0 / max(steps, 1), step_b * 1024.0 / max(steps, 1), steps
 
 
+def per_buffer(fd, read_meas, write_meas):
+    """Bytes per env-step by buffer: the 650 B of the roofline plus what the
+    auto-reset adds at fd episodes finished per env-step, against the measured read / write bytes."""
+    rd = {"state (32 fp64 SoA fields)": 256.0, "t + flags (int32)": 8.0, "action (2 f32)": 8.0,
+          "episode counter (int32, every step)": 4.0,
+          "finished episodes: reset-cache tag + accumulators (4 + 64 B)": 68.0 * fd,
+          "fill kernel: cache tags / episode counters, every 16th step (8 B / 16)": 0.5}
+    wr = {"state (32 fp64 SoA fields; the spawn state for envs that reset)": 256.0, "t + flags": 8.0,
+          "obs row (27 f32)": 108.0, "reward (f32)": 4.0, "terminated + truncated (u8)": 2.0,
+          "finished episodes: episode counter + terminal obs row + 7 accumulators (4 + 108 + 56 B)": 168.0 * fd,
+          "fill kernel: reset-cache obs row + flags + tag (108 + 4 + 4 B) per finished episode": 116.0 * fd}
+    r_alg, w_alg = sum(rd.values()), sum(wr.values())
+    return {"done_frac": fd, "read": rd, "write": wr, "read_attributed": r_alg, "write_attributed": w_alg,
+            "read_measured": read_meas, "write_measured": write_meas,
+            "unattributed": (read_meas - r_alg) + (write_meas - w_alg),
+            "note": "650 B algorithmic (272 read + 378 write) + the auto-reset's per-episode bytes at the bench's "
+                    "episode rate; measured = FETCH_SIZE x 2 / WRITE_SIZE per env-step. The joint sweep's "
+                    "scratch spill (40 B each way, round 5 until the LDS stash) is gone"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("prof_dir")
     ap.add_argument("--out", default=None)
     ap.add_argument("--envs", type=int, default=65536)
+    ap.add_argument("--done-frac", type=float, default=None,
+                    help="episodes finished per env-step (the bench line's episodes: finished / sum_len); "
+                         "adds the per-buffer table")
+    ap.add_argument("--source", default=None, help="the committed PMC CSVs the figures come from")
+    ap.add_argument("--commit", default=None, help="the commit the profile was taken on")
     a = ap.parse_args()
     fetch = counter(os.path.join(a.prof_dir, "pmc_fetch"), "FETCH_SIZE")
     write = counter(os.path.join(a.prof_dir, "pmc_write"), "WRITE_SIZE")
@@ -56,6 +81,12 @@ def main():
            "step_kernel_only_bytes": f_step + w_step, "step_launches": [nf, nw],
            "note": "per step = (step + fill kernel bytes) / step launches over the second half of the "
                    "profiled launches; FETCH_SIZE x2 (gfx950)"}
+    if a.done_frac is not None:
+        res["per_buffer"] = per_buffer(a.done_frac, f / a.envs, w / a.envs)
+    if a.source:
+        res["source"] = a.source
+    if a.commit:
+        res["commit"] = a.commit
     print(json.dumps(res, indent=1))
     if a.out:
         json.dump(res, open(a.out, "w"), indent=1)

@@ -40,6 +40,14 @@ __global__ __launch_bounds__(256) void rd_f64x2(const double2* src, int F2, int 
     }
     out[i] = s;
 }
+// int32 fields SoA read (K1's t / flags / episode counter loads)
+__global__ __launch_bounds__(256) void rd_i32_soa(const int* src, int F, int n, int* out) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    int s = 0;
+    for (int f = 0; f < F; ++f) s += src[(size_t)f * n + i];
+    out[i] = s;
+}
 // F fp64 fields written SoA (K1's state stores)
 __global__ __launch_bounds__(256) void wr_f64_soa(double* dst, int F, int n) {
     const int i = blockIdx.x * 256 + threadIdx.x;
@@ -84,6 +92,10 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&rew, sizeof(float) * n));
     CK(hipMalloc(&obs, sizeof(float) * 27 * n));
     CK(hipMalloc(&u8, n));
+    int *ist3, *iout;
+    CK(hipMalloc(&ist3, sizeof(int) * 3 * n));
+    CK(hipMalloc(&iout, sizeof(int) * n));
+    CK(hipMemset(ist3, 0, sizeof(int) * 3 * n));
     CK(hipMemset(st, 0, sizeof(double) * F * n));
     const dim3 g((n + 255) / 256), b(256);
     for (int rep = 0; rep < 5; ++rep) {
@@ -91,6 +103,7 @@ int main(int argc, char** argv) {
         hipLaunchKernelGGL(rd_f64x2, g, b, 0, 0, (const double2*)st, F / 2, n, out);
         hipLaunchKernelGGL(wr_f64_soa, g, b, 0, 0, st, F, n);
         hipLaunchKernelGGL(wr_i32_soa, g, b, 0, 0, ist, 2, n);
+        hipLaunchKernelGGL(rd_i32_soa, g, b, 0, 0, ist3, 3, n, iout);
         hipLaunchKernelGGL(wr_f32, g, b, 0, 0, rew, n);
         hipLaunchKernelGGL(wr_u8, g, b, 0, 0, u8, n);
         hipLaunchKernelGGL(wr_obs_tile, dim3(n / 64), b, 0, 0, (float4*)obs, n);
@@ -98,9 +111,10 @@ int main(int argc, char** argv) {
     CK(hipDeviceSynchronize());
     printf("{\"envs\": %d, \"rd_f64_soa\": {\"read\": %zu, \"write\": %zu}, \"rd_f64x2\": {\"read\": %zu, \"write\": %zu}, "
            "\"wr_f64_soa\": {\"write\": %zu}, \"wr_i32_soa\": {\"write\": %zu}, \"wr_f32\": {\"write\": %zu}, "
-           "\"wr_u8\": {\"write\": %zu}, \"wr_obs_tile\": {\"write\": %zu}}\n",
+           "\"wr_u8\": {\"write\": %zu}, \"wr_obs_tile\": {\"write\": %zu}, "
+           "\"rd_i32_soa\": {\"read\": %zu, \"write\": %zu}}\n",
            n, sizeof(double) * F * n, sizeof(double) * n, sizeof(double) * F * n, sizeof(double) * n,
            sizeof(double) * F * n, sizeof(int) * 2 * (size_t)n, sizeof(float) * (size_t)n, (size_t)n,
-           sizeof(float) * 27 * (size_t)n);
+           sizeof(float) * 27 * (size_t)n, sizeof(int) * 3 * (size_t)n, sizeof(int) * (size_t)n);
     return 0;
 }

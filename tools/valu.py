@@ -24,14 +24,17 @@ def main():
     ap.add_argument("--out", required=True)
     ap.add_argument("--mix", nargs="*", default=[],
                     help="counter CSVs of the VALU-mix passes (tools/profile.sh pmc_mix, pmc_mix2)")
+    ap.add_argument("--util", default=None,
+                    help="counter CSV of the lane-utilisation pass (tools/profile.sh pmc_util)")
     ap.add_argument("--envs", type=int, default=65536, help="envs per launch (per-env-step figures)")
     ap.add_argument("--commit", default=None, help="the commit the profile was taken on")
     a = ap.parse_args()
     per = defaultdict(lambda: defaultdict(float))
-    for f in [a.csv, *a.mix]:
+    util = defaultdict(lambda: defaultdict(float))
+    for f, dst in [(f, per) for f in [a.csv, *a.mix]] + ([(a.util, util)] if a.util else []):
         for r in csv.DictReader(open(f)):
             if a.kernel in r["Kernel_Name"]:
-                per[r["Counter_Name"]][(f, r["Dispatch_Id"])] += float(r["Counter_Value"])
+                dst[r["Counter_Name"]][(f, r["Dispatch_Id"])] += float(r["Counter_Value"])
     med = {k: statistics.median(v.values()) / SIMDS for k, v in per.items()}
     # SQ_WAVE_CYCLES and SQ_ACTIVE_INST_VALU count in units of 4 cycles (quad-cycles); SQ_WAVE_CYCLES
     # sums the lifetimes of the SIMD's waves
@@ -63,6 +66,17 @@ def main():
             # instruction-derived figure (round 4 printed it without the x 64: "123")
             out["fp64_flops_per_env_step_counter"] = med["SQ_INSTS_VALU_FLOPS_FP64"] * per_env
         out["salu_per_simd"] = med.get("SQ_INSTS_SALU")
+        if util:
+            # lanes a VALU instruction actually computes for (exec mask): thread-cycles over 64 x the
+            # VALU-issue cycles of the same pass (rocprofiler's VALUUtilization).  The Brent
+            # continuation runs with few active lanes, so the issued-lane fp64 figure overstates the
+            # useful work; x this fraction estimates the active-lane figure (assuming the fp64
+            # instructions' lane occupancy is the VALU average)
+            um = {k: statistics.median(v.values()) for k, v in util.items()}
+            frac = um["SQ_THREAD_CYCLES_VALU"] / (um["SQ_ACTIVE_INST_VALU"] * 64.0)
+            out["valu_lane_util"] = frac
+            out["fp64_flops_per_env_step_active_est"] = out["fp64_flops_per_env_step_issued"] * frac
+            out["util_source"] = a.util
         out["mix_sources"] = a.mix
     json.dump(out, open(a.out, "w"), indent=1)
     print(json.dumps(out, indent=1))
