@@ -221,12 +221,6 @@ __device__ __forceinline__ double sqrt_nz(double x) {
 #ifndef D2D_FAST_EARLY
 #define D2D_FAST_EARLY 1  // the one-compare interval test decided from the bracket alone (brent_step)
 #endif
-#ifndef D2D_OPEN_SPEC
-#define D2D_OPEN_SPEC 0  // A/B: 1 = the next loop condition computed for both decisions during the probe
-#endif
-#ifndef D2D_GOLD_FIRST
-#define D2D_GOLD_FIRST 0  // A/B: 1 = the golden candidate computed ahead of the parabolic branch
-#endif
 #ifndef D2D_PAR_NOBRANCH
 #define D2D_PAR_NOBRANCH 0  // A/B: 1 = the parabolic step's division on every Brent step (no ballot branch)
 #endif
@@ -470,7 +464,6 @@ struct Brent {
     double ka, kxf;
     int num, ia, ib, ixf;
     int rci;  // record cache (D2D_RCACHE, global-memory tables): interval whose record the lane holds in LDS, -1: none
-    bool open;  // D2D_OPEN_SPEC: the loop condition of the state after the last brent_step
 };
 constexpr double BR_SQRT_EPS = 1.4832396974191326e-08;  // sqrt(2.2e-16)
 constexpr double BR_GOLDEN = 0.3819660112501051;        // 0.5*(3.0 - sqrt(5.0))
@@ -503,13 +496,6 @@ __device__ __forceinline__ bool brent_open(const Brent& B) {
     return fabs(B.xf - xm) > (tol2 - 0.5 * (B.b - B.a));
 }
 __device__ __forceinline__ bool brent_active(const Brent& B) { return brent_open(B) & (B.num < 500); }
-// the same condition for a bracket [a, b] and best point xf given separately
-__device__ __forceinline__ bool brent_open3(double a, double b, double xf) {
-    const double xm = 0.5 * (a + b);
-    const double tol1 = BR_SQRT_EPS * fabs(xf) + BR_XATOL3;
-    const double tol2 = 2.0 * tol1;
-    return fabs(xf - xm) > (tol2 - 0.5 * (b - a));
-}
 // KN: the knot scan reads the lane's knots staged in LDS at kn (global-memory tables, closest_u)
 template <bool KN = false, class S>
 __device__ __forceinline__ void brent_step(const S& s, const PathK& K, double px, double py, Brent& B,
@@ -537,32 +523,18 @@ __device__ __forceinline__ void brent_step(const S& s, const PathK& K, double px
     const bool par = (fabs(B.e) > tol1) & (fabs(p) < fabs(0.5 * q * B.e)) & (p > q * (a - xf)) & (p < q * (b - xf));
     // only used when `par` holds: then q > 0 and |p / q| < |e| / 2, a normal quotient.  Skipped
     // when no lane of the wave takes the parabolic step (the golden tails of long searches)
-#if D2D_GOLD_FIRST
-    // golden-section candidate, and the parabolic step's fallback tol1 * (np.sign(d) + (d == 0)) for
-    // d = xm - xf (a, b and xf are finite, so d is not NaN: -tol1 for d < 0, else +tol1), ahead of the
-    // branch below: independent work between the ballot's compare and the branch that reads it
-    const double e_g = (xf >= xm) ? a - xf : b - xf;
-    const double rat_g = BR_GOLDEN * e_g;
-    const double tol_d = (xm - xf < 0.0) ? -tol1 : tol1;
-#endif
     double rat_p = 0.0;
     if (D2D_PAR_NOBRANCH || __ballot(par) != 0ull) {
         rat_p = div_normal(p + 0.0, q);
         const double xp = xf + rat_p;
-#if D2D_GOLD_FIRST
-        rat_p = (((xp - a) < tol2) | ((b - xp) < tol2)) ? tol_d : rat_p;
-#else
         // tol1 * (np.sign(d) + (d == 0)) for d = xm - xf: a, b and xf are finite (the initial
         // bracket and finite steps), so d is not NaN and the product is -tol1 for d < 0, else +tol1
         const double d = xm - xf;
         rat_p = (((xp - a) < tol2) | ((b - xp) < tol2)) ? ((d < 0.0) ? -tol1 : tol1) : rat_p;
-#endif
     }
-#if !D2D_GOLD_FIRST
     // golden-section candidate
     const double e_g = (xf >= xm) ? a - xf : b - xf;
     const double rat_g = BR_GOLDEN * e_g;
-#endif
     B.e = par ? B.rat : e_g;
     const double rat = par ? rat_p : rat_g;
     B.rat = rat;
@@ -574,14 +546,6 @@ __device__ __forceinline__ void brent_step(const S& s, const PathK& K, double px
     // |q| or tol1 times a nonzero sign, so copysign gives the same -mx / +mx)
     const double x = xf + copysign(mx, rat);
     BST(1, x);
-#if D2D_OPEN_SPEC
-    // the next step's loop condition for both outcomes of the coming decision, while the probe is
-    // evaluated: better (xf' = x; a' = xf if x >= xf, else b' = xf) or not (xf' = xf; b' = x if
-    // x >= xf, else a' = x) -- the operands the update below selects, so the same bits
-    const bool gex = x >= xf;
-    const bool open_le = brent_open3(gex ? xf : a, gex ? b : xf, x);
-    const bool open_gt = brent_open3(gex ? a : x, gex ? x : b, xf);
-#endif
     // knot interval of x: one compare once the bracket spans <= 2 intervals (wave-uniform choice).
     // x is always in [a, b], so the choice depends on the bracket alone -- known at the step's start,
     // which takes the branch off the step's dependency chain (a branch on a just-computed condition
@@ -683,9 +647,6 @@ __device__ __forceinline__ void brent_step(const S& s, const PathK& K, double px
     B.fnfc = nfnfc;
     B.xf = le ? x : xf;
     B.fx = le ? fu : fx;
-#if D2D_OPEN_SPEC
-    B.open = le ? open_le : open_gt;
-#endif
 #ifdef D2D_BSTAMP
     BST(4, B.fx);
     const uint64_t act = __ballot(1);
@@ -708,7 +669,7 @@ __device__ __forceinline__ void brent_run(const S& s, const PathK& K, double px,
                                           double* kn = nullptr) {
     constexpr int IT_FREE = 500 - (BT_K_MAX + 1);
     for (int it = 0;; ++it) {
-        bool act = (D2D_OPEN_SPEC && it > 0) ? B.open : brent_open(B);
+        bool act = brent_open(B);
         if (__builtin_expect(it >= IT_FREE, 0)) {
             asm volatile("" ::: "memory");  // a scalar branch, not a per-pass compare
             act = act & (B.num + it < 500);
