@@ -218,6 +218,9 @@ __device__ __forceinline__ double sqrt_nz(double x) {
 // NaN fix-up is a wave-uniform branch taken only when some lane needs it (a probe exactly on the
 // drone's position): one compare per distance instead of a compare and two selects.  The same
 // results as sqrt_nz bit for bit (d2d_selftest checks it against sqrt()).
+#ifndef D2D_ABL_FASTDIV
+#define D2D_ABL_FASTDIV 0  // timing ablation only (not exact): the parabolic step as p * rcp(q)
+#endif
 #ifndef D2D_FAST_EARLY
 #define D2D_FAST_EARLY 1  // the one-compare interval test decided from the bracket alone (brent_step)
 #endif
@@ -227,7 +230,11 @@ __device__ __forceinline__ double sqrt_nz(double x) {
 #ifndef D2D_SQRT_SEL
 #define D2D_SQRT_SEL 0  // A/B: 1 = the fix-up by selects (sqrt_nz) in every distance
 #endif
+#ifndef D2D_ABL_FASTSQRT
+#define D2D_ABL_FASTSQRT 0  // timing ablation only (not exact): v_sqrt_f64 alone for distances
+#endif
 __device__ __forceinline__ double sqrt_dist(double x) {
+    if (D2D_ABL_FASTSQRT) return __builtin_amdgcn_sqrt(x);
     if (D2D_SQRT_SEL) return sqrt_nz(x);
     double g = sqrt_refine(x);
     if (__builtin_expect(__ballot(__builtin_amdgcn_class(x, 0x260)) != 0ull, 0)) {
@@ -525,7 +532,7 @@ __device__ __forceinline__ void brent_step(const S& s, const PathK& K, double px
     // when no lane of the wave takes the parabolic step (the golden tails of long searches)
     double rat_p = 0.0;
     if (D2D_PAR_NOBRANCH || __ballot(par) != 0ull) {
-        rat_p = div_normal(p + 0.0, q);
+        rat_p = D2D_ABL_FASTDIV ? (p + 0.0) * __builtin_amdgcn_rcp(q) : div_normal(p + 0.0, q);
         const double xp = xf + rat_p;
         // tol1 * (np.sign(d) + (d == 0)) for d = xm - xf: a, b and xf are finite (the initial
         // bracket and finite steps), so d is not NaN and the product is -tol1 for d < 0, else +tol1
