@@ -29,7 +29,7 @@
 // bool conditions are combined with & / | on purpose (selects instead of short-circuit branches)
 #pragma clang diagnostic ignored "-Wbitwise-instead-of-logical"
 
-// Diagnostic-only ablation mask (tools/ablate.py builds separate timing-only libraries with it;
+// Diagnostic-only ablation mask (tools/variants.py builds separate timing-only libraries with it;
 // the product is always built with 0): 1 skip Brent, 2 skip sensing, 4 skip joint iterations,
 // 8 skip collision test, 16 skip the Brent continuation after the golden-march tables, 128 the fresh
 // curriculum generator skips the obstacles.
@@ -452,7 +452,7 @@ __device__ __forceinline__ double path_dist_n(const S& s, const PathK& K, double
                                               double& u1) {
     double x, y;
     path_eval_n(s, K, u, n, x, y, u1);
-    // (sqrt_nz measured slower here than the library sequence: tools/ubench_brent.py)
+    // (sqrt_nz measured slower here than the library sequence: tools/ubench_step.hip, D2D_SQRT_SEL)
     return norm2(x - px, y - py);
 }
 // get_closest_u (predef_path.py:226-248) = scipy fminbound(x1=-10, x2=L+10, xtol=1e-6, maxfun=500),
