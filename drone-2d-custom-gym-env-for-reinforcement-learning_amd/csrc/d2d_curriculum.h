@@ -166,6 +166,7 @@ __device__ inline void gen_gradient(const d2d_scn& s, double u, double& gx, doub
         gy = s.ya[last] * u * 2.0 + s.yb[last];
         return;
     }
+    // (a branch-free count of the knots below u measured equal in K5: the loop stays)
     int n = 0;
     while (n < nw - 1 && !(u <= s.us[n + 1])) ++n;
     const double du = s.us[n + 1] - s.us[n];
@@ -286,13 +287,19 @@ __device__ inline void gen_curriculum(const d2d_curriculum& c, double W, double 
 
 // ------------------------------------------------------------------ wave-cooperative generation (K5)
 // The same scenario as gen_curriculum, built by the 64 lanes of one wave in LDS: the stream's first
-// GEN_WIN words (64 Philox blocks, one per lane), the azimuths' sincos, the segment lengths, the 20
+// GEN_WIN words (Philox blocks, D2D_GEN_WIN_BLOCKS per lane), the azimuths' sincos, the segment lengths, the 20
 // QPMI2D 3 x 3 solves and the 16 interval records in parallel; the few truly sequential parts (the
 // waypoint and arc-length prefix sums, the obstacle rejection loop, which consumes a data-dependent
 // number of draws) on lane 0 reading the stream from LDS.  Every value is produced by the same
 // operations on the same operands as gen_curriculum (so the tables stay bit-identical to the CPU
 // oracle's o_gen_curriculum); only the order in which independent values are computed changes.
-constexpr int GEN_WIN = 256;   // stream words precomputed per item (corner + waypoints + ~25 obstacle tries)
+#ifndef D2D_GEN_WIN_BLOCKS
+#define D2D_GEN_WIN_BLOCKS 2  // Philox blocks per lane in the window (1: round 4's 256 words)
+#endif
+// stream words precomputed per item: corner + waypoints + the obstacle trials, which the wave evaluates
+// at 64 starts 4 words apart (gen_obstacles_wave) -- 512 words keep the first evaluation's trials
+// inside the window
+constexpr int GEN_WIN = 256 * D2D_GEN_WIN_BLOCKS;
 
 // LDS hand-off between the lanes of the one wave that runs the generator
 __device__ __forceinline__ void wave_sync() {
@@ -405,11 +412,14 @@ struct GenLds {
 };
 
 // generate_obstacles_around_path (gen_obstacles) with the wave: one rejection trial is a pure function
-// of the stream word it starts at (every draw consumes an even number of words), so lane l evaluates
-// the trial starting at word w0 + 2 l and the wave then walks the chain of trials the serial loop would
-// run (w -> w + words consumed) in scalar registers, reading each visited trial from its lane, and
-// appends the accepted circles in order; a chain that leaves the 64 evaluated starts continues from
-// a new w0.  Same trials, same order, same arithmetic as gen_obstacles.
+// of the stream word it starts at, and every trial consumes a multiple of 4 words (uniform 2 + the
+// polar normal 4 per attempt + uniform 2), so the chain's trials start at w0, w0 + 4 k, ...: lane l
+// evaluates the trial starting at word w0 + 4 l and the wave then walks the chain of trials the serial
+// loop would run (w -> w + words consumed) in scalar registers, reading each visited trial from its
+// lane, and appends the accepted circles in order; a chain that leaves the 64 evaluated starts
+// continues from a new w0.  Same trials, same order, same arithmetic as gen_obstacles.  (Starts every
+// 2 words, as in round 4, covered half the chain per evaluation: the stage-5 items with many
+// obstacles needed 2-3 evaluations and set K5's duration.)
 // then_on_path: the reference's next call, generate_obstacles_around_path(1, mean 0, std 0, on_path)
 // (stage 5), is folded in.  Its trial at a word consumes the same draws as this call's trial there and
 // is always accepted (on the path: the circle sits at the trial's path point), so once this call's
@@ -436,7 +446,7 @@ __device__ inline void gen_obstacles_wave(GenLds& G, uint64_t seed, uint32_t gid
         int tok, tcons;
         {
             GenStream R;
-            R.init(G.win, seed, gid, key, w + 2 * lane);
+            R.init(G.win, seed, gid, key, w + 4 * lane);
             const double u = R.uniform(0.20 * L, 0.90 * L);
             double gx, gy;
             gen_gradient(s, u, gx, gy);
@@ -454,12 +464,12 @@ __device__ inline void gen_obstacles_wave(GenLds& G, uint64_t seed, uint32_t gid
             tpx = x;
             tpy = y;
             tsz = size;
-            tcons = R.pos - (w + 2 * lane);
+            tcons = R.pos - (w + 4 * lane);
         }
         const int w0 = w;
         if (phase == 0) {
-            while ((double)num < n && nc < D2D_MAX_CIRCLES && tries < 4096 && w < w0 + 128) {
-                const int t = (w - w0) >> 1;
+            while ((double)num < n && nc < D2D_MAX_CIRCLES && tries < 4096 && w < w0 + 256) {
+                const int t = (w - w0) >> 2;
                 ++tries;
                 if (gen_rl(tok, t)) {
                     const double cx = gen_rl(tox, t), cy = gen_rl(toy, t), cr = gen_rl(tsz, t);
@@ -483,8 +493,8 @@ __device__ inline void gen_obstacles_wave(GenLds& G, uint64_t seed, uint32_t gid
             // generate_obstacles_around_path(1.0, 0.0, 0.0, on_path=True): one trial, accepted
             if (nc >= D2D_MAX_CIRCLES) {
                 phase = 2;
-            } else if (w < w0 + 128) {
-                const int t = (w - w0) >> 1;
+            } else if (w < w0 + 256) {
+                const int t = (w - w0) >> 2;
                 const double cx = gen_rl(tpx, t), cy = gen_rl(tpy, t), cr = gen_rl(tsz, t);
                 if (lane == 0) {
                     s.cx[nc] = cx;
@@ -523,10 +533,12 @@ __device__ inline int gen_path_wave(const d2d_curriculum& c, double W, double H,
                                     uint32_t key, GenLds& G, int lane, uint64_t* st = nullptr) {
     (void)st;
     GSTAMP(st, 0);
-    {
+#pragma unroll
+    for (int blk = 0; blk < D2D_GEN_WIN_BLOCKS; ++blk) {
         uint32_t o[4];
-        philox(gid, key, GEN_TAG + (uint32_t)lane, 0u, (uint32_t)seed, (uint32_t)(seed >> 32), o);
-        for (int k = 0; k < 4; ++k) G.win[4 * lane + k] = o[k];
+        const uint32_t b = (uint32_t)(64 * blk + lane);
+        philox(gid, key, GEN_TAG + b, 0u, (uint32_t)seed, (uint32_t)(seed >> 32), o);
+        for (int k = 0; k < 4; ++k) G.win[4 * b + k] = o[k];
     }
     wave_sync();
     GSTAMP(st, 1);
