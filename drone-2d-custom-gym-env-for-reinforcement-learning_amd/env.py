@@ -145,7 +145,9 @@ class Drone2dVecEnv:
         # episode (default: the faster build, a few ulp apart).  native_lib: an alternative build of
         # the same source (diagnostic A/B builds only).
         self.exact_trig = bool(exact_trig)
-        if exact_trig and native_lib is None:
+        if exact_trig:
+            if native_lib is not None:
+                raise ValueError("exact_trig selects the exact-trig library build; do not also pass native_lib")
             from ._native import EXACT_LIB_PATH
 
             native_lib = EXACT_LIB_PATH

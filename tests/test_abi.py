@@ -82,6 +82,21 @@ def test_hip_library_is_gfx950(d2):
     assert b"hipv4-amdgcn-amd-amdhsa--gfx950" in data  # the embedded code-object bundle id
 
 
+def test_exact_trig_library_exports_the_same_abi(d2):
+    """The exact-trig build (Drone2dVecEnv(exact_trig=True)) is the same source and ABI; asking for it
+    together with another library is refused before anything is loaded."""
+    import ctypes
+
+    from drone2d_amd import _build, _native
+
+    _build.build()
+    lib = ctypes.CDLL(_native.EXACT_LIB_PATH)
+    for f in header_functions():
+        assert hasattr(lib, f), f
+    with pytest.raises(ValueError):
+        d2.Drone2dVecEnv(4, device="cpu", exact_trig=True, native_lib=_native.LIB_PATH)
+
+
 def test_errors_without_device(hip_lib):
     """Argument validation happens before any device call."""
     from drone2d_amd import abi
