@@ -221,6 +221,9 @@ __device__ __forceinline__ double sqrt_nz(double x) {
 #ifndef D2D_ABL_FASTDIV
 #define D2D_ABL_FASTDIV 0  // timing ablation only (not exact): the parabolic step as p * rcp(q)
 #endif
+#ifndef D2D_TOP4_SKIP
+#define D2D_TOP4_SKIP 1  // sensing skips a circle no lane's top 4 takes (wave ballot; 0: A/B)
+#endif
 #ifndef D2D_FAST_EARLY
 #define D2D_FAST_EARLY 1  // the one-compare interval test decided from the bracket alone (brent_step)
 #endif
@@ -1361,8 +1364,11 @@ __device__ __forceinline__ void sensor_pos(const d2d_cfg& cfg, const S& s, doubl
             const double ay = (-5.0 + y) - cy, byy = (5.0 + y) - cy;
             const double mx = fmin(fabs(ax), fabs(bxx)), my = fmin(fabs(ay), fabs(byy));
             const double q = mx * mx + my * my;
-            const bool l0 = (i0 < 0) || q < q0, l1 = (i1 < 0) || q < q1, l2 = (i2 < 0) || q < q2,
-                       l3 = (i3 < 0) || q < q3;
+            const bool l3 = (i3 < 0) || q < q3;
+            // a circle no lane's top 4 takes changes nothing below (every l is false): skip the
+            // insertion for the whole wave (most circles once the top 4 hold near ones)
+            if (D2D_TOP4_SKIP && __ballot(l3) == 0ull) continue;
+            const bool l0 = (i0 < 0) || q < q0, l1 = (i1 < 0) || q < q1, l2 = (i2 < 0) || q < q2;
             q3 = l2 ? q2 : (l3 ? q : q3);
             i3 = l2 ? i2 : (l3 ? i : i3);
             q2 = l1 ? q1 : (l2 ? q : q2);
