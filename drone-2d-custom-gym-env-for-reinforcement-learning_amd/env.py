@@ -187,6 +187,13 @@ class Drone2dVecEnv:
                       for _ in range(2)]
         self._k = 0
         self._stats = torch.zeros(abi.NSTATS, dtype=torch.float64, device=dev)
+        # step()'s host path: the output pointers of both buffer sets as plain ints (ctypes converts
+        # them for the c_void_p parameters) and the raw current-stream query, so an eager step costs
+        # one ctypes call and a few attribute reads on the host (tools/eager_probe.py)
+        self._bufp = [tuple(b[k].data_ptr() if (k != "info" or with_info) else None
+                            for k in ("obs", "rew", "term", "trunc", "info", "tobs")) for b in self._bufs]
+        self._act_shape = (N, abi.ACT_DIM)
+        self._raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
 
     # ------------------------------------------------------------------ plumbing
     def _check(self, code: int, what: str) -> None:
@@ -315,14 +322,18 @@ class Drone2dVecEnv:
         pre-reset observation is in ``self.terminal_obs``.  ``info`` is the float32 [N, 12] table
         of include/drone2d.h (D2D_INFO_*), or None when ``with_info=False``.
         """
-        a = self._prep_actions(actions)
+        a = actions
+        if not (type(a) is torch.Tensor and a.dtype is torch.float32 and a.is_cuda and a.shape == self._act_shape
+                and a.get_device() == self.device.index and a.is_contiguous()):
+            a = self._prep_actions(actions)
         self._k ^= 1
-        b = self._bufs[self._k]
-        self._check(self._lib.d2d_step(self._h, self._ptr(a), self._ptr(b["obs"]), self._ptr(b["rew"]),
-                                 self._ptr(b["term"]), self._ptr(b["trunc"]),
-                                 self._ptr(b["info"]) if self.with_info else None,
-                                 self._ptr(b["tobs"]), self._stream()), "d2d_step")
+        k = self._k
+        st = self._raw_stream(self.device.index) if self._raw_stream else self._stream()
+        rc = self._lib.d2d_step(self._h, a.data_ptr(), *self._bufp[k], st)
+        if rc:
+            self._check(rc, "d2d_step")
         self._last_actions = a  # keep alive until the kernel has consumed it
+        b = self._bufs[k]
         return b["obs"], b["rew"], b["term"], b["trunc"], (b["info"] if self.with_info else None)
 
     @property
