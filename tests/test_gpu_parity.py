@@ -362,6 +362,35 @@ def test_single_env_api(d2):
     env.close()
 
 
+def test_step_accepts_every_action_form(d2):
+    """``step()`` takes the fast host path for float32 contiguous device tensors of shape [N, 2] and
+    converts everything else (numpy float64, CPU tensors, float64 / non-contiguous / flat device
+    tensors): both paths give bit-identical steps, and each step writes the other output buffer."""
+    n = 1000
+    kw = _cfgkw()
+    va = d2.Drone2dVecEnv(n, seed=21, **kw)
+    vb = d2.Drone2dVecEnv(n, seed=21, **kw)
+    va.reset()
+    vb.reset()
+    g = torch.Generator(device="cuda").manual_seed(3)
+    forms = [lambda a: a.cpu().numpy().astype(np.float64), lambda a: a.cpu(), lambda a: a.double(),
+             lambda a: a.t().contiguous().t(), lambda a: a.reshape(-1), lambda a: a.cpu().numpy().tolist()]
+    prev = None
+    for k in range(60):
+        act = torch.rand(n, 2, device="cuda", generator=g) * 2 - 1
+        oa, ra, ta, ua, ia = va.step(act)
+        ob, rb, tb, ub, ib = vb.step(forms[k % len(forms)](act))
+        assert torch.equal(oa, ob) and torch.equal(ra, rb) and torch.equal(ta, tb) and torch.equal(ua, ub)
+        assert torch.equal(ia, ib) and torch.equal(va.terminal_obs, vb.terminal_obs)
+        if prev is not None:
+            assert oa.data_ptr() != prev  # double-buffered outputs
+        prev = oa.data_ptr()
+    with pytest.raises(RuntimeError):
+        va.step(torch.zeros(n + 1, 2, device="cuda"))  # wrong size: refused, not read past the end
+    va.close()
+    vb.close()
+
+
 @pytest.mark.parametrize("which", [0, 1, 2])
 def test_device_math_selftest(d2, which):
     """The kernels' shortcut fp64 routines (range-limited sqrt and division, division by a
