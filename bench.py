@@ -139,6 +139,49 @@ def _upload_graphs(graphs, stream):
         pass
 
 
+def sysfs_card(dev_index: int):
+    """The DRM sysfs directory of HIP device ``dev_index``, matched by its PCI address (None when not
+    found, e.g. no amdgpu sysfs in a container)."""
+    import glob
+
+    try:
+        p = torch.cuda.get_device_properties(dev_index)
+        want = "%04x:%02x:%02x." % (p.pci_domain_id, p.pci_bus_id, p.pci_device_id)
+    except (RuntimeError, AttributeError, AssertionError):
+        return None
+    for d in sorted(glob.glob("/sys/class/drm/card*/device")):
+        if os.path.basename(os.path.realpath(d)).lower().startswith(want):
+            return d
+    return None
+
+
+def gpu_clock(card):
+    """The shader clock right now, read from sysfs (file reads only): the current level of
+    ``pp_dpm_sclk`` (the line marked '*') and the hwmon ``freq1_input`` (sclk, Hz).  None if neither
+    is readable."""
+    import glob
+    import re
+
+    if card is None:
+        return None
+    out = {}
+    try:
+        for line in open(os.path.join(card, "pp_dpm_sclk")):
+            if "*" in line:
+                m = re.search(r"(\d+)\s*[Mm][Hh]z", line)
+                if m:
+                    out["pp_dpm_sclk_mhz"] = float(m.group(1))
+    except OSError:
+        pass
+    for f in sorted(glob.glob(os.path.join(card, "hwmon", "hwmon*", "freq1_input"))):
+        try:
+            out["hwmon_sclk_mhz"] = int(open(f).read().strip()) / 1e6
+            break
+        except (OSError, ValueError):
+            pass
+    return out or None
+
+
 def barrier_sync(world):
     if world > 1:
         dist.barrier()
@@ -285,6 +328,8 @@ def main():
     # run would measure instead of the kernel: 31.4 vs 29.0 us per step (profiles/r04/clock/).  So
     # the same step kernels first run for --clock-warmup-ms on a separate, throwaway batch of this
     # rank's size; fp64 GEMMs instead do not raise the clock (31.4 us).
+    card = sysfs_card(dev.index)
+    clk = {"card": os.path.basename(os.path.dirname(card)) if card else None, "at_start": gpu_clock(card)}
     if args.clock_warmup_ms > 0:
         spin = shard.make_shard_venv(n * world, rank, world, device=dev, seed=777, with_info=args.info, **kwargs)
         spin.reset()
@@ -300,6 +345,8 @@ def main():
     for k in range(args.warmup):
         venv.step(bank[k % ACTION_BANK])
     venv.episode_stats(clear=True)
+    torch.cuda.synchronize()
+    clk["before_timed"] = gpu_clock(card)
 
     # eager: one event pair around the whole loop (an event record per step is a queue marker of a
     # few us each on the GPU side: it measured 35 instead of 28 us per step, tools/eager_probe.py)
@@ -325,6 +372,7 @@ def main():
     n_timed = args.steps
     barrier_sync(world)
     wall = time.perf_counter() - t0
+    clk["after_timed"] = gpu_clock(card)
 
     # episode statistics of the interval: the one RCCL all-reduce (timed separately)
     stats = venv.episode_stats(clear=True)
@@ -396,6 +444,9 @@ def main():
             "kernel_ms_per_rank": kern_ranks,
             # HIP device of each rank (RCCL: one per rank; the gloo rehearsal shares one GPU)
             "device_per_rank": dev_ranks,
+            # rank 0's shader clock (sysfs) at start, right before and right after the timed window:
+            # tells a slow box or an unramped clock apart from a slower kernel
+            "gpu_clock": clk,
         }
         vf = os.path.join(REPO, "profiles", f"valu_{tag}.json")
         if os.path.exists(vf):

@@ -1069,10 +1069,14 @@ __device__ __forceinline__ void arm_lds(const double* ab, int stride, int k, dou
     r2y = (k < 3) ? -sn : sn;
 }
 
+// The Chipmunk arithmetic (this stage and phys_velocities) is contracted: every a + b * c of
+// cpBodyUpdatePosition / UpdateVelocity, the PivotJoint preStep and applyImpulse is one fma, in the
+// operand order oracle/d2d_oracle.c spells out with C fma() (the physics is parity-unpinned, SURVEY.md
+// §8c; the unfused Python restatement tests/golden/ref_shims.py stays within the state tolerance).
 __device__ __forceinline__ void advance_position(Body& b) {
-    b.px = b.px + (b.vx + 0.0) * DT;
-    b.py = b.py + (b.vy + 0.0) * DT;
-    b.a = b.a + (b.w + 0.0) * DT;
+    b.px = fma(b.vx + 0.0, DT, b.px);
+    b.py = fma(b.vy + 0.0, DT, b.py);
+    b.a = fma(b.w + 0.0, DT, b.a);
 }
 template <class S>
 __device__ __forceinline__ bool frame_hits(const S& s, const Body& F, double cs, double sn) {
@@ -1180,14 +1184,13 @@ __device__ __forceinline__ void phys_velocities(const Arms& A, const double pos[
         double r1x, r1y, r2x, r2y;
         arm(A, k, r1x, r1y, r2x, r2y);
         const double m_sum = MI_M + MI_F;
-        double k11 = m_sum, k12 = 0.0, k21 = 0.0, k22 = m_sum;
-        const double r1xsq = r1x * r1x * II_M, r1ysq = r1y * r1y * II_M;
-        const double r1nxy = -r1x * r1y * II_M;
-        k11 += r1ysq; k12 += r1nxy; k21 += r1nxy; k22 += r1xsq;
-        const double r2xsq = r2x * r2x * II_F, r2ysq = r2y * r2y * II_F;
-        const double r2nxy = -r2x * r2y * II_F;
-        k11 += r2ysq; k12 += r2nxy; k21 += r2nxy; k22 += r2xsq;
-        const double det = k11 * k22 - k12 * k21;
+        // k_mat: K = m_sum I + I_a^-1 [r1y^2, -r1x r1y; ., r1x^2] + I_F^-1 [...r2...]; k12 == k21
+        double k11 = fma(r1y * r1y, II_M, m_sum), k22 = fma(r1x * r1x, II_M, m_sum);
+        double k12 = fma(-r1x * r1y, II_M, 0.0);
+        k11 = fma(r2y * r2y, II_F, k11);
+        k12 = fma(-r2x * r2y, II_F, k12);
+        k22 = fma(r2x * r2x, II_F, k22);
+        const double det = fma(k11, k22, -(k12 * k12));
         const double det_inv = 1.0 / det;
         const double dx = (pos[0] + r2x) - (pos[2 * m] + r1x);
         const double dy = (pos[1] + r2y) - (pos[2 * m + 1] + r1y);
@@ -1201,14 +1204,14 @@ __device__ __forceinline__ void phys_velocities(const Arms& A, const double pos[
         }
     }
     // cpBodyUpdateVelocity: gravity (0, -1000), damping^dt, forces on the frame only
-    vel[0] = vel[0] * damping_dt + (0.0 + fx * MI_F) * DT;
-    vel[1] = vel[1] * damping_dt + (GRAV_Y + fy * MI_F) * DT;
-    vel[2] = vel[2] * damping_dt + tq * II_F * DT;
+    vel[0] = fma(vel[0], damping_dt, (0.0 + fx * MI_F) * DT);
+    vel[1] = fma(vel[1], damping_dt, fma(fy, MI_F, GRAV_Y) * DT);
+    vel[2] = fma(vel[2], damping_dt, tq * II_F * DT);
 #pragma unroll
     for (int b = 1; b < 3; ++b) {
-        vel[3 * b + 0] = vel[3 * b + 0] * damping_dt + (0.0 + 0.0 * MI_M) * DT;
-        vel[3 * b + 1] = vel[3 * b + 1] * damping_dt + (GRAV_Y + 0.0 * MI_M) * DT;
-        vel[3 * b + 2] = vel[3 * b + 2] * damping_dt + 0.0 * II_M * DT;
+        vel[3 * b + 0] = fma(vel[3 * b + 0], damping_dt, (0.0 + 0.0 * MI_M) * DT);
+        vel[3 * b + 1] = fma(vel[3 * b + 1], damping_dt, fma(0.0, MI_M, GRAV_Y) * DT);
+        vel[3 * b + 2] = fma(vel[3 * b + 2], damping_dt, 0.0 * II_M * DT);
     }
     // applyCachedImpulse with dt_coef = 1
 #pragma unroll
@@ -1217,12 +1220,12 @@ __device__ __forceinline__ void phys_velocities(const Arms& A, const double pos[
         double r1x, r1y, r2x, r2y;
         arm(A, k, r1x, r1y, r2x, r2y);
         const double jx = j[2 * k] * 1.0, jy = j[2 * k + 1] * 1.0;
-        vel[3 * m + 0] = vel[3 * m + 0] + (-jx) * MI_M;
-        vel[3 * m + 1] = vel[3 * m + 1] + (-jy) * MI_M;
-        vel[3 * m + 2] += II_M * (r1x * (-jy) - r1y * (-jx));
-        vel[0] = vel[0] + jx * MI_F;
-        vel[1] = vel[1] + jy * MI_F;
-        vel[2] += II_F * (r2x * jy - r2y * jx);
+        vel[3 * m + 0] = fma(-jx, MI_M, vel[3 * m + 0]);
+        vel[3 * m + 1] = fma(-jy, MI_M, vel[3 * m + 1]);
+        vel[3 * m + 2] = fma(II_M, fma(r1x, -jy, -(r1y * (-jx))), vel[3 * m + 2]);
+        vel[0] = fma(jx, MI_F, vel[0]);
+        vel[1] = fma(jy, MI_F, vel[1]);
+        vel[2] = fma(II_F, fma(r2x, jy, -(r2y * jx)), vel[2]);
     }
     // 10 sequential-impulse sweeps (Space.iterations default)
 #pragma unroll 1  // (unrolled twice: 28 B of spills, no gain)
@@ -1253,24 +1256,24 @@ __device__ __forceinline__ void phys_velocities(const Arms& A, const double pos[
             // gravity / force update adds +0 or a nonzero term, sums of nonzero terms round to +0,
             // never -0); they are dropped for finite states
             const bool za = (k % 3 == 1);
-            const double v1x = za ? vel[3 * m + 0] : vel[3 * m + 0] + (-r1y) * vel[3 * m + 2];
-            const double v1y = za ? vel[3 * m + 1] : vel[3 * m + 1] + r1x * vel[3 * m + 2];
-            const double v2x = vel[0] + (-r2y) * vel[2], v2y = vel[1] + r2x * vel[2];
+            const double v1x = za ? vel[3 * m + 0] : fma(-r1y, vel[3 * m + 2], vel[3 * m + 0]);
+            const double v1y = za ? vel[3 * m + 1] : fma(r1x, vel[3 * m + 2], vel[3 * m + 1]);
+            const double v2x = fma(-r2y, vel[2], vel[0]), v2y = fma(r2x, vel[2], vel[1]);
             const double ux = bx - (v2x - v1x), uy = by - (v2y - v1y);
-            double jx = ux * ka + uy * kb;
-            double jy = ux * kc + uy * kd;
+            double jx = fma(ux, ka, uy * kb);
+            double jy = fma(ux, kc, uy * kd);
             const double ox = j[2 * k], oy = j[2 * k + 1];
             const double nx = ox + jx, ny = oy + jy;
             j[2 * k] = nx;
             j[2 * k + 1] = ny;
             jx = nx - ox;
             jy = ny - oy;
-            vel[3 * m + 0] = vel[3 * m + 0] + (-jx) * MI_M;
-            vel[3 * m + 1] = vel[3 * m + 1] + (-jy) * MI_M;
-            if (!za) vel[3 * m + 2] += II_M * (r1x * (-jy) - r1y * (-jx));
-            vel[0] = vel[0] + jx * MI_F;
-            vel[1] = vel[1] + jy * MI_F;
-            vel[2] += II_F * (r2x * jy - r2y * jx);
+            vel[3 * m + 0] = fma(-jx, MI_M, vel[3 * m + 0]);
+            vel[3 * m + 1] = fma(-jy, MI_M, vel[3 * m + 1]);
+            if (!za) vel[3 * m + 2] = fma(II_M, fma(r1x, -jy, -(r1y * (-jx))), vel[3 * m + 2]);
+            vel[0] = fma(jx, MI_F, vel[0]);
+            vel[1] = fma(jy, MI_F, vel[1]);
+            vel[2] = fma(II_F, fma(r2x, jy, -(r2y * jx)), vel[2]);
         }
     }
 }

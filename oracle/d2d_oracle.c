@@ -309,10 +309,13 @@ static int box_circle_touch(const obody* f, double cx, double cy, double r) {
 
 typedef struct { double r1x, r1y, r2x, r2y, ka, kb, kc, kd, bx, by; } ojoint;
 
+/* cpBody applyImpulse: v += j m^-1, w += I^-1 cross(r, j), each a + b*c one fma (the contraction
+ * libdrone2d_hip.so's physics uses, in the same operand order: the Chipmunk step is parity-unpinned,
+ * and the unfused Python restatement in tests/golden stays within the state tolerance) */
 static void apply_imp(obody* b, double jx, double jy, double rx, double ry) {
-    b->vx = b->vx + jx * b->m_inv;
-    b->vy = b->vy + jy * b->m_inv;
-    b->w += b->i_inv * (rx * jy - ry * jx);
+    b->vx = fma(jx, b->m_inv, b->vx);
+    b->vy = fma(jy, b->m_inv, b->vy);
+    b->w = fma(b->i_inv, fma(rx, jy, -(ry * jx)), b->w);
 }
 
 /* cpSpaceStep(dt) on (frame, left, right) + 6 pivots; st is the D2D_S_* state vector */
@@ -329,9 +332,9 @@ static int o_space_step(const d2d_cfg* cfg, const d2d_scn* scn, double* st, doub
     apply_force_local(&B[0], fR, DRONE_R);
     /* 1. cpBodyUpdatePosition (v_bias = 0) */
     for (int i = 0; i < 3; ++i) {
-        B[i].px = B[i].px + (B[i].vx + 0.0) * dt;
-        B[i].py = B[i].py + (B[i].vy + 0.0) * dt;
-        B[i].a = B[i].a + (B[i].w + 0.0) * dt;
+        B[i].px = fma(B[i].vx + 0.0, dt, B[i].px);
+        B[i].py = fma(B[i].vy + 0.0, dt, B[i].py);
+        B[i].a = fma(B[i].w + 0.0, dt, B[i].a);
         B[i].c = cos(B[i].a);
         B[i].s = sin(B[i].a);
     }
@@ -349,14 +352,14 @@ static int o_space_step(const d2d_cfg* cfg, const d2d_scn* scn, double* st, doub
         j->r2x = b->c * JB[k] + (-b->s) * 0.0;
         j->r2y = b->s * JB[k] + b->c * 0.0;
         double m_sum = a->m_inv + b->m_inv;
-        double k11 = m_sum, k12 = 0.0, k21 = 0.0, k22 = m_sum;
-        double r1xsq = j->r1x * j->r1x * a->i_inv, r1ysq = j->r1y * j->r1y * a->i_inv;
-        double r1nxy = -j->r1x * j->r1y * a->i_inv;
-        k11 += r1ysq; k12 += r1nxy; k21 += r1nxy; k22 += r1xsq;
-        double r2xsq = j->r2x * j->r2x * b->i_inv, r2ysq = j->r2y * j->r2y * b->i_inv;
-        double r2nxy = -j->r2x * j->r2y * b->i_inv;
-        k11 += r2ysq; k12 += r2nxy; k21 += r2nxy; k22 += r2xsq;
-        double det = k11 * k22 - k12 * k21;
+        /* k_tensor: K = m_sum I + sum over both bodies of I^-1 [ry^2, -rx ry; -rx ry, rx^2] */
+        double k11 = fma(j->r1y * j->r1y, a->i_inv, m_sum), k22 = fma(j->r1x * j->r1x, a->i_inv, m_sum);
+        double k12 = fma(-j->r1x * j->r1y, a->i_inv, 0.0), k21;
+        k11 = fma(j->r2y * j->r2y, b->i_inv, k11);
+        k12 = fma(-j->r2x * j->r2y, b->i_inv, k12);
+        k22 = fma(j->r2x * j->r2x, b->i_inv, k22);
+        k21 = k12;
+        double det = fma(k11, k22, -(k12 * k21));
         double det_inv = 1.0 / det;
         j->ka = k22 * det_inv; j->kb = -k12 * det_inv; j->kc = -k21 * det_inv; j->kd = k11 * det_inv;
         double dx = (b->px + j->r2x) - (a->px + j->r1x);
@@ -369,9 +372,9 @@ static int o_space_step(const d2d_cfg* cfg, const d2d_scn* scn, double* st, doub
     const double damping = pow(cfg->damping, dt);
     for (int i = 0; i < 3; ++i) {
         obody* b = &B[i];
-        b->vx = b->vx * damping + (0.0 + b->fx * b->m_inv) * dt;
-        b->vy = b->vy * damping + (-1000.0 + b->fy * b->m_inv) * dt;
-        b->w = b->w * damping + b->t * b->i_inv * dt;
+        b->vx = fma(b->vx, damping, (0.0 + b->fx * b->m_inv) * dt);
+        b->vy = fma(b->vy, damping, fma(b->fy, b->m_inv, -1000.0) * dt);
+        b->w = fma(b->w, damping, b->t * b->i_inv * dt);
         b->fx = b->fy = b->t = 0.0;
     }
     /* 5. applyCachedImpulse with dt_coef = dt/prev_dt = 1 (0 after reset, where jAcc = 0 anyway) */
@@ -387,11 +390,11 @@ static int o_space_step(const d2d_cfg* cfg, const d2d_scn* scn, double* st, doub
             obody* a = &B[k < 3 ? 1 : 2];
             obody* b = &B[0];
             ojoint* j = &J[k];
-            double v1x = a->vx + (-j->r1y) * a->w, v1y = a->vy + j->r1x * a->w;
-            double v2x = b->vx + (-j->r2y) * b->w, v2y = b->vy + j->r2x * b->w;
+            double v1x = fma(-j->r1y, a->w, a->vx), v1y = fma(j->r1x, a->w, a->vy);
+            double v2x = fma(-j->r2y, b->w, b->vx), v2y = fma(j->r2x, b->w, b->vy);
             double ux = j->bx - (v2x - v1x), uy = j->by - (v2y - v1y);
-            double jx = ux * j->ka + uy * j->kb;
-            double jy = ux * j->kc + uy * j->kd;
+            double jx = fma(ux, j->ka, uy * j->kb);
+            double jy = fma(ux, j->kc, uy * j->kd);
             double ox = st[D2D_S_J + 2 * k], oy = st[D2D_S_J + 2 * k + 1];
             double nx = ox + jx, ny = oy + jy;
             st[D2D_S_J + 2 * k] = nx;

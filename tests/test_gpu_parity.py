@@ -527,3 +527,54 @@ def test_config5_size_on_one_gpu_windows(d2):
     stats = venv.episode_stats()
     assert torch.isfinite(stats).all() and stats[1] > 0
     venv.close()
+
+
+@pytest.mark.parametrize("scn", ["corridor", "large", "S_corridor"])
+def test_bench_launch_windows(d2, scn):
+    """The exact launch ``bench.py`` times (BASELINE configs[2] / [3], and S_corridor as the
+    maximum-obstacle case): 65 536 envs of one scenario built as bench.py builds them
+    (``make_shard_venv``, info rows off), i.e. the ungrouped ``d2d_step_kernel`` with the scenario and
+    its golden-march tables staged in LDS, 1 024 workgroups, the three-way re-check off (more
+    workgroups than CUs).  After 64 untested steps (the bench's steady-state mix of episode ages,
+    reset-cache fills included), three windows of 384 envs (the first, an unaligned middle span, the
+    last) are compared with oracle batches keyed by the same global env ids, teacher-forced every step
+    for 40 steps with auto-reset on (drone_2d_env.py:394-615)."""
+    import oracle
+    from drone2d_amd import shard
+    from drone2d_amd.config import make_cfg
+
+    n = FULL
+    kw = _cfgkw(scn)
+    venv = shard.make_shard_venv(n, 0, 1, seed=12345, with_info=False, **kw)
+    assert venv.group_layout() is None  # identity slot layout: the ungrouped kernel
+    venv.reset()
+    g = torch.Generator(device=venv.device).manual_seed(1000)
+    for k in range(64):
+        venv.step(torch.rand(n, 2, device=venv.device, generator=g) * 2 - 1)
+    m = 384
+    wins = [0, n // 2 + 37, n - m]
+    cfg_for = lambda o: make_cfg(dict(kw), auto_reset=True, env_id_base=o)  # noqa: E731
+    orcs = [oracle.OracleBatch(cfg_for(o), [s.to_c() for s in venv.scenarios], m) for o in wins]
+    for o, orc in zip(wins, orcs):
+        orc.reset(12345)
+    rng = np.random.default_rng(8)
+    dones = 0
+    for t in range(40):
+        st, ist = (x.cpu().numpy() for x in venv.get_state())
+        for o, orc in zip(wins, orcs):
+            orc.set_state(st[:, o:o + m].copy(), ist[:, o:o + m].copy())
+        act = rng.uniform(-1, 1, (n, 2)).astype(np.float32)
+        obs, rew, term, trunc, _ = venv.step(torch.as_tensor(act, device=venv.device))
+        obs, rew, term = obs.cpu().numpy(), rew.cpu().numpy(), term.cpu().numpy()
+        assert np.isfinite(obs).all() and np.isfinite(rew).all()
+        for o, orc in zip(wins, orcs):
+            o_obs, o_rew, o_term, _, _ = orc.step(act[o:o + m])
+            np.testing.assert_array_equal(term[o:o + m], o_term)
+            np.testing.assert_allclose(rew[o:o + m], o_rew, rtol=REW_RTOL, atol=REW_ATOL)
+            np.testing.assert_allclose(obs[o:o + m], o_obs, rtol=0, atol=OBS_ATOL)
+            dones += int(o_term.sum())
+    st2 = venv.get_state()[0].cpu().numpy()
+    for o, orc in zip(wins, orcs):
+        np.testing.assert_allclose(st2[:, o:o + m], orc.get_state()[0], rtol=1e-9, atol=1e-9)
+    assert dones > 0  # auto-resets happened inside the windows
+    venv.close()

@@ -12,7 +12,15 @@ import pytest
 from conftest import SCENARIOS
 
 OBS_ATOL = 1e-6      # oracle emits float32 obs; golden is float64
-STATE_RTOL = 1e-12
+# Post-step state.  The golden physics is ref_shims.py's unfused Python restatement of Chipmunk; the
+# oracle (like the HIP kernels) contracts every a + b*c of the step into one fma (DESIGN.md
+# "Arithmetic"), so the two differ by rounding only.  Measured over traj + crafted (round 6):
+# positions / angles <= 3.1e-14 relative, velocities <= 4.9e-12, jAcc <= 4.0e-11 (Gauss-Seidel
+# cancellation), total_reward <= 5.0e-11 (one crafted CA case amplifies a velocity difference).
+STATE_RTOL = 1e-12   # positions, angles
+DYN_RTOL = 1e-10     # velocities, jAcc, path_error, total_reward
+POS_COLS = [0, 1, 2, 6, 7, 8, 12, 13, 14]
+DYN_COLS = [c for c in range(32) if c not in POS_COLS]
 
 
 def _flags(pre_i):
@@ -48,7 +56,8 @@ def test_one_step_teacher_forced(oracle_mod, d2, scenarios_c, which):
     np.testing.assert_allclose(obs, g["obs"], rtol=0, atol=OBS_ATOL)
     np.testing.assert_allclose(rew, g["rew"], rtol=1e-6, atol=1e-5)
     # post-step physics state and bookkeeping
-    np.testing.assert_allclose(st2.T, g["post"], rtol=STATE_RTOL, atol=1e-9)
+    np.testing.assert_allclose(st2.T[:, POS_COLS], g["post"][:, POS_COLS], rtol=STATE_RTOL, atol=1e-9)
+    np.testing.assert_allclose(st2.T[:, DYN_COLS], g["post"][:, DYN_COLS], rtol=DYN_RTOL, atol=1e-9)
     np.testing.assert_array_equal(ist2[0], g["post_i"][:, 0])
     np.testing.assert_array_equal(ist2[1], _flags(g["post_i"]))
     # info terms (keys: see make_golden.INFO_KEYS)
