@@ -287,19 +287,17 @@ __device__ inline void gen_curriculum(const d2d_curriculum& c, double W, double 
 
 // ------------------------------------------------------------------ wave-cooperative generation (K5)
 // The same scenario as gen_curriculum, built by the 64 lanes of one wave in LDS: the stream's first
-// GEN_WIN words (Philox blocks, D2D_GEN_WIN_BLOCKS per lane), the azimuths' sincos, the segment lengths, the 20
+// GEN_WIN words (GEN_WIN_BLOCKS Philox blocks per lane), the azimuths' sincos, the segment lengths, the 20
 // QPMI2D 3 x 3 solves and the 16 interval records in parallel; the few truly sequential parts (the
 // waypoint and arc-length prefix sums, the obstacle rejection loop, which consumes a data-dependent
 // number of draws) on lane 0 reading the stream from LDS.  Every value is produced by the same
 // operations on the same operands as gen_curriculum (so the tables stay bit-identical to the CPU
 // oracle's o_gen_curriculum); only the order in which independent values are computed changes.
-#ifndef D2D_GEN_WIN_BLOCKS
-#define D2D_GEN_WIN_BLOCKS 2  // Philox blocks per lane in the window (1: round 4's 256 words)
-#endif
+constexpr int GEN_WIN_BLOCKS = 2;  // Philox blocks per lane in the window (round 4's 1: 256 words)
 // stream words precomputed per item: corner + waypoints + the obstacle trials, which the wave evaluates
 // at 64 starts 4 words apart (gen_obstacles_wave) -- 512 words keep the first evaluation's trials
 // inside the window
-constexpr int GEN_WIN = 256 * D2D_GEN_WIN_BLOCKS;
+constexpr int GEN_WIN = 256 * GEN_WIN_BLOCKS;
 
 // LDS hand-off between the lanes of the one wave that runs the generator
 __device__ __forceinline__ void wave_sync() {
@@ -534,7 +532,7 @@ __device__ inline int gen_path_wave(const d2d_curriculum& c, double W, double H,
     (void)st;
     GSTAMP(st, 0);
 #pragma unroll
-    for (int blk = 0; blk < D2D_GEN_WIN_BLOCKS; ++blk) {
+    for (int blk = 0; blk < GEN_WIN_BLOCKS; ++blk) {
         uint32_t o[4];
         const uint32_t b = (uint32_t)(64 * blk + lane);
         philox(gid, key, GEN_TAG + b, 0u, (uint32_t)seed, (uint32_t)(seed >> 32), o);
@@ -655,7 +653,7 @@ __device__ inline void gen_rest_wave(const d2d_curriculum& c, double W, double H
     }
     if (lane < D2D_MAX_CIRCLES) s.cx[lane] = s.cy[lane] = s.cr[lane] = 0.0;
     wave_sync();
-    if (stg >= 3 && !(D2D_ABLATE & 128)) {  // (128: diagnostic timing builds skip the obstacles)
+    if (stg >= 3) {
         // the draws before the obstacle calls (lane 0), then the calls (gen_obstacles_wave; the path
         // in G.s is already built)
         __shared__ double s_nobs;

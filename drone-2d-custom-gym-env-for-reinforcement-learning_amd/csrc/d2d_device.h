@@ -29,20 +29,6 @@
 // bool conditions are combined with & / | on purpose (selects instead of short-circuit branches)
 #pragma clang diagnostic ignored "-Wbitwise-instead-of-logical"
 
-// Diagnostic-only ablation mask (tools/variants.py builds separate timing-only libraries with it;
-// the product is always built with 0): 1 skip Brent, 2 skip sensing, 4 skip joint iterations,
-// 8 skip collision test, 16 skip the Brent continuation after the golden-march tables, 128 the fresh
-// curriculum generator skips the obstacles.
-#ifndef D2D_RM_CARRY_KA
-#define D2D_RM_CARRY_KA 1  // A/B: brent_step carries ka in the state for global-memory tables (0: reload)
-#endif
-#ifndef D2D_RCACHE
-#define D2D_RCACHE 0  // A/B: 1 = K1's plain search over global-memory tables caches the probe's
-                      // interval record in LDS instead of staging the lane's knots there.  Measured
-                      // slower (fresh K1 80.5 vs 77.7 us, profiles/r05/a): 68 % of probes hit the
-                      // cached interval, but some lane of the wave misses on most early steps, so the
-                      // wave still waits for a global record load on nearly every step of its chain
-#endif
 // D2D_BSTAMP (diagnostic builds only, tools/bstamps.py): s_memtime stamps inside the golden-march
 // continuation's Brent steps, per path wave -- [workgroup][step < 64][8] in d2d_bst: entry, candidate
 // computed, interval found, probe evaluated, state updated, the step's B.num, whether the wave took
@@ -65,9 +51,6 @@ __device__ uint64_t d2d_bst[BST_N];
 #define BST(k, dep) \
     do {       \
     } while (0)
-#endif
-#ifndef D2D_ABLATE
-#define D2D_ABLATE 0
 #endif
 
 namespace d2d {
@@ -98,10 +81,7 @@ enum { REC_XB = 0, REC_XA = 6, REC_U0 = 12, REC_U1 = 13, REC_IDU = 14, REC_T = 1
 //         one QPMI2D evaluation touches two cache lines per lane instead of 16.
 // Measured (profiles/r04/layout/): ScnR for every path costs the LDS paths 0.6 % (corridor), 3 %
 // (mixed) and 5.6 % (4 096 envs); ScnF for the fresh curriculum's step kernel 179 vs 105 us.
-#ifndef D2D_REC_PAD
-#define D2D_REC_PAD 1  // A/B: ScnR's pad word (136-byte stride: LDS-bank-conflict-free)
-#endif
-constexpr int REC_W = REC_N + D2D_REC_PAD;
+constexpr int REC_W = REC_N + 1;  // ScnR's pad word: a 136-byte record stride
 #define D2D_SCN_TAIL                                                                                      \
     double cx[D2D_MAX_CIRCLES], cy[D2D_MAX_CIRCLES], cr[D2D_MAX_CIRCLES];                               \
     double wp_last_x, wp_last_y;                                                                          \
@@ -218,27 +198,9 @@ __device__ __forceinline__ double sqrt_nz(double x) {
 // NaN fix-up is a wave-uniform branch taken only when some lane needs it (a probe exactly on the
 // drone's position): one compare per distance instead of a compare and two selects.  The same
 // results as sqrt_nz bit for bit (d2d_selftest checks it against sqrt()).
-#ifndef D2D_ABL_FASTDIV
-#define D2D_ABL_FASTDIV 0  // timing ablation only (not exact): the parabolic step as p * rcp(q)
-#endif
-#ifndef D2D_TOP4_SKIP
-#define D2D_TOP4_SKIP 1  // sensing skips a circle no lane's top 4 takes (wave ballot; 0: A/B)
-#endif
-#ifndef D2D_FAST_EARLY
-#define D2D_FAST_EARLY 1  // the one-compare interval test decided from the bracket alone (brent_step)
-#endif
-#ifndef D2D_PAR_NOBRANCH
-#define D2D_PAR_NOBRANCH 0  // A/B: 1 = the parabolic step's division on every Brent step (no ballot branch)
-#endif
-#ifndef D2D_SQRT_SEL
-#define D2D_SQRT_SEL 0  // A/B: 1 = the fix-up by selects (sqrt_nz) in every distance
-#endif
-#ifndef D2D_ABL_FASTSQRT
-#define D2D_ABL_FASTSQRT 0  // timing ablation only (not exact): v_sqrt_f64 alone for distances
-#endif
+// (the fix-up by selects in every distance measured +2.8 % corridor / +4.2 % small batch,
+// profiles/r05/stash/)
 __device__ __forceinline__ double sqrt_dist(double x) {
-    if (D2D_ABL_FASTSQRT) return __builtin_amdgcn_sqrt(x);
-    if (D2D_SQRT_SEL) return sqrt_nz(x);
     double g = sqrt_refine(x);
     if (__builtin_expect(__ballot(__builtin_amdgcn_class(x, 0x260)) != 0ull, 0)) {
         asm volatile("" ::: "memory");  // keeps the branch (no if-conversion into selects)
@@ -455,7 +417,7 @@ __device__ __forceinline__ double path_dist_n(const S& s, const PathK& K, double
                                               double& u1) {
     double x, y;
     path_eval_n(s, K, u, n, x, y, u1);
-    // (sqrt_nz measured slower here than the library sequence: tools/ubench_step.hip, D2D_SQRT_SEL)
+    // (sqrt_nz measured slower here than the library sequence: tools/ubench_step.hip)
     return norm2(x - px, y - py);
 }
 // get_closest_u (predef_path.py:226-248) = scipy fminbound(x1=-10, x2=L+10, xtol=1e-6, maxfun=500),
@@ -473,7 +435,6 @@ struct Brent {
     double a, b, fulc, ffulc, nfc, fnfc, xf, fx, rat, e;
     double ka, kxf;
     int num, ia, ib, ixf;
-    int rci;  // record cache (D2D_RCACHE, global-memory tables): interval whose record the lane holds in LDS, -1: none
 };
 constexpr double BR_SQRT_EPS = 1.4832396974191326e-08;  // sqrt(2.2e-16)
 constexpr double BR_GOLDEN = 0.3819660112501051;        // 0.5*(3.0 - sqrt(5.0))
@@ -496,7 +457,6 @@ __device__ __forceinline__ void brent_init(const S& s, const PathK& K, double px
     B.num = 1;
     B.ffulc = B.fx;
     B.fnfc = B.fx;
-    B.rci = -1;
 }
 // scipy's loop condition without maxfun: |xf - xm| > tol2 - (b - a) / 2
 __device__ __forceinline__ bool brent_open(const Brent& B) {
@@ -519,7 +479,7 @@ __device__ __forceinline__ void brent_step(const S& s, const PathK& K, double px
     // table; carried in the state (B.ka, B.kxf, from the records the probes already read) when the
     // table is read per lane from global memory (ScnR), where that load sat on every step's chain.
     // (Prefetching a's whole record before the candidate is known, or xf's, measured no faster.)
-    const double ka = (S::RM && D2D_RM_CARRY_KA) ? B.ka : SREC(s, REC_U1, B.ia);
+    const double ka = S::RM ? B.ka : SREC(s, REC_U1, B.ia);
     const double xm = 0.5 * (a + b);
     const double tol1 = BR_SQRT_EPS * fabs(xf) + BR_XATOL3;
     const double tol2 = 2.0 * tol1;
@@ -532,10 +492,11 @@ __device__ __forceinline__ void brent_step(const S& s, const PathK& K, double px
     q = fabs(q);
     const bool par = (fabs(B.e) > tol1) & (fabs(p) < fabs(0.5 * q * B.e)) & (p > q * (a - xf)) & (p < q * (b - xf));
     // only used when `par` holds: then q > 0 and |p / q| < |e| / 2, a normal quotient.  Skipped
-    // when no lane of the wave takes the parabolic step (the golden tails of long searches)
+    // when no lane of the wave takes the parabolic step (the golden tails of long searches; the
+    // division on every step without this branch measured +2 %, profiles/r05/stash/)
     double rat_p = 0.0;
-    if (D2D_PAR_NOBRANCH || __ballot(par) != 0ull) {
-        rat_p = D2D_ABL_FASTDIV ? (p + 0.0) * __builtin_amdgcn_rcp(q) : div_normal(p + 0.0, q);
+    if (__ballot(par) != 0ull) {
+        rat_p = div_normal(p + 0.0, q);
         const double xp = xf + rat_p;
         // tol1 * (np.sign(d) + (d == 0)) for d = xm - xf: a, b and xf are finite (the initial
         // bracket and finite steps), so d is not NaN and the product is -tol1 for d < 0, else +tol1
@@ -564,8 +525,8 @@ __device__ __forceinline__ void brent_step(const S& s, const PathK& K, double px
     // farther end by 0.38 of a distance >= (b - a) / 2 (or by tol1 < (b - a) / 2); an accepted
     // parabolic step either lands at least tol2 inside the bracket or is replaced by a tol1 step from
     // xf toward the midpoint, and max(|rat|, tol1) then moves it by less than tol1 more.  The margins
-    // (tol1 >= 3.3e-7) dwarf the roundings.  D2D_FAST_EARLY=0 restores the explicit x test (A/B).
-    const bool fast = D2D_FAST_EARLY ? (B.ib <= B.ia + 1) : ((x >= a) & (x <= b) & (B.ib <= B.ia + 1));
+    // (tol1 >= 3.3e-7) dwarf the roundings.
+    const bool fast = B.ib <= B.ia + 1;
     int ix;
     if (__ballot(!fast) == 0ull) {
         ix = min(B.ia + ((x <= ka) ? 0 : 1), K.nw - 1);
@@ -578,18 +539,7 @@ __device__ __forceinline__ void brent_step(const S& s, const PathK& K, double px
         if constexpr (S::RM) {
             int z = 0;
             asm volatile("" : "+v"(z));
-            if constexpr (KN && D2D_RCACHE) {
-                // the cached record's interval first: u_index(x) == n exactly when us[n] < x <= us[n+1]
-                // (n >= 1; n = 0: x <= us[1]), the knots being non-decreasing (NaN fails both)
-                const int lane = (int)(threadIdx.x & 63);
-                const double c0 = kn[64 * REC_U0 + lane], c1 = kn[64 * REC_U1 + lane];
-                const bool inc = (B.rci >= 0) & (x <= c1) & ((B.rci == 0) | (c0 < x));
-                ix = B.rci;
-                if (__ballot(!inc) != 0ull) {
-                    const int iscan = u_index_at(s, x, z);
-                    ix = inc ? ix : iscan;
-                }
-            } else if constexpr (KN) {
+            if constexpr (KN) {
                 ix = u_index_kn(kn, K.nw, x, z);
             } else {
                 ix = u_index_at(s, x, z);
@@ -601,31 +551,10 @@ __device__ __forceinline__ void brent_step(const S& s, const PathK& K, double px
         }
     }
     BST(2, ix);
+    // (a per-lane LDS cache of the probe's interval record for global-memory tables measured slower:
+    // fresh K1 80.5 vs 77.7 us, profiles/r05/a/ -- some lane of the wave misses on most early steps)
     double kx;
-    double fu;
-    if constexpr (KN && D2D_RCACHE) {
-        // global-memory tables (one scenario per lane, fresh curriculum): the interval's record from the
-        // lane's LDS cache when it is the interval of the previous probe (most probes once the bracket
-        // has closed in), else from global memory into the cache -- one record load per interval
-        // change instead of one per probe
-        const int lane = (int)(threadIdx.x & 63);
-        const bool hit = ix == B.rci;
-        if (__ballot(!hit) != 0ull) {
-            if (!hit) {
-#pragma unroll
-                for (int f = 0; f < REC_N; ++f) kn[64 * f + lane] = SREC(s, f, ix);
-                B.rci = ix;
-            }
-        }
-        double r[REC_N];
-#pragma unroll
-        for (int f = 0; f < REC_N; ++f) r[f] = kn[64 * f + lane];
-        double xq, yq;
-        path_eval_rec(r, K, x, ix, xq, yq, kx);
-        fu = norm2(xq - px, yq - py);
-    } else {
-        fu = path_dist_n(s, K, x, ix, px, py, kx);
-    }
+    const double fu = path_dist_n(s, K, x, ix, px, py, kx);
     BST(3, fu);
     // (num, scipy's maxfun count, is not advanced here: brent_run derives it from its pass count)
     const bool le = fu <= fx;
@@ -642,7 +571,7 @@ __device__ __forceinline__ void brent_step(const S& s, const PathK& K, double px
     B.ia = to_a ? ti : B.ia;
     B.ib = to_a ? B.ib : ti;
     B.ixf = le ? ix : B.ixf;
-    if constexpr (S::RM && D2D_RM_CARRY_KA) {  // (the same bookkeeping brtab_build does for its snapshots)
+    if constexpr (S::RM) {  // (the same bookkeeping brtab_build does for its snapshots)
         const double tk = le ? B.kxf : kx;
         B.ka = to_a ? tk : B.ka;
         B.kxf = le ? kx : B.kxf;
@@ -700,9 +629,8 @@ __device__ __forceinline__ void brent_run(const S& s, const PathK& K, double px,
 template <bool KN = false, class S>
 __device__ __forceinline__ double closest_u(const S& s, double px, double py, int& iu, double* kn = nullptr) {
     static_assert(!KN || S::RM, "staged knots / record cache: global-memory tables only");
-    static_assert(REC_N <= D2D_MAX_WPS, "the record cache reuses the knot staging's LDS (K1_KN_BYTES)");
     const PathK K = path_k(s);
-    if constexpr (KN && !D2D_RCACHE) {
+    if constexpr (KN) {
 #pragma unroll
         for (int k = 0; k < D2D_MAX_WPS; ++k) kn[64 * k + (threadIdx.x & 63)] = SUS(s, k);
     }
@@ -731,9 +659,6 @@ __device__ __forceinline__ double closest_u(const S& s, double px, double py, in
 //      (its fx / fnfc / ffulc are the distances at recorded probes) and continues with brent_step.
 // Both stages perform exactly the operations brent_step performs on the same operands, so the
 // result is bit-identical to closest_u for every point (tests/test_gpu_parity.py grid test).
-#ifndef D2D_BT_MASK
-#define D2D_BT_MASK 1  // exec-masked table loads in the re-check (global-memory tables only; A/B: 0)
-#endif
 constexpr int BT_K = BT_K_MAX;  // recorded steps per kind (longer marches continue in brent_step)
 constexpr int BT_HOT = BT_K + 3;  // probe entries per kind: 0..BT_K, plus zero entries the 3-step
                                   // unrolled check may read past a table's end
@@ -908,7 +833,6 @@ __device__ __forceinline__ void bt_verify(const BtHot* hot, BtLane& L, int k0, i
     int dev = L.dev;
     const int kind = L.kind;
     for (int k = k0; __ballot(k < min(dev, k1)) != 0ull; k += 3) {
-#if D2D_BT_MASK
         // tables in global memory (a lane's own scenario): a lane that is done loads nothing, so a
         // wave's long marches do not drag every lane's table lines in from HBM
         BtIt ha{}, hb{}, hc{};
@@ -917,10 +841,6 @@ __device__ __forceinline__ void bt_verify(const BtHot* hot, BtLane& L, int k0, i
             hb = bt_hot<LT>(hot, kind, k + 2);
             hc = bt_hot<LT>(hot, kind, k + 3);
         }
-#else
-        const BtIt ha = bt_hot<LT>(hot, kind, k + 1), hb = bt_hot<LT>(hot, kind, k + 2),
-                   hc = bt_hot<LT>(hot, kind, k + 3);
-#endif
         const double fd = bt_check(ha, k, px, py, fa, fb, fc, dev);
         const double fe = bt_check(hb, k + 1, px, py, fb, fc, fd, dev);
         const double ff = bt_check(hc, k + 2, px, py, fc, fd, fe, dev);
@@ -953,13 +873,12 @@ __device__ __forceinline__ double bt_finish(const SC& s, const BrTab& T, const B
     B.ia = S.ia;
     B.ib = S.ib;
     B.ixf = S.ixf;
-    B.rci = -1;
     if (__ballot(brent_active(B)) != 0ull) {
         const PathK K = path_k(s);
         B.ffulc = bt_dist<LT>(hot, kind, S.j_fulc, px, py);
         B.fnfc = bt_dist<LT>(hot, kind, S.j_nfc, px, py);
         B.fx = bt_dist<LT>(hot, kind, S.j_xf, px, py);
-        if (!(D2D_ABLATE & 16)) brent_run(s, K, px, py, B);
+        brent_run(s, K, px, py, B);
     }
     iu = B.ixf;
     return B.xf;
@@ -1081,7 +1000,7 @@ __device__ __forceinline__ void advance_position(Body& b) {
 template <class S>
 __device__ __forceinline__ bool frame_hits(const S& s, const Body& F, double cs, double sn) {
     bool hit = false;
-    for (int k = 0; k < ((D2D_ABLATE & 8) ? 0 : s.n_circles); ++k) {
+    for (int k = 0; k < s.n_circles; ++k) {
         const double dx = s.cx[k] - F.px, dy = s.cy[k] - F.py;
         {
             // skip the circle for the whole wave when it is out of every lane's reach: every point of
@@ -1229,7 +1148,7 @@ __device__ __forceinline__ void phys_velocities(const Arms& A, const double pos[
     }
     // 10 sequential-impulse sweeps (Space.iterations default)
 #pragma unroll 1  // (unrolled twice: 28 B of spills, no gain)
-    for (int it = 0; it < ((D2D_ABLATE & 4) ? 0 : 10); ++it) {
+    for (int it = 0; it < 10; ++it) {
 #pragma unroll
         for (int k = 0; k < 6; ++k) {
             const int m = k < 3 ? 1 : 2;
@@ -1350,7 +1269,7 @@ __device__ __forceinline__ void sensor_pos(const d2d_cfg& cfg, const S& s, doubl
     o[7] = m1to1(y, 0.0, H);
     double bd0 = __builtin_inf(), bd1 = __builtin_inf(), bd2 = __builtin_inf();
     int bi0 = -1, bi1 = -1, bi2 = -1;
-    const int nc = (D2D_ABLATE & 2) ? 0 : s.n_circles;
+    const int nc = s.n_circles;
     bool full = true;
     if (s.r_uniform == s.r_uniform) {
         // every circle has radius r: d = sqrt(q) - r is non-decreasing in the squared distance q,
@@ -1370,7 +1289,7 @@ __device__ __forceinline__ void sensor_pos(const d2d_cfg& cfg, const S& s, doubl
             const bool l3 = (i3 < 0) || q < q3;
             // a circle no lane's top 4 takes changes nothing below (every l is false): skip the
             // insertion for the whole wave (most circles once the top 4 hold near ones)
-            if (D2D_TOP4_SKIP && __ballot(l3) == 0ull) continue;
+            if (__ballot(l3) == 0ull) continue;
             const bool l0 = (i0 < 0) || q < q0, l1 = (i1 < 0) || q < q1, l2 = (i2 < 0) || q < q2;
             q3 = l2 ? q2 : (l3 ? q : q3);
             i3 = l2 ? i2 : (l3 ? i : i3);
@@ -1491,10 +1410,8 @@ __device__ __forceinline__ void path_obs(const d2d_cfg& cfg, const S& s, const B
                                          double al, uint32_t& flags, double o[8], const BtHot* hot = nullptr,
                                          double* kn = nullptr) {
     int iu = -1;
-    const double u = (D2D_ABLATE & 1) ? clipd(x - 100.0, -10.0, SUS(s, s.n_wps - 1))
-                     : (T ? (LT ? closest_u_tab<true>(s, *T, hot, x, y, iu)
-                                : closest_u_tab<false>(s, *T, &T->hot, x, y, iu))
-                          : closest_u<KN>(s, x, y, iu, kn));
+    const double u = T ? (LT ? closest_u_tab<true>(s, *T, hot, x, y, iu) : closest_u_tab<false>(s, *T, &T->hot, x, y, iu))
+                       : closest_u<KN>(s, x, y, iu, kn);
     path_obs_u(cfg, s, x, y, al, u, flags, o, iu);
 }
 

@@ -109,7 +109,7 @@ StepArgs make_args(const d2d_t* h) {
     a.wg_scn = h->wg_scn;
     a.scn_tag = h->scn_tag;
     a.clock = h->clock;
-    if (D2D_K1_QUEUE && h->cfg.scn_pool == 2 && h->fresh_q) {
+    if (h->cfg.scn_pool == 2 && h->fresh_q) {
         a.fq = h->fresh_q;
         a.fqc = reinterpret_cast<uint32_t*>(h->fresh_q + h->fresh_ring);
         a.fq_mask = (uint32_t)h->fresh_ring - 1u;
@@ -117,9 +117,7 @@ StepArgs make_args(const d2d_t* h) {
     return a;
 }
 
-#ifndef D2D_GEN_GRID
-#define D2D_GEN_GRID 2048  // K5b workgroups (A/B)
-#endif
+constexpr int GEN_GRID = 2048;  // K5b workgroups
 // K5: the fresh curriculum's scenario slots (restore: every slot from its recipe), on `stream`
 hipError_t fresh_regen(d2d_t* h, hipStream_t stream, bool restore = false, bool queued = false) {
     FreshArgs f{};
@@ -148,7 +146,7 @@ hipError_t fresh_regen(d2d_t* h, hipStream_t stream, bool restore = false, bool 
     if (!queued) hipLaunchKernelGGL(d2d_fresh_scan_kernel, dim3((items + 255) / 256), dim3(256), 0, stream, f);
     // one wave per queued slot: ~800 per step at 65 536 envs stepped with random actions (the items
     // of a step all run at once); a reset queues every env (the grid's workgroups then take several)
-    hipLaunchKernelGGL(d2d_fresh_gen_kernel, dim3(std::min(items, D2D_GEN_GRID)), dim3(64), 0, stream, f);
+    hipLaunchKernelGGL(d2d_fresh_gen_kernel, dim3(std::min(items, GEN_GRID)), dim3(64), 0, stream, f);
     hipError_t e = hipGetLastError();
     // after a K1, K5b itself leaves the next tail (FreshRing: no launch; the round-4 clear kernel
     // after every K5b cost 5.5 us per step); after a scan, both tails to the head
@@ -728,7 +726,7 @@ int32_t d2d_step(d2d_t* h, const float* act_dev, float* obs_dev, float* rew_dev,
         // the three-way table re-check pays when the SIMDs have idle issue slots (at most one K1
         // workgroup per CU: 4 096 / 16 384 envs -4 %), not at full load (65 536 envs +3.6 %)
         const int nwg = h->lane_env ? h->n_groups : (int)grid.x;
-        const bool s3 = D2D_SPLIT3 > 0 || (D2D_SPLIT3 < 0 && nwg <= std::max(h->n_cu, 1));
+        const bool s3 = nwg <= std::max(h->n_cu, 1);
         auto launch = [&](auto kern, dim3 g, size_t lds) {
             hipLaunchKernelGGL(kern, g, dim3(K1_THREADS), lds, (hipStream_t)stream, a);
         };
@@ -753,7 +751,7 @@ int32_t d2d_step(d2d_t* h, const float* act_dev, float* obs_dev, float* rew_dev,
     }
     e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(e, "d2d_step launch");
-    if (fresh_mode(h) && (e = fresh_regen(h, (hipStream_t)stream, false, D2D_K1_QUEUE && h->cfg.auto_reset)) !=
+    if (fresh_mode(h) && (e = fresh_regen(h, (hipStream_t)stream, false, h->cfg.auto_reset != 0)) !=
                              hipSuccess)
         return hip_fail(e, "d2d_step: fresh scenarios");
     if (h->cfg.auto_reset && ++h->n_steps % FILL_PERIOD == 0 &&

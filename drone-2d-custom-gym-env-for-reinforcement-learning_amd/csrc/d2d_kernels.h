@@ -102,7 +102,7 @@ struct StepArgs {
     const int32_t* scn_tag;   // [2 n]
     int64_t* clock;           // [1]
     // ... and K5's queue: K1 appends the slot of the episode after next of every env it resets
-    // (D2D_K1_QUEUE; null: K5a scans for them)
+    // (null: K5a scans for them; auto-reset off)
     int32_t* fq;              // [fq_mask + 1] slots (a ring, see FreshRing)
     uint32_t* fqc;            // FreshRing words ([FR_HEAD]: appends so far)
     uint32_t fq_mask;         // ring size - 1 (a power of two >= 2 n)
@@ -121,20 +121,6 @@ __device__ __forceinline__ const S* scn_tab(const StepArgs& a) { return static_c
 // takes an entry only when its tag matches; otherwise (an episode shorter than the fill period) it
 // computes the observation synchronously.  Running the fill as its own kernel keeps it off K1's
 // issue slots: inside K1 it would run a whole wave for the ~0.5 of 64 envs that reset per step.
-#ifndef D2D_ABL
-#define D2D_ABL 0        // diagnostic builds only: bit r skips role r's compute, bit 4 = perfect
-                         // reset cache (no fills, every entry taken as ready): timing ablations
-#endif
-#ifndef D2D_K1_QUEUE
-#define D2D_K1_QUEUE 1  // K1 queues the fresh curriculum's slots itself (no K5a scan per step; A/B: 0)
-#endif
-#ifndef D2D_GLOBAL_NOSPLIT
-#define D2D_GLOBAL_NOSPLIT 1  // tables in global memory: W2 re-checks the whole table, W3 none (A/B: 0)
-#endif
-#ifndef D2D_SPLIT3
-#define D2D_SPLIT3 -1    // W2, W1 and W3 re-check one third each of the golden-march table: 1 always,
-                         // 0 never, -1 when K1 has at most one workgroup per CU (chosen in d2d_step)
-#endif
 // Reset-cache entries per env: the next reset's observation and the one after (slot = episode
 // counter mod 2), so K4 may fill every 48 steps instead of 16 without more envs falling back to the
 // synchronous reset.  K4 is launched after every FILL_PERIOD steps (a captured 16-step graph holds one
@@ -428,7 +414,7 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const SC* scns, const
         double ov[19];
         Body B[3];
         double j[12], cs[3], sn[3], fx = 0.0, fy = 0.0, tq = 0.0;
-        if (valid && !(D2D_ABL & 1)) {
+        if (valid) {
 #pragma unroll
             for (int b = 0; b < 3; ++b) {
                 B[b].px = fld(a.st, 6 * b + 0, n, i);
@@ -453,7 +439,7 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const SC* scns, const
             done = cause != 0;
             // which envs end (for W1, W2, W3) and whether their reset observation is cached
             const int32_t ep = fld(a.ist, D2D_I_EPISODE, n, i);
-            const bool cv = done && auto_reset && ((D2D_ABL & 16) != 0 || a.rc_tag[rc_entry(a, i, (uint32_t)ep)] == ep);
+            const bool cv = done && auto_reset && a.rc_tag[rc_entry(a, i, (uint32_t)ep)] == ep;
             sh.ep[lane] = (uint32_t)ep;
             sh.cause[lane] = (uint8_t)cause;
             sh.sina[lane] = sn[0];
@@ -472,7 +458,7 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const SC* scns, const
             }
         }
         flag_raise(sh.f_done);
-        if (valid && !(D2D_ABL & 1)) {
+        if (valid) {
             const Arms A = make_arms(cs, sn);
             const double pos[6] = {B[0].px, B[0].py, B[1].px, B[1].py, B[2].px, B[2].py};
             double vel[9] = {B[0].vx, B[0].vy, B[0].w, B[1].vx, B[1].vy, B[1].w, B[2].vx, B[2].vy, B[2].w};
@@ -559,7 +545,7 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const SC* scns, const
         if (S3) {
             // the middle third of W2's golden-march re-check first, at W2's priority (its critical path)
             __builtin_amdgcn_s_setprio(PRIO_W2);
-            if (valid && !(D2D_ABL & 4) && !(D2D_ABLATE & 1) && a.brt) {
+            if (valid && a.brt) {
                 const BrTab& T = a.brt[sh.scn[lane]];
                 const BtHot* hot = LTAB ? hots + sh.scn[lane] : &T.hot;
                 Body F = PF;
@@ -576,7 +562,7 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const SC* scns, const
             flag_raise(sh.f_ver1);
         }
         __builtin_amdgcn_s_setprio(PRIO_W1);
-        if (valid && !(D2D_ABL & 2)) {
+        if (valid) {
             Body F = PF;
             advance_position(F);
             double so[19];
@@ -638,17 +624,17 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const SC* scns, const
         __builtin_amdgcn_s_setprio(PRIO_W2);
         double po[8];
         Body F{};
-        if (valid && !(D2D_ABL & 4)) {
+        if (valid) {
             F = PF;
             advance_position(F);
             uint32_t f = (uint32_t)fld(a.ist, D2D_I_FLAGS, n, i);
             const BrTab* T = brtab(a, sh.scn[lane]);
-            if (T && !(D2D_ABLATE & 1)) {
+            if (T) {
                 // golden-march re-check of steps [1, split); W3 checks [split, len) meanwhile
                 const BtHot* hot = LTAB ? hots + sh.scn[lane] : &T->hot;
                 BtLane L = bt_start<LTAB>(*T, hot, F.px, F.py);
-                bt_verify<LTAB>(hot, L, 1, (D2D_GLOBAL_NOSPLIT && !LDS) ? BT_K : S3 ? bt_third(*T, 1) : bt_split(*T),
-                                F.px, F.py);
+                // (tables in global memory: W2 re-checks the whole table, W3 none)
+                bt_verify<LTAB>(hot, L, 1, !LDS ? BT_K : S3 ? bt_third(*T, 1) : bt_split(*T), F.px, F.py);
                 flag_wait(sh.f_ver);
                 if (S3) flag_wait(sh.f_ver1);
                 L.dev = min(L.dev, (int)sh.pflags[lane]);
@@ -705,9 +691,9 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const SC* scns, const
         // ---------------------------------------------------------------- auto-reset observation
         __builtin_amdgcn_s_setprio(PRIO_W2);  // the re-check below is on W2's critical path
         double po[8];
-        if (D2D_GLOBAL_NOSPLIT && !LDS) {
+        if (!LDS) {
             sh.pflags[lane] = 0x7fffffffu;
-        } else if (valid && !(D2D_ABL & 4) && !(D2D_ABLATE & 1) && a.brt) {
+        } else if (valid && a.brt) {
             // second half of W2's golden-march re-check (its first wave-priority work)
             const BrTab& T = a.brt[sh.scn[lane]];
             const BtHot* hot = LTAB ? hots + sh.scn[lane] : &T.hot;
@@ -738,7 +724,7 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const SC* scns, const
 #pragma unroll
             for (int k = 0; k < D2D_NSTATS; ++k) sh.acc[k][lane] = fld(a.acc, k, n, i);
         }
-        if (valid && done && auto_reset && !(D2D_ABL & 8)) {
+        if (valid && done && auto_reset) {
             // the next episode: spawn state, reset observation (cached or computed), new state
             const uint32_t ep = sh.ep[lane];
             const int nscn = next_scenario(a, ie, ep);
@@ -769,7 +755,7 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const SC* scns, const
             fld(a.ist, D2D_I_EPISODE, n, i) = (int32_t)(ep + 1u);
             if (a.cfg.scn_pool && a.env_scn) a.env_scn[ie] = nscn;
         }
-        if (D2D_K1_QUEUE && !LDS && a.fq) {  // (fresh mode reads its tables from global memory: the LDS
+        if (!LDS && a.fq) {  // (fresh mode reads its tables from global memory: the LDS
                                              // instantiations carry no queue code, +0.9 us at 4 096 envs)
             // fresh curriculum: the slot the finished episode ran on now takes the episode after
             // next (key ep + 2 - 1 = the new counter), generated by K5 after this launch
@@ -799,14 +785,14 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const SC* scns, const
     // ---------------------------------------------------------------- epilogue
     // obs tile: rows [e0, e0+rows) are one contiguous span of global memory (grouped: one
     // contiguous 108-byte row per env)
-    if (GRP && !(D2D_ABLATE & 32)) {
+    if (GRP) {
         for (int k = qt; gvalid && k < EPB * D2D_OBS_DIM; k += K1_THREADS) {
             const int r = k / D2D_OBS_DIM;
             const int e = a.lane_env[e0 + r];
             if (e >= 0) a.obs[(size_t)e * D2D_OBS_DIM + (k - r * D2D_OBS_DIM)] = sh.u.p.obs[k];
         }
     } else {
-        const int rows = gvalid ? max(0, min(EPB, a.n - e0)) : 0;  // (D2D_ABLATE & 32: timing-only slot-order rows)
+        const int rows = gvalid ? max(0, min(EPB, a.n - e0)) : 0;
         const int words = rows * D2D_OBS_DIM;
         float* dst = a.obs + (size_t)e0 * D2D_OBS_DIM;
         // a full tile is 64 x 27 floats = 432 float4 at a 16-B aligned offset (e0 * 108 B, e0 % 64
@@ -836,7 +822,7 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const SC* scns, const
             trunc = true;
             term = false;
         }
-        const int io = (D2D_ABLATE & 64) ? min(i, a.n - 1) : ie;  // (64: timing-only slot order)
+        const int io = ie;
         a.rew[io] = (float)reward;
         a.term[io] = (uint8_t)term;
         a.trunc[io] = (uint8_t)trunc;
@@ -887,7 +873,8 @@ __device__ __forceinline__ void k1_group(const StepArgs& a, S* s_scn, K1Shared& 
     k1_body<LDS, LTAB, GRP, S3, S>(a, scns, hots, s0, sh, wg, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6),
                                    (int)threadIdx.x);
 }
-// S3: the three-way table re-check (D2D_SPLIT3), chosen at launch
+// S3: the three-way table re-check (W2, W1 and W3 one third each of the golden-march table), chosen at
+// launch when K1 has at most one workgroup per CU (4 096 / 16 384 envs -4 %; at full load +3.6 %)
 // (LDS: the handle's tables are ScnF, staged; otherwise ScnR, read per lane from global memory)
 template <bool LDS, bool LTAB, bool S3>
 __global__ __launch_bounds__(K1_THREADS, 4) void d2d_step_kernel(StepArgs a) {

@@ -1,6 +1,7 @@
 #!/bin/bash
 # VALU instruction mix of the step kernel per variant library (tools/variants.py builds, e.g. the
-# D2D_ABL role ablations): one rocprofv3 --pmc pass per variant.  The difference base - variant is
+# role ablations: `variants.py build r0:D2D_ABL=1@role_ablation ...`,
+# tools/patches/role_ablation.patch): one rocprofv3 --pmc pass per variant.  The difference base - variant is
 # the skipped role's share.  Usage: bash tools/role_mix.sh TAG...  -> gpurun_out/role_mix/<TAG>/...
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}

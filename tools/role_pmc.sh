@@ -1,6 +1,7 @@
 #!/bin/bash
 # Per-variant SQ instruction counters of the step kernel (GPU box): one rocprofv3 --pmc pass per
-# variant library built by tools/variants.py (e.g. the D2D_ABL role ablations).
+# variant library built by tools/variants.py (e.g. the role ablations: `variants.py build r0:D2D_ABL=1@role_ablation ...`,
+# tools/patches/role_ablation.patch).
 # Usage: bash tools/role_pmc.sh TAG...   -> gpurun_out/role_pmc/<TAG>/..., summary on stdout
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}

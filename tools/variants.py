@@ -4,15 +4,19 @@
     python tools/variants.py build base p0:D2D_PRIO=0     # CPU container: tools/_abl/libd2d_var_<tag>.so
     python tools/variants.py run base p0 [--envs N]        # GPU box: ms/step of each, interleaved rounds
 
-A spec is TAG[:DEF[,DEF...]]; DEF is passed as -DDEF.
+A spec is TAG[:DEF[,DEF...]][::FLAG+FLAG][@PATCH]; DEF is passed as -DDEF, PATCH names a diagnostic
+patch under tools/patches/ (e.g. ``r0:D2D_ABL=1@role_ablation``: the role ablations), applied to a
+copy of the package sources before the build.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import shutil
 import subprocess
 import sys
+import tempfile
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
@@ -30,12 +34,25 @@ def build(specs):
 
     os.makedirs(ABL, exist_ok=True)
     for spec in specs:
+        spec, _, patch = spec.partition("@")
         spec, _, flags = spec.partition("::")   # TAG[:DEF,DEF][::flag+flag] (e.g. -mllvm+-misched=...)
         tag, _, defs = spec.partition(":")
         d = [f"-D{x}" for x in defs.split(",") if x] + [f for f in flags.split("+") if f]
-        subprocess.run([_build.hipcc(), *_build.HIPCC_FLAGS, *d, "-I", os.path.join(REPO, "include"), _build.SRC,
+        src, tmp = _build.SRC, None
+        if patch:
+            # the package sources + include/ copied, the patch applied to the copy (never to the tree)
+            tmp = tempfile.mkdtemp(prefix="d2d_var_")
+            pkg = os.path.basename(os.path.dirname(os.path.dirname(_build.SRC)))
+            shutil.copytree(os.path.join(REPO, pkg, "csrc"), os.path.join(tmp, pkg, "csrc"))
+            shutil.copytree(os.path.join(REPO, "include"), os.path.join(tmp, "include"))
+            subprocess.run(["patch", "-s", "-p1", "-d", tmp, "-i",
+                            os.path.join(REPO, "tools", "patches", patch + ".patch")], check=True)
+            src = os.path.join(tmp, os.path.relpath(_build.SRC, REPO))
+        subprocess.run([_build.hipcc(), *_build.HIPCC_FLAGS, *d, "-I", os.path.join(REPO, "include"), src,
                         "-o", lib_for(tag)], check=True)
-        print("built", lib_for(tag), d)
+        if tmp:
+            shutil.rmtree(tmp)
+        print("built", lib_for(tag), d, patch or "")
 
 
 def time_variant(d2, torch, lib, n, scenario, steps=1000, warmup=300, auto_reset=True):
@@ -98,5 +115,5 @@ if __name__ == "__main__":
     if a.mode == "build":
         build(a.specs)
     else:
-        run([s.partition("::")[0].partition(":")[0] for s in a.specs], a.envs, a.scenario, a.rounds, not a.no_auto_reset,
+        run([s.partition("@")[0].partition("::")[0].partition(":")[0] for s in a.specs], a.envs, a.scenario, a.rounds, not a.no_auto_reset,
             a.steps, a.warmup)
