@@ -64,16 +64,25 @@ def _compile(src: str, out: str, verbose: bool, flags=None):
     os.replace(tmp, out)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    """The in-tree libraries: the env (libdrone2d_hip.so: every mode, one scenario layout), its
-    exact-trig build (libdrone2d_hip_exact.so) and the PPO update kernels (libd2d_ppo.so)."""
+def build_exact(force: bool = False, verbose: bool = False) -> str:
+    """The exact-trig build (libdrone2d_hip_exact.so), compiled only when asked for: by
+    ``build(exact=True)`` (``__graft_entry__.build()``, which the tests rely on) or by the first
+    ``Drone2dVecEnv(exact_trig=True)`` that finds it missing."""
+    if force or needs_build(EXACT_OUT):
+        _compile(SRC, EXACT_OUT, verbose, HIPCC_FLAGS + ["-DD2D_EXACT_TRIG=1"])
+    return EXACT_OUT
+
+
+def build(force: bool = False, verbose: bool = False, exact: bool = False) -> str:
+    """The in-tree libraries: the env (libdrone2d_hip.so: every mode, one scenario layout), the PPO
+    update kernels (libd2d_ppo.so) and, with ``exact``, the env's exact-trig build."""
     stale = os.path.join(PKG_DIR, "_lib", "libdrone2d_hip_rm.so")  # rounds 1-3's second layout build
     if os.path.exists(stale):
         os.remove(stale)
     if force or needs_build():
         _compile(SRC, OUT, verbose)
-    if force or needs_build(EXACT_OUT):
-        _compile(SRC, EXACT_OUT, verbose, HIPCC_FLAGS + ["-DD2D_EXACT_TRIG=1"])
+    if exact:
+        build_exact(force, verbose)
     if force or needs_build(PPO_OUT, PPO_SRC, PPO_HDRS):
         _compile(PPO_SRC, PPO_OUT, verbose, PPO_FLAGS)
     return OUT

@@ -465,8 +465,14 @@ __device__ inline void gen_obstacles_wave(GenLds& G, uint64_t seed, uint32_t gid
             tcons = R.pos - (w + 4 * lane);
         }
         const int w0 = w;
+        // A trial at word w was evaluated (on lane (w - w0) / 4) iff w - w0 is a multiple of 4 below
+        // 256.  Every trial consumes a multiple of 4 words today (uniform 2, each polar-normal attempt
+        // 4, uniform 2), so the walk stays on the evaluated starts; should a draw ever consume another
+        // count, the walk leaves the window at that trial and the next pass evaluates from there
+        // (slower, never a wrong trial).
+        const auto evaluated = [&](int wv) { return (wv < w0 + 256) & (((wv - w0) & 3) == 0); };
         if (phase == 0) {
-            while ((double)num < n && nc < D2D_MAX_CIRCLES && tries < 4096 && w < w0 + 256) {
+            while ((double)num < n && nc < D2D_MAX_CIRCLES && tries < 4096 && evaluated(w)) {
                 const int t = (w - w0) >> 2;
                 ++tries;
                 if (gen_rl(tok, t)) {
@@ -491,7 +497,7 @@ __device__ inline void gen_obstacles_wave(GenLds& G, uint64_t seed, uint32_t gid
             // generate_obstacles_around_path(1.0, 0.0, 0.0, on_path=True): one trial, accepted
             if (nc >= D2D_MAX_CIRCLES) {
                 phase = 2;
-            } else if (w < w0 + 256) {
+            } else if (evaluated(w)) {
                 const int t = (w - w0) >> 2;
                 const double cx = gen_rl(tpx, t), cy = gen_rl(tpy, t), cr = gen_rl(tsz, t);
                 if (lane == 0) {

@@ -11,6 +11,7 @@ CPU or PyTorch fallback.
 from __future__ import annotations
 
 import ctypes as C
+import os
 from typing import Sequence
 
 import numpy as np
@@ -150,6 +151,10 @@ class Drone2dVecEnv:
                 raise ValueError("exact_trig selects the exact-trig library build; do not also pass native_lib")
             from ._native import EXACT_LIB_PATH
 
+            if not os.path.exists(EXACT_LIB_PATH):  # built on first use (hipcc, ~1 min)
+                from ._build import build_exact
+
+                build_exact()
             native_lib = EXACT_LIB_PATH
         self._lib = load(native_lib)
         if device is None:
@@ -237,9 +242,12 @@ class Drone2dVecEnv:
         elif sim_num is not None:
             self.kwargs["scenario"] = "curriculum"
             self.kwargs["sim_num"] = int(sim_num)
-        elif self.fresh and self.kwargs.get("scenario") == "curriculum":
-            # neither given: the schedule carries on where the device clock has it (the library
-            # zeroes the clock, so sim_num0 takes the progress: sim_num + clock x envs_total)
+        elif self.fresh and self.kwargs.get("scenario") not in CURRICULUM_STAGES:
+            # neither given, and the stage follows the sim_num schedule (scenario 'curriculum' or any
+            # non-stage scenario with mode='curriculum', drone_2d_env.py:324-334 -- the test
+            # make_curriculum uses to pick stage 0): the schedule carries on where the device clock
+            # has it (the library zeroes the clock, so sim_num0 takes the progress: sim_num + clock x
+            # envs_total)
             clock = self.fresh_recipes()[2]
             self.kwargs["sim_num"] = int(self.kwargs.get("sim_num", 0)) + clock * self.envs_total
         self.kwargs["mode"] = "curriculum"

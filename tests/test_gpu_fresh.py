@@ -187,6 +187,28 @@ def test_set_curriculum_seed_only_keeps_progress(d2):
     venv.close()
 
 
+def test_set_curriculum_keeps_progress_non_stage_scenario(d2):
+    """mode='curriculum' with a non-stage scenario (the reference's default train config,
+    scenario='large') follows the sim_num schedule too (drone_2d_env.py:324-334), so set_curriculum()
+    with neither stage nor sim_num carries the clock's progress into sim_num0 as well."""
+    n = 1024
+    venv = d2.Drone2dVecEnv(n, seed=5, **dict(_kw(sim_num=690000), scenario="large"))
+    assert venv.fresh and venv.curriculum.stage == 0  # the schedule picks the stage
+    venv.reset()
+    for _ in range(50):
+        venv.step(torch.rand(n, 2, device=venv.device) * 2 - 1)
+    venv.set_curriculum(seed=7)
+    assert venv.kwargs["sim_num"] == 690000 + 50 * n
+    keys, _, clock = venv.fresh_recipes()
+    assert clock == 0
+    tab = venv.scenario_table(0, 2 * n)
+    for s in np.flatnonzero(keys >= 0):
+        assert (tab[s].spawn_xmin, tab[s].spawn_xmax) == (100.0, 1200.0), s
+    venv.set_curriculum()  # neither given again: still no restart of the schedule
+    assert venv.kwargs["sim_num"] == 690000 + 50 * n
+    venv.close()
+
+
 def test_masked_fresh_reset_keeps_seed(d2):
     """a masked fresh reset with a new seed is refused (the envs it leaves running would
     keep old-seed scenarios that no checkpoint recipe regenerates); with the same seed it works."""
