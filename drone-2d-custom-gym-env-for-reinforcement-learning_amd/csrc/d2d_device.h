@@ -215,6 +215,18 @@ __device__ __forceinline__ double max_abs_fin(double r, double t) {
     asm("v_max_f64 %0, |%1|, %2" : "=v"(m) : "v"(r), "v"(t));
     return m;
 }
+// min / max of two non-NaN doubles, one instruction each (fmin / fmax first quiet their operands for
+// the NaN rule: two more v_max_f64 per call)
+__device__ __forceinline__ double min_fin(double a, double b) {
+    double m;
+    asm("v_min_f64 %0, %1, %2" : "=v"(m) : "v"(a), "v"(b));
+    return m;
+}
+__device__ __forceinline__ double max_fin(double a, double b) {
+    double m;
+    asm("v_max_f64 %0, %1, %2" : "=v"(m) : "v"(a), "v"(b));
+    return m;
+}
 // Correctly rounded a / b for normal operands with a normal quotient (no div_scale / div_fixup
 // range handling: results for zero / inf / NaN / extreme-exponent operands are unspecified).
 // Checked bitwise against '/' by d2d_selftest.
@@ -1291,14 +1303,19 @@ __device__ __forceinline__ void sensor_pos(const d2d_cfg& cfg, const S& s, doubl
             // insertion for the whole wave (most circles once the top 4 hold near ones)
             if (__ballot(l3) == 0ull) continue;
             const bool l0 = (i0 < 0) || q < q0, l1 = (i1 < 0) || q < q1, l2 = (i2 < 0) || q < q2;
-            q3 = l2 ? q2 : (l3 ? q : q3);
+            // the indices by the stable insertion's selects; the sorted keys by min / max (the
+            // same values: inserting q into q0 <= q1 <= q2 <= q3 gives min(q_k, max(q_k-1, q)) in
+            // slot k, empty slots hold +inf; one fp64 op per slot instead of two 32-bit selects per
+            // nesting level -- a NaN q only arises for a NaN position, whose result the fallback
+            // below recomputes, so the NaN-free min / max apply)
             i3 = l2 ? i2 : (l3 ? i : i3);
-            q2 = l1 ? q1 : (l2 ? q : q2);
             i2 = l1 ? i1 : (l2 ? i : i2);
-            q1 = l0 ? q0 : (l1 ? q : q1);
             i1 = l0 ? i0 : (l1 ? i : i1);
-            q0 = l0 ? q : q0;
             i0 = l0 ? i : i0;
+            q3 = min_fin(q3, max_fin(q2, q));
+            q2 = min_fin(q2, max_fin(q1, q));
+            q1 = min_fin(q1, max_fin(q0, q));
+            q0 = min_fin(q0, q);
         }
         const double d0 = sqrt_dist(q0) - r, d1 = sqrt_dist(q1) - r, d2 = sqrt_dist(q2) - r,
                      d3 = sqrt_dist(q3) - r;
