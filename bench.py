@@ -9,16 +9,19 @@ A "step" = one ``d2d_step`` (libdrone2d_hip.so) over all envs of a GPU: thrust -
 equivalent 3-body/6-joint solve -> collision -> 3-nearest sensing -> Brent closest point ->
 27-dim obs -> reward/termination -> in-kernel auto-reset.  Workload (BASELINE.json configs[2]):
 65 536 envs per GPU on the ``corridor`` test scenario (18 circles), U(-1,1) float32 actions
-pre-generated on the device (a bank of 16, cycled), inputs resident in HBM before timing.  The 16
-steps of one bank pass are captured once as a hipGraph and the timed loop replays it (no host work
-per step); ``--eager`` launches each step from Python instead.  Either way every step runs the full
-kernel on fresh state.
+pre-generated on the device (a bank of 16, cycled), inputs resident in HBM before timing.  The timed
+loop launches every step from Python (``venv.step``, the SB3 adapter's path; ~5.5 us of host work
+per call, GPU-bound at ~26 us); ``--graph`` replays the steps captured as hipGraphs instead.  Either
+way every step runs the full kernel on fresh state.  Eager is the default because it measured
+faster: 2.39-2.42 G vs 2.31-2.36 G env-steps/s for 20 timed steps after 5 warm-up steps, alternating
+on one box, and 2.451-2.457 G vs 2.446-2.452 G for 2 000 steps (profiles/r06/short/): a graph's
+kernel nodes cost ~0.8 us more per step on this ROCm.
 Multi-GPU: one process per GPU, each with its own 65 536 envs (weak scaling, global env ids), no
 collective in the step; the episode statistics are all-reduced once per timed interval (RCCL).
 
 Prints ONE JSON line (rank 0).  ``roofline.achieved`` = 650 algorithmic bytes per env-step x envs
-per launch / mean step-kernel duration (HIP events on the launch stream, per graph replay / 16
-steps); ``cpu_baseline`` = the C
+per launch / mean step time on the device (HIP events on the launch stream around the timed
+steps: one pair around the eager loop, one per graph replay with --graph); ``cpu_baseline`` = the C
 oracle (a scalar port of the same algorithm) timed on this host's cores on a bounded sample.
 """
 from __future__ import annotations
@@ -66,8 +69,9 @@ def parse():
                         "throwaway batch (the measured envs are untouched); 0 disables")
     p.add_argument("--info", action="store_true",
                    help="also write the per-env info rows (f32 [N, 12], what the SB3 adapter reads): +48 B/env-step")
-    p.add_argument("--eager", action="store_true",
-                   help="launch every step from Python instead of replaying the captured hipGraph")
+    p.add_argument("--graph", action="store_true",
+                   help="replay the steps captured as hipGraphs instead of launching each step from Python")
+    p.add_argument("--eager", action="store_true", help="(the default) launch every step from Python")
     p.add_argument("--exact-trig", action="store_true",
                    help="the exact-trig library build (Drone2dVecEnv(exact_trig=True): fdlibm sin / cos / "
                         "atan2, the reference's bearing sequence; bit-identical to the oracle's exact build)")
@@ -307,7 +311,7 @@ def main():
     glen = args.steps if args.steps <= 512 else 256
     reps, rem = divmod(args.steps, glen)
     graph = tail = None
-    hipgraph = not args.eager
+    hipgraph = args.graph and not args.eager
     if hipgraph:
         def capture(n_steps):
             g = torch.cuda.CUDAGraph()

@@ -22,6 +22,6 @@ run cfg3_large_65536 --scenario large
 run cfg3_S_corridor_65536 --scenario S_corridor
 run cfg4_mixed_65536 --scenario mixed
 run cfg2_free_65536 --scenario corridor_free
-run cfg2_corridor_65536_eager --scenario corridor --eager
+run cfg2_corridor_65536_graph --scenario corridor --graph
 run cfg2_corridor_65536_info --scenario corridor --info
 run fresh_curriculum_65536 --scenario curriculum

@@ -24,7 +24,7 @@ step() {  # step <name> <timeout> <cmd...>: stop on any failure
 
 # the bench's own defaults (2 000 graph-replayed steps after 300 warmup steps)
 step kt 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/kt" -o kt -- $B
-step kt_eager 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/kt_eager" -o kt -- $B --eager --steps 300 --warmup 300
+step kt_graph 600 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/kt_graph" -o kt -- $B --graph
 step pmc_fetch 600 rocprofv3 $KR -T --output-format csv -d "$OUT/pmc_fetch" -o fetch --pmc FETCH_SIZE -- $B --eager --steps 40 --warmup 300
 step pmc_write 600 rocprofv3 $KR -T --output-format csv -d "$OUT/pmc_write" -o write --pmc WRITE_SIZE -- $B --eager --steps 40 --warmup 300
 step pmc_sq 600 rocprofv3 $KR -T --output-format csv -d "$OUT/pmc_sq" -o sq --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_ANY -- $B --eager --steps 40 --warmup 300
