@@ -1,21 +1,36 @@
 #!/bin/bash
-# A/B of tools/_abl/libd2d_var_<tag>.so builds plus the GPU suite on the current tree (GPU box).
-# Usage: bash tools/gpu_ab.sh OUTTAG TAG... [-- extra]   (env: NOTEST=1 skips pytest, TRAFFIC=1 adds
-# the FETCH / WRITE / lane-utilisation passes of the current tree)
+# A/B GPU session (GPU box): driver-style first 20/5 line, GPU suite, A/B of tools/_abl variant
+# builds, default bench, rocprofv3 kernel-trace summary.  Each GPU step under its own timeout; a
+# crash / abort / timeout ends the script (test failures, rc 1, do not).
+# Usage: bash tools/gpu_ab.sh OUTTAG [VARIANT_TAG...]   env: NOTEST=1, NOPROF=1, AB_SCN="corridor S_corridor"
 set -u
 O=gpurun_out/$1; shift
 TAGS="$*"
 mkdir -p $O
 export TMPDIR=/tmp
-[ -x tools/ubench_lat ] && { timeout -k 10 60 ./tools/ubench_lat > $O/lat.json 2>&1 || exit 1; cat $O/lat.json; }
+R=$(pwd)
+fail() { echo "STOP at $1 (rc $2)"; exit $2; }
+timeout -k 10 200 python bench.py --steps 20 --warmup 5 > $O/bench_k20_first.log 2>&1 || fail bench_k20_first $?
+tail -1 $O/bench_k20_first.log
 if [ "${NOTEST:-0}" != 1 ]; then
-timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -1 $O/pytest_gpu.log; [ $rc -eq 0 ] || exit 1
+  timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1
+  rc=$?; echo "pytest rc=$rc"; tail -3 $O/pytest_gpu.log; [ $rc -le 1 ] || fail pytest $rc
 fi
-timeout -k 10 600 python tools/variants.py run $TAGS --envs 65536 --scenario corridor --rounds 3 > $O/ab_corridor.log 2>&1 || exit 1
-timeout -k 10 600 python tools/variants.py run $TAGS --envs 65536 --scenario S_corridor --rounds 2 > $O/ab_S_corridor.log 2>&1 || exit 1
-timeout -k 10 400 python tools/variants.py run $TAGS --envs 4096 --scenario corridor_free --rounds 3 > $O/ab_small.log 2>&1 || exit 1
-timeout -k 10 200 python bench.py --steps 20 --warmup 5 > $O/bench_k20.log 2>&1 || exit 1
-timeout -k 10 200 python bench.py > $O/bench.log 2>&1 || exit 1
-timeout -k 10 300 python tools/stamps.py run --scenario corridor > $O/stamps.json 2>&1 || exit 1
-if [ "${TRAFFIC:-0}" = 1 ]; then bash tools/gpu_traffic.sh $(basename $O) > $O/traffic.log 2>&1 || exit 1; fi
+if [ -n "$TAGS" ]; then
+  for scn in ${AB_SCN:-corridor S_corridor}; do
+    timeout -k 10 600 python tools/variants.py run $TAGS --envs 65536 --scenario $scn --rounds 3 > $O/ab_$scn.log 2>&1 || fail ab_$scn $?
+    python - $O/ab_$scn.log <<'PY'
+import json, sys
+t = open(sys.argv[1]).read(); d = json.loads(t[t.index("{"):])
+print(d["scenario"], {k: round(v["ms_per_step_min"] * 1e3, 2) for k, v in d["variants"].items()})
+PY
+  done
+fi
+timeout -k 10 200 python bench.py > $O/bench.log 2>&1 || fail bench $?
+tail -1 $O/bench.log | cut -c1-400
+timeout -k 10 200 python bench.py --steps 20 --warmup 5 > $O/bench_k20.log 2>&1 || fail bench_k20 $?
+if [ "${NOPROF:-0}" != 1 ]; then
+  (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d $R/$O/kt -o kt -- python3 $R/bench.py --no-cpu-baseline > $R/$O/kt.log 2>&1) || fail rocprof $?
+  find $O/kt -name '*kernel_stats.csv' -exec head -5 {} \;
+fi
 exit 0
