@@ -74,7 +74,7 @@ TEST_SCENARIOS = ("perpendicular", "parallel", "S_parallel", "corridor", "S_corr
 CURRICULUM_STAGES = ("stage_1", "stage_2", "stage_3", "stage_4", "stage_5")
 
 # Relative step-kernel cost of each test scenario (us per step at 65 536 envs of that scenario alone,
-# MI355X, DESIGN.md "Every test scenario alone"): the grouped layout deals its 64-env groups over the
+# MI355X, docs/DESIGN_HISTORY.md "Every test scenario alone"): the grouped layout deals its 64-env groups over the
 # CUs by these weights (d2d_set_scenario_costs; placement only, never results).
 SCENARIO_STEP_COST = {"perpendicular": 31.2, "parallel": 31.3, "S_parallel": 43.8, "corridor": 32.4,
                       "S_corridor": 45.1, "large": 41.5, "impossible": 32.4}

@@ -285,7 +285,7 @@ __device__ __forceinline__ double sgn_nz(double x) {
 // rotated unit vectors: state and observation are then bit-identical to that oracle's, so a closed
 // loop (a policy acting on the observations) stays identical to it, episode for episode
 // (tests/test_harness.py).  The default build uses the device library and the cheaper sequences
-// (a few ulp apart; DESIGN.md "Round 5").
+// (a few ulp apart; DESIGN.md "Arithmetic").
 #ifndef D2D_EXACT_TRIG
 #define D2D_EXACT_TRIG 0
 #endif

@@ -91,7 +91,7 @@ StepArgs make_args(const d2d_t* h) {
     a.ist = h->ist;
     a.acc = h->acc;
     a.scn = h->scn;
-    a.brt = h->brt;  // (null in fresh curriculum mode: DESIGN.md "Round 4")
+    a.brt = h->brt;  // (null in fresh curriculum mode: docs/DESIGN_HISTORY.md "Round 4")
     a.env_scn = h->env_scn;
     a.pool_base = h->pool_dev;
     a.pool_n = h->pool_n;

@@ -21,7 +21,7 @@
 //
 // W2's Brent search runs at the highest wave priority.  At 65 536 envs this is 1 024 workgroups = 4
 // per CU = 4 waves per SIMD, one of each role (VGPR <= 128, LDS <= 40 KB); every SIMD then issues
-// VALU work ~87 % of the time (DESIGN.md "What bounds it").  The scenario (+ probe table) is staged
+// VALU work ~87 % of the time (DESIGN.md "What bounds K1").  The scenario (+ probe table) is staged
 // into LDS by LDS-DMA while the waves' first state loads are in flight.  d2d_step_grouped_kernel is
 // the same body over the scenario-grouped slot layout (StepArgs::lane_env).
 //
@@ -54,7 +54,7 @@ constexpr size_t K2_LDS_BUDGET = 64 * 1024;
 // to PRIO_W2_POST once its search is done (the reward terms and waits).
 constexpr int PRIO_W0 = 2, PRIO_W1 = 1, PRIO_W2 = 3, PRIO_W3 = 1, PRIO_W2_POST = 0;
 // (A four-group 1 024-thread "quad" workgroup with host-chosen role -> SIMD placement was measured
-// 2-13 % slower than four 256-thread workgroups and removed in round 4: DESIGN.md.)
+// 2-13 % slower than four 256-thread workgroups and removed in round 4: docs/DESIGN_HISTORY.md.)
 
 struct StepArgs {
     int n;                   // envs
@@ -383,7 +383,7 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const SC* scns, const
     if (S3 && wave == 0) sh.pflags[lane] = 0x7fffffffu;  // W1 and W3 min their table parts in
     // W1..W3 load the pre-step frame before the staging barrier, so its HBM latency overlaps the
     // staging (and every read precedes W0's stores of the new positions).  W0 loads its state after
-    // the barrier: issuing those ~30 loads earlier spilled registers (42 vs 32 us).
+    // the barrier: issuing those ~30 loads earlier spilled registers (42 vs 32 us, docs/DESIGN_HISTORY.md).
     Body PF{};
     if (valid && wave != 0) PF = load_frame(a, i);
     if (qt == 0) {
@@ -1166,7 +1166,7 @@ __global__ __launch_bounds__(256) void d2d_fresh_scan_kernel(FreshArgs f) {
 }
 // K5b: one wave per queued slot generates the scenario in LDS (d2d_curriculum.h) and writes the device
 // table and the ABI record.  (No golden-march tables in fresh mode: built per scenario they cost K5b
-// more than they save K1, DESIGN.md "Round 4".)  It drains the ring from the tail to the head
+// more than they save K1, docs/DESIGN_HISTORY.md "Round 4".)  It drains the ring from the tail to the head
 // (FreshRing) and, after a K1, leaves the head as the next tail.
 __global__ __launch_bounds__(64) void d2d_fresh_gen_kernel(FreshArgs f) {
     __shared__ __attribute__((aligned(16))) GenLds G;

@@ -108,7 +108,7 @@ typedef struct d2d_cfg {
     double reach_end_radius, rew_reach_end;
     double aa_angle, aa_band, rew_aa;  /* AA_angle, AA_band, rew_AA            */
     double force_scale;                /* 1000 (drone_2d_env.py:150)            */
-    double damping;                    /* Space.damping; 1.0    */
+    double damping;                    /* Space.damping; 1.0 (docs/DESIGN_HISTORY.md) */
     int32_t n_steps;                   /* max episode steps (1100)              */
     int32_t use_lambda;                /* use_Lambda                            */
     int32_t auto_reset;                /* 1: SB3 VecEnv auto-reset inside d2d_step */

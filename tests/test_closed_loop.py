@@ -44,7 +44,7 @@ def test_agent_episode_distributions_match_reference(d2, scn):
     (run17see3/res/<scn>/{time_spent,apes,rewards}.npy, tests/golden/agent_17_90_episodes.npz):
     two-sample KS test, p > 1e-3.  The reference's saved rewards were produced with its
     env_train_config reward weights (PP_rew_max 3.5, abs_inv_CA_min_rew 1/6; tools/closed_loop.py
-    --config train vs test, DESIGN.md "Closed loop"), so this run uses those kwargs; the dynamics and
+    --config train vs test, DESIGN.md "Closed-loop parity"), so this run uses those kwargs; the dynamics and
     observations do not depend on them."""
     import numpy as np
     from scipy.stats import ks_2samp

@@ -312,7 +312,7 @@ def test_test_loop_hip_matches_oracle(d2, scn):
     evaluated on the host for both (so both see one action stream).  The contract is statistical,
     not per record (the kernel's bearings, obs 9-18 / 23-26, are rotated unit vectors a few ulp
     from the reference's atan2 / ssa / sincos, so an occasional f32 observation rounds one ulp
-    apart and that closed-loop episode drifts; DESIGN.md "Round 4" item 2).  ``_records_equal``
+    apart and that closed-loop episode drifts; docs/DESIGN_HISTORY.md "Round 4" item 2).  ``_records_equal``
     asserts: >= 98 % of episodes end at the same step with the same collision flag; success / fail
     counts within max(2, 1 %); on the episodes that end alike, flight paths within 1 px on >= 97 %,
     and |APE_hip - APE_oracle| <= that flight's own maximum deviation + 1e-3 px on >= 99 %; total
