@@ -212,3 +212,48 @@ def test_two_rank_ppo_hip_keeps_one_policy(tmp_path, d2):
     """The same with each rank's HIP env shard and the libd2d_ppo.so update kernels (two processes
     on the one GPU; the flat gradient buffer all-reduced over gloo before clip + Adam)."""
     _two_rank_ppo(tmp_path, hip=True)
+
+
+_RCCL_SCRIPT = r'''
+import os, sys
+sys.path.insert(0, os.environ["D2D_REPO"])
+import torch
+import torch.distributed as dist
+import drone2d_amd  # noqa: F401
+from drone2d_amd import shard
+from drone2d_amd.config import ENV_TRAIN_CONFIG
+
+torch.cuda.set_device(0)
+dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+assert dist.get_backend() == "nccl" and dist.get_world_size() == 1
+venv = shard.make_shard_venv(4096, 0, 1, seed=3, with_info=False, **dict(ENV_TRAIN_CONFIG, scenario="corridor"))
+venv.reset()
+for _ in range(120):
+    venv.step(torch.rand(4096, 2, device="cuda") * 2 - 1)
+stats = venv.episode_stats(clear=False).clone()
+before = stats.clone()
+dist.all_reduce(stats, op=dist.ReduceOp.SUM)   # the bench's one collective, on RCCL
+torch.cuda.synchronize()
+assert torch.equal(stats, before) and before[1].item() > 0, (stats, before)
+venv.close()
+dist.destroy_process_group()
+print("RCCL_OK", int(before[1].item()))
+'''
+
+
+@pytest.mark.gpu
+def test_rccl_backend_runs_the_stats_allreduce():
+    """The `nccl` (RCCL) branch of the multi-GPU path on hardware: one rank (RCCL refuses two ranks on
+    one device, and the 8-GPU runs are the driver's) initialises the RCCL process group the way
+    ``shard.init_process_group_from_env`` does and all-reduces a real batch's episode-statistics
+    vector on the device -- the fp64 SUM ``bench.py`` runs over ranks.  With one rank the sum is the
+    vector itself, bit for bit."""
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0", WORLD_SIZE="1",
+               LOCAL_RANK="0", D2D_REPO=repo)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    r = subprocess.run([sys.executable, "-c", _RCCL_SCRIPT], env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0 and "RCCL_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]

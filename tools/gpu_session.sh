@@ -31,4 +31,4 @@ run fresh 600 bash tools/gpu_fresh.sh "$TAG" drone-2d-custom-gym-env-for-reinfor
 run ppo_corridor 600 python tools/train_ppo.py --updates 60
 case "$SKIP" in *" ppo_corridor "*) ;; *) cp gpurun_out/ppo.jsonl "$OUT/ppo_corridor_60.jsonl";; esac
 run ppo_fresh 600 python tools/train_ppo.py --curriculum --pool 0 --updates 100
-cp gpurun_out/ppo.jsonl "$OUT/ppo_fresh_100.jsonl"
+case "$SKIP" in *" ppo_fresh "*) ;; *) cp gpurun_out/ppo.jsonl "$OUT/ppo_fresh_100.jsonl";; esac
