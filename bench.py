@@ -186,6 +186,28 @@ def gpu_clock(card):
     return out or None
 
 
+def valu_budget(bytes_per_launch: float, valu: dict, clk: dict | None, frac: float = 0.40) -> dict:
+    """The VALU-issue budget that ``frac`` of the HBM roof implies (DESIGN.md "What bounds K1"): the
+    launch must last bytes / (frac x peak); at the profiled busy fraction and cycles per VALU
+    instruction (``valu``: the committed VALU profile) and this run's shader clock (``clk``: the
+    line's ``gpu_clock``), that leaves this many VALU wave-instructions per SIMD per launch."""
+    t = bytes_per_launch / (frac * HBM_PEAK_GBS * 1e9)
+    mhz, src = None, None
+    for key in ("after_timed", "before_timed"):
+        c = (clk or {}).get(key) or {}
+        if c.get("pp_dpm_sclk_mhz"):
+            mhz, src = float(c["pp_dpm_sclk_mhz"]), f"sysfs pp_dpm_sclk ({key})"
+            break
+    if mhz is None:
+        mhz, src = 2100.0, "assumed 2.1 GHz (sysfs clock unreadable)"
+    cpi = valu["valu_active_cycles_per_simd"] / valu["valu_insts_per_simd"]
+    budget = t * mhz * 1e6 * valu["valu_busy_frac"] / cpi
+    return {"roof_frac": frac, "launch_us": t * 1e6, "clock_mhz": mhz, "clock_source": src,
+            "busy_frac": valu["valu_busy_frac"], "cycles_per_valu": cpi, "valu_per_simd_budget": budget,
+            "valu_per_simd_profiled": valu["valu_insts_per_simd"],
+            "cut_needed_frac": 1.0 - budget / valu["valu_insts_per_simd"]}
+
+
 def barrier_sync(world):
     if world > 1:
         dist.barrier()
@@ -460,26 +482,7 @@ def main():
                                               "wave_lifetime_cycles", "valu_busy_frac", "source")}
             line["valu"]["profile"] = os.path.relpath(vf, REPO)
             line["valu"]["commit"] = v.get("commit")
-            # the VALU-issue budget the north_star's 40 % of the HBM roof implies (DESIGN.md "Instruction
-            # budget"): the launch must last bytes / (0.4 x peak); at the profiled busy fraction and
-            # cycles per VALU instruction, and this run's shader clock, that leaves this many VALU
-            # wave-instructions per SIMD per launch
-            t40 = bytes_env * n / (0.40 * HBM_PEAK_GBS * 1e9)
-            mhz, src = None, None
-            for key in ("after_timed", "before_timed"):
-                c = (clk or {}).get(key) or {}
-                if c.get("pp_dpm_sclk_mhz"):
-                    mhz, src = c["pp_dpm_sclk_mhz"], f"sysfs pp_dpm_sclk ({key})"
-                    break
-            if mhz is None:
-                mhz, src = 2100.0, "assumed 2.1 GHz (sysfs clock unreadable)"
-            cpi = v["valu_active_cycles_per_simd"] / v["valu_insts_per_simd"]
-            budget = t40 * mhz * 1e6 * v["valu_busy_frac"] / cpi
-            line["valu"]["valu_budget_for_40pct"] = {
-                "launch_us_at_40pct": t40 * 1e6, "clock_mhz": mhz, "clock_source": src,
-                "busy_frac": v["valu_busy_frac"], "cycles_per_valu": cpi,
-                "valu_per_simd_budget": budget, "valu_per_simd_profiled": v["valu_insts_per_simd"],
-                "cut_needed_frac": 1.0 - budget / v["valu_insts_per_simd"]}
+            line["valu"]["valu_budget_for_40pct"] = valu_budget(bytes_env * n, v, clk)
             if v.get("fp64_flops_per_env_step_issued"):
                 # the fp64 co-roofline: fp64 flops per env-step from the committed
                 # rocprofv3 VALU-mix pass x the env-steps this run's kernel did per second

@@ -89,3 +89,37 @@ def test_bench_refuses_more_gpus_than_devices():
     r = subprocess.run([sys.executable, "bench.py", "--gpus", "4", *ARGS], cwd=REPO, env=env,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 2 and "HIP device" in r.stderr
+
+
+def test_gpu_clock_reads_sysfs(tmp_path):
+    """The line's ``gpu_clock``: the current pp_dpm_sclk level (the '*' line) and hwmon freq1_input;
+    None when neither file is readable (no GPU / no amdgpu sysfs)."""
+    sys.path.insert(0, REPO)
+    import bench
+
+    card = tmp_path / "device"
+    (card / "hwmon" / "hwmon3").mkdir(parents=True)
+    (card / "pp_dpm_sclk").write_text("0: 500Mhz\n1: 1600Mhz\n2: 2316Mhz *\n")
+    (card / "hwmon" / "hwmon3" / "freq1_input").write_text("2316000000\n")
+    assert bench.gpu_clock(str(card)) == {"pp_dpm_sclk_mhz": 2316.0, "hwmon_sclk_mhz": 2316.0}
+    (card / "pp_dpm_sclk").write_text("0: 500Mhz\n1: 2100Mhz\n")  # no current level marked
+    assert bench.gpu_clock(str(card)) == {"hwmon_sclk_mhz": 2316.0}
+    assert bench.gpu_clock(str(tmp_path / "nothing")) is None and bench.gpu_clock(None) is None
+
+
+def test_valu_budget_for_40pct():
+    """valu_budget: 40 % of 8 TB/s at 650 B x 65 536 is a 13.312 us launch; at 2.316 GHz, 84.4 % busy
+    and 4.15 cycles per VALU instruction that is ~6.27 k VALU per SIMD (DESIGN.md "What bounds K1");
+    without a readable clock it assumes 2.1 GHz and says so."""
+    sys.path.insert(0, REPO)
+    import bench
+
+    v = {"valu_active_cycles_per_simd": 44556.09375, "valu_insts_per_simd": 10727.45849609375,
+         "valu_busy_frac": 0.8443313720606864}
+    b = bench.valu_budget(650 * 65536, v, {"before_timed": {"pp_dpm_sclk_mhz": 2000.0},
+                                           "after_timed": {"pp_dpm_sclk_mhz": 2316.0}})
+    assert abs(b["launch_us"] - 13.312) < 1e-9 and b["clock_mhz"] == 2316.0 and "after_timed" in b["clock_source"]
+    assert abs(b["valu_per_simd_budget"] - 6267.36) < 0.1
+    assert abs(b["cut_needed_frac"] - (1 - 6267.36 / 10727.458)) < 1e-4
+    b = bench.valu_budget(650 * 65536, v, None)
+    assert b["clock_mhz"] == 2100.0 and "assumed" in b["clock_source"]
