@@ -754,9 +754,22 @@ int32_t d2d_step(d2d_t* h, const float* act_dev, float* obs_dev, float* rew_dev,
     if (fresh_mode(h) && (e = fresh_regen(h, (hipStream_t)stream, false, h->cfg.auto_reset != 0)) !=
                              hipSuccess)
         return hip_fail(e, "d2d_step: fresh scenarios");
-    if (h->cfg.auto_reset && ++h->n_steps % FILL_PERIOD == 0 &&
-        (e = rc_fill(h, (hipStream_t)stream)) != hipSuccess)
-        return hip_fail(e, "d2d_step: cache fill");
+    if (h->cfg.auto_reset && ++h->n_steps % FILL_PERIOD == 0) {
+        // K4's cadence.  A step being captured into a graph launches K4 every FILL_PERIOD steps and
+        // lets the device tick pick every FILL_EVERY-th launch to fill, so replays keep the cadence
+        // whatever the graph's length; an eager step launches only the filling launches (every
+        // FILL_PERIOD x FILL_EVERY steps), saving the two launches per period that would find the tick
+        // says "skip" (~4 us each).  Either way an entry is an optimisation: a reset whose entry is
+        // missing computes the same observation in K1.
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if ((e = hipStreamIsCapturing((hipStream_t)stream, &cs)) != hipSuccess)
+            return hip_fail(e, "d2d_step: capture query");
+        if (cs != hipStreamCaptureStatusNone) {
+            if ((e = rc_fill(h, (hipStream_t)stream)) != hipSuccess) return hip_fail(e, "d2d_step: cache fill");
+        } else if (h->n_steps % (FILL_PERIOD * FILL_EVERY) == 0) {
+            if ((e = rc_fill(h, (hipStream_t)stream, true)) != hipSuccess) return hip_fail(e, "d2d_step: cache fill");
+        }
+    }
     return D2D_OK;
 }
 
