@@ -597,7 +597,8 @@ __device__ __forceinline__ void brent_step(const S& s, const PathK& K, double px
     B.nfc = nnfc;
     B.fnfc = nfnfc;
     B.xf = le ? x : xf;
-    B.fx = le ? fu : fx;
+    B.fx = min_fin(fu, fx);  // == le ? fu : fx (le = fu <= fx; equal values are the same number; the
+                             // distances are NaN only all together, for a NaN point)
 #ifdef D2D_BSTAMP
     BST(4, B.fx);
     const uint64_t act = __ballot(1);
@@ -1191,14 +1192,13 @@ __device__ __forceinline__ void phys_velocities(const Arms& A, const double pos[
             const double v1y = za ? vel[3 * m + 1] : fma(r1x, vel[3 * m + 2], vel[3 * m + 1]);
             const double v2x = fma(-r2y, vel[2], vel[0]), v2y = fma(r2x, vel[2], vel[1]);
             const double ux = bx - (v2x - v1x), uy = by - (v2y - v1y);
-            double jx = fma(ux, ka, uy * kb);
-            double jy = fma(ux, kc, uy * kd);
-            const double ox = j[2 * k], oy = j[2 * k + 1];
-            const double nx = ox + jx, ny = oy + jy;
-            j[2 * k] = nx;
-            j[2 * k + 1] = ny;
-            jx = nx - ox;
-            jy = ny - oy;
+            const double jx = fma(ux, ka, uy * kb);
+            const double jy = fma(ux, kc, uy * kd);
+            // jAcc += j.  Chipmunk clamps the sum to max_force * dt and applies the difference
+            // jAcc_new - jAcc_old; max_force = inf makes the clamp the identity, so that difference is
+            // j up to the rounding of the round trip, and j itself is applied (the oracle likewise)
+            j[2 * k] = j[2 * k] + jx;
+            j[2 * k + 1] = j[2 * k + 1] + jy;
             vel[3 * m + 0] = fma(-jx, MI_M, vel[3 * m + 0]);
             vel[3 * m + 1] = fma(-jy, MI_M, vel[3 * m + 1]);
             if (!za) vel[3 * m + 2] = fma(II_M, fma(r1x, -jy, -(r1y * (-jx))), vel[3 * m + 2]);

@@ -395,12 +395,11 @@ static int o_space_step(const d2d_cfg* cfg, const d2d_scn* scn, double* st, doub
             double ux = j->bx - (v2x - v1x), uy = j->by - (v2y - v1y);
             double jx = fma(ux, j->ka, uy * j->kb);
             double jy = fma(ux, j->kc, uy * j->kd);
-            double ox = st[D2D_S_J + 2 * k], oy = st[D2D_S_J + 2 * k + 1];
-            double nx = ox + jx, ny = oy + jy;
-            st[D2D_S_J + 2 * k] = nx;
-            st[D2D_S_J + 2 * k + 1] = ny;
-            jx = nx - ox;
-            jy = ny - oy;
+            /* jAcc = cpvclamp(jAcc + j, max_force * dt) is jAcc + j (max_force = inf); Chipmunk then
+               applies jAcc_new - jAcc_old, which is j up to the round trip's rounding: j is applied
+               (the kernels' contraction of the step, DESIGN.md "Arithmetic") */
+            st[D2D_S_J + 2 * k] = st[D2D_S_J + 2 * k] + jx;
+            st[D2D_S_J + 2 * k + 1] = st[D2D_S_J + 2 * k + 1] + jy;
             apply_imp(a, -jx, -jy, j->r1x, j->r1y);
             apply_imp(b, jx, jy, j->r2x, j->r2y);
         }
