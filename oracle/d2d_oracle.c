@@ -23,7 +23,11 @@
  *
  * Floating point follows the reference's NumPy evaluation order exactly.  Compiled with
  * -ffp-contract=off; the two places where NumPy itself fuses (np.linalg.norm of a 2-vector and a
- * 2x2 np.matmul, both through OpenBLAS) use explicit fma() in the same order NumPy does.
+ * 2x2 np.matmul, both through OpenBLAS) use explicit fma() in the same order NumPy does.  The
+ * Chipmunk step (parity unpinned) is written the way libdrone2d_hip.so computes it: every a + b*c as
+ * one fma() and the sweep's impulse applied directly (o_space_step), so the kernels match this file
+ * as closely as before; tests/test_oracle_golden.py bounds its distance to the unfused Python
+ * restatement the golden vectors hold.
  */
 #include "d2d_oracle.h"
 
