@@ -478,14 +478,21 @@ __device__ __forceinline__ bool brent_open(const Brent& B) {
     return fabs(B.xf - xm) > (tol2 - 0.5 * (B.b - B.a));
 }
 __device__ __forceinline__ bool brent_active(const Brent& B) { return brent_open(B) & (B.num < 500); }
+// One scipy iteration in its two halves: brent_cand = the candidate probe of the next step (it sets
+// B.e and B.rat exactly as scipy's iteration does before the evaluation), brent_update = the decision
+// on the evaluated probe.  brent_step = cand + evaluation + update.  (A speculative search built on
+// the split -- a second probe per pass, the next step's under the last decision -- was bit-exact but
+// slower everywhere it was tried: DESIGN.md "Curriculum".)
+struct BrCand {
+    double x;
+    int ix;
+};
+template <bool KN, class S>
+__device__ __forceinline__ int brent_interval(const S& s, const PathK& K, const Brent& B, double x, double ka,
+                                              double* kn);
 // KN: the knot scan reads the lane's knots staged in LDS at kn (global-memory tables, closest_u)
 template <bool KN = false, class S>
-__device__ __forceinline__ void brent_step(const S& s, const PathK& K, double px, double py, Brent& B,
-                                           double* kn = nullptr BST_ARG) {
-#ifdef D2D_BSTAMP
-    uint64_t bst_t[5];
-#endif
-    BST(0, B.xf);
+__device__ __forceinline__ BrCand brent_cand(const S& s, const PathK& K, Brent& B, double* kn = nullptr) {
     const double a = B.a, b = B.b, xf = B.xf, fx = B.fx, nfc = B.nfc, fulc = B.fulc;
     // the upper knot of a's interval, for the one-compare interval test: re-read from a staged (LDS)
     // table; carried in the state (B.ka, B.kxf, from the records the probes already read) when the
@@ -528,7 +535,12 @@ __device__ __forceinline__ void brent_step(const S& s, const PathK& K, double px
     // (rat is never -0: e_g = a - xf or b - xf is +0 at worst, the parabolic step is p + 0.0 over
     // |q| or tol1 times a nonzero sign, so copysign gives the same -mx / +mx)
     const double x = xf + copysign(mx, rat);
-    BST(1, x);
+    return BrCand{x, brent_interval<KN>(s, K, B, x, ka, kn)};
+}
+// the knot interval of a probe x in [B.a, B.b] (ka = us[B.ia + 1])
+template <bool KN, class S>
+__device__ __forceinline__ int brent_interval(const S& s, const PathK& K, const Brent& B, double x, double ka,
+                                              double* kn) {
     // knot interval of x: one compare once the bracket spans <= 2 intervals (wave-uniform choice).
     // x is always in [a, b], so the choice depends on the bracket alone -- known at the step's start,
     // which takes the branch off the step's dependency chain (a branch on a just-computed condition
@@ -562,12 +574,15 @@ __device__ __forceinline__ void brent_step(const S& s, const PathK& K, double px
             ix = u_index(*sp, x);
         }
     }
-    BST(2, ix);
-    // (a per-lane LDS cache of the probe's interval record for global-memory tables measured slower:
-    // fresh K1 80.5 vs 77.7 us, profiles/r05/a/ -- some lane of the wave misses on most early steps)
-    double kx;
-    const double fu = path_dist_n(s, K, x, ix, px, py, kx);
-    BST(3, fu);
+    return ix;
+}
+// the decision on probe c (value fu, kx = us[c.ix + 1] from its record); returns le (the probe is not
+// worse than xf)
+template <class S>
+__device__ __forceinline__ bool brent_update(Brent& B, const BrCand& c, double fu, double kx) {
+    const double a = B.a, b = B.b, xf = B.xf, fx = B.fx, nfc = B.nfc, fulc = B.fulc;
+    const double x = c.x;
+    const int ix = c.ix;
     // (num, scipy's maxfun count, is not advanced here: brent_run derives it from its pass count)
     const bool le = fu <= fx;
     const bool c1 = !le & ((fu <= B.fnfc) | (nfc == xf));
@@ -599,6 +614,25 @@ __device__ __forceinline__ void brent_step(const S& s, const PathK& K, double px
     B.xf = le ? x : xf;
     B.fx = min_fin(fu, fx);  // == le ? fu : fx (le = fu <= fx; equal values are the same number; the
                              // distances are NaN only all together, for a NaN point)
+    return le;
+}
+template <bool KN = false, class S>
+__device__ __forceinline__ void brent_step(const S& s, const PathK& K, double px, double py, Brent& B,
+                                           double* kn = nullptr BST_ARG) {
+#ifdef D2D_BSTAMP
+    uint64_t bst_t[5];
+#endif
+    BST(0, B.xf);
+    const bool fast = B.ib <= B.ia + 1;
+    const BrCand c = brent_cand<KN>(s, K, B, kn);
+    BST(1, c.x);
+    BST(2, c.ix);
+    // (a per-lane LDS cache of the probe's interval record for global-memory tables measured slower:
+    // fresh K1 80.5 vs 77.7 us, profiles/r05/a/ -- some lane of the wave misses on most early steps)
+    double kx;
+    const double fu = path_dist_n(s, K, c.x, c.ix, px, py, kx);
+    BST(3, fu);
+    brent_update<S>(B, c, fu, kx);
 #ifdef D2D_BSTAMP
     BST(4, B.fx);
     const uint64_t act = __ballot(1);
@@ -608,6 +642,8 @@ __device__ __forceinline__ void brent_step(const S& s, const PathK& K, double px
         bst[6] = (uint64_t)(__ballot(!fast) != 0ull);
         bst[7] = (uint64_t)__popcll(act);
     }
+#else
+    (void)fast;
 #endif
 }
 // scipy's `while` loop (maxfun = 500 included).  A lane takes one step per pass of the wave's loop

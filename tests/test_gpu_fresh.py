@@ -271,3 +271,27 @@ def test_fresh_graph_replay_keeps_every_slot(d2):
     assert bytes(venv.scenario_table()) == bytes(b.scenario_table())
     venv.close()
     b.close()
+
+
+def test_fresh_search_bitwise(d2):
+    """The fresh curriculum's closest-point search -- scipy's fminbound over each lane's own tables
+    in global memory, run speculatively in K1's path wave (two probes per pass, csrc/d2d_device.h
+    brent_run_spec) -- gives the oracle's closest and lookahead points (obs 19..22) and path error
+    bit for bit, teacher-forced every step, across auto-resets and the stage 4 -> 5 change."""
+    from drone2d_amd import abi
+    from parity_util import sync_oracle
+
+    n, rng = 4096, np.random.default_rng(8)
+    venv, orc = _pair(d2, n, 23, _kw(sim_num=1990000))
+    dones = 0
+    for t in range(60):
+        sync_oracle(venv, orc)
+        act = rng.uniform(-1, 1, (n, 2)).astype(np.float32)
+        obs = venv.step(torch.as_tensor(act, device=venv.device))[0].cpu().numpy()
+        o_obs, _, o_term, _, _ = orc.step(act)
+        np.testing.assert_array_equal(obs[:, 19:23], o_obs[:, 19:23])
+        st, o_st = venv.get_state()[0].cpu().numpy(), orc.get_state()[0]
+        np.testing.assert_array_equal(st[abi.S_PATH_ERR], o_st[abi.S_PATH_ERR])
+        dones += int(o_term.sum())
+    assert dones > 50
+    venv.close()

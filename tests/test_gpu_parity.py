@@ -405,23 +405,24 @@ def test_device_math_selftest(d2, which):
     assert bad.value == 0
 
 
-def test_closest_point_grid_bitwise(d2):
+@pytest.mark.parametrize("per,gn", [(8192, 64), (512, 16)])
+def test_closest_point_grid_bitwise(d2, per, gn):
     """Brent closest-point search over the whole plane and around every path, all 7 scenarios:
     the golden-march tables (golden-left / golden-right prefixes, resume at the first differing
     step) must give exactly the probe sequence of the plain search, so the closest / lookahead
     points (obs 19..22) and the accumulated path error are bit-identical to the C oracle (grouped
-    layout: every 64-env group stages its scenario and probe table)."""
+    layout: every 64-env group stages its scenario and probe table).  per = 512 (56 workgroups, fewer
+    than CUs): the small-batch launch, whose continuation runs speculatively (brent_run_spec)."""
     from drone2d_amd import abi
 
-    per = 8192
     n = per * len(SCENARIOS)
     venv, orc = make_pair(d2, n, SCENARIOS, seed=5, kwargs=_cfgkw(), env_scenario=np.repeat(np.arange(7), per),
                           auto_reset=False)
     rng = np.random.default_rng(11)
     pts = []
     for s in venv.scenarios:
-        g = np.linspace(-600.0, 1900.0, 64)
-        grid = np.stack(np.meshgrid(g, g), -1).reshape(-1, 2)  # 4096: behind, beyond, around the path
+        g = np.linspace(-600.0, 1900.0, gn)
+        grid = np.stack(np.meshgrid(g, g), -1).reshape(-1, 2)  # gn^2: behind, beyond, around the path
         L = float(s.path.us[-1])
         u = rng.uniform(-10.0, L + 10.0, per - len(grid))
         near = np.array([s.path(x) for x in u]) + rng.normal(0.0, 40.0, (len(u), 2))  # parabolic searches

@@ -41,8 +41,9 @@ def fminbound_log(f, x1, x2, xatol=1e-6, maxfun=500):
     xm = 0.5 * (a + b)
     tol1 = SQRT_EPS * abs(xf) + xatol / 3.0
     tol2 = 2.0 * tol1
-    log = []  # (par, le) per step
+    log = []  # (par, le, plain worse, speculation possible before the step) per step
     while abs(xf - xm) > (tol2 - 0.5 * (b - a)):
+        spec_ok = (nfc != xf) and (fulc != xf) and (fulc != nfc)
         golden = True
         par = False
         if abs(e) > tol1:
@@ -73,6 +74,7 @@ def fminbound_log(f, x1, x2, xatol=1e-6, maxfun=500):
         fu = f(x)
         num += 1
         le = fu <= fx
+        plain_worse = (not le) and not (fu <= fnfc) and not (fu <= ffulc)
         if le:
             if x >= xf:
                 a = xf
@@ -91,7 +93,9 @@ def fminbound_log(f, x1, x2, xatol=1e-6, maxfun=500):
                 nfc, fnfc = x, fu
             elif (fu <= ffulc) or (fulc == xf) or (fulc == nfc):
                 fulc, ffulc = x, fu
-        log.append((par, le))
+        if log:  # the previous step's "better" speculation held iff it was better and this step is golden
+            log[-1] = log[-1][:4] + (log[-1][1] and not par,)
+        log.append((par, le, plain_worse, spec_ok, False))
         xm = 0.5 * (a + b)
         tol1 = SQRT_EPS * abs(xf) + xatol / 3.0
         tol2 = 2.0 * tol1
@@ -106,10 +110,36 @@ def table_dev(log, kind_len):
     kind = 1 if log and log[0][1] else 0
     n = kind_len[kind]
     for k in range(1, min(len(log), n)):
-        par, le = log[k]
+        par, le = log[k][:2]
         if par or not le:
             return kind, k
     return kind, min(len(log), n)
+
+
+def spec_iterations(steps, mode="worse"):
+    """Wave-loop passes a lane needs for `steps` (log entries) when every pass evaluates the step's
+    probe AND, speculatively, the next step's probe under the assumption that this step's new probe
+    is "plain worse" (not better, no nfc / fulc update: the next probe then depends on the bracket
+    alone); a pass whose assumption holds completes two steps."""
+    it = k = 0
+    prev_better = False
+    while k < len(steps):
+        par, le, pw, ok, bg = steps[k]
+        it += 1
+        w_hit = ok and pw
+        b_hit = bg
+        if mode == "worse":
+            hit = w_hit
+        elif mode == "better":
+            hit = b_hit
+        elif mode == "predict":   # the previous step's outcome picks the speculation
+            hit = b_hit if prev_better else w_hit
+        else:                     # both (three probes per pass)
+            hit = w_hit or b_hit
+        hit = hit and k + 1 < len(steps)
+        prev_better = steps[k + 1][1] if hit else le
+        k += 2 if hit else 1
+    return it
 
 
 def main():
@@ -183,12 +213,14 @@ def main():
         cont = log[dev:] if dev < len(log) else []
         # trailing run of golden-worse steps in the continuation
         tail = 0
-        for par, le in reversed(cont):
+        for par, le, *_ in reversed(cont):
             if par or le:
                 break
             tail += 1
         rows.append(dict(n=len(log), kind=kind, dev=dev, cont=len(cont), tail=tail,
-                         par=sum(p for p, _ in cont), gw=sum((not p) and (not l) for p, l in cont)))
+                         par=sum(x[0] for x in cont), gw=sum((not x[0]) and (not x[1]) for x in cont),
+                         **{f"cont_{m}": spec_iterations(cont, m) for m in ("worse", "better", "predict", "both")},
+                         **{f"full_{m}": spec_iterations(log, m) for m in ("worse", "better", "predict", "both")}))
     C = np.array([r["cont"] for r in rows])
     T = np.array([r["tail"] for r in rows])
     waves = C.reshape(-1, 64)
@@ -216,6 +248,11 @@ def main():
         "wave_max_without_golden_tail": float(notail.mean()),
         "par_frac_of_cont": float(sum(r["par"] for r in rows) / max(1, C.sum())),
         "golden_worse_frac_of_cont": float(sum(r["gw"] for r in rows) / max(1, C.sum())),
+        # speculative next-probe evaluation (spec_iterations): wave-max passes of the continuation
+        # (tables) and of the whole search (no tables: the fresh curriculum's plain search)
+        "wave_full_max_mean": float(np.array([r["n"] for r in rows]).reshape(-1, 64).max(1).mean()),
+        **{f"wave_{p}_max_spec_{m}": float(np.array([r[f"{p}_{m}"] for r in rows]).reshape(-1, 64).max(1).mean())
+           for p in ("cont", "full") for m in ("worse", "better", "predict", "both")},
     }
     print(json.dumps(res, indent=1))
     if args.out:
