@@ -169,6 +169,7 @@ def gpu_clock(card):
     if card is None:
         return None
     out = {}
+    t0 = time.perf_counter()
     try:
         for line in open(os.path.join(card, "pp_dpm_sclk")):
             if "*" in line:
@@ -183,6 +184,8 @@ def gpu_clock(card):
             break
         except (OSError, ValueError):
             pass
+    if out:
+        out["read_ms"] = round((time.perf_counter() - t0) * 1e3, 3)
     return out or None
 
 
