@@ -92,8 +92,8 @@ def test_bench_refuses_more_gpus_than_devices():
 
 
 def test_gpu_clock_reads_sysfs(tmp_path):
-    """The line's ``gpu_clock``: the current pp_dpm_sclk level (the '*' line) and hwmon freq1_input;
-    None when neither file is readable (no GPU / no amdgpu sysfs)."""
+    """The line's ``gpu_clock``: the current pp_dpm_sclk level (the '*' line) and hwmon freq1_input,
+    plus how long the reads took; None when neither file is readable (no GPU / no amdgpu sysfs)."""
     sys.path.insert(0, REPO)
     import bench
 
@@ -101,9 +101,11 @@ def test_gpu_clock_reads_sysfs(tmp_path):
     (card / "hwmon" / "hwmon3").mkdir(parents=True)
     (card / "pp_dpm_sclk").write_text("0: 500Mhz\n1: 1600Mhz\n2: 2316Mhz *\n")
     (card / "hwmon" / "hwmon3" / "freq1_input").write_text("2316000000\n")
-    assert bench.gpu_clock(str(card)) == {"pp_dpm_sclk_mhz": 2316.0, "hwmon_sclk_mhz": 2316.0}
+    c = bench.gpu_clock(str(card))
+    assert c.pop("read_ms") >= 0.0 and c == {"pp_dpm_sclk_mhz": 2316.0, "hwmon_sclk_mhz": 2316.0}
     (card / "pp_dpm_sclk").write_text("0: 500Mhz\n1: 2100Mhz\n")  # no current level marked
-    assert bench.gpu_clock(str(card)) == {"hwmon_sclk_mhz": 2316.0}
+    c = bench.gpu_clock(str(card))
+    assert c.pop("read_ms") >= 0.0 and c == {"hwmon_sclk_mhz": 2316.0}
     assert bench.gpu_clock(str(tmp_path / "nothing")) is None and bench.gpu_clock(None) is None
 
 
