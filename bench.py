@@ -461,7 +461,10 @@ def main():
                                   + (", info f32[N,12]" if args.info else " (info rows off)")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": "d2d_step_kernel + d2d_fill_kernel/16 (per step)", "kernel_ms": kern_ms,
+                         "kernel": ("d2d_step_kernel + d2d_fill_kernel (every 16th step, filling every 3rd) per "
+                                    "step, graph replay" if hipgraph else
+                                    "d2d_step_kernel + d2d_fill_kernel (every 48th step) per step, eager"),
+                         "kernel_ms": kern_ms,
                          "bytes_per_env_step": bytes_env},
             "episodes": {"finished": float(st[1]), "mean_return": float(st[0] / max(st[1], 1)),
                          "success": float(st[2]), "fails": float(st[3]), "collisions": float(st[4]),
