@@ -287,6 +287,11 @@ __device__ __forceinline__ int next_scenario(const StepArgs& a, int j, uint32_t 
 //   f_rp    W2 -> W0        the position / path terms of the reward (W0 sums the reward: the physics
 //                           wave ends last at full load, so the sum waits for no other wave)
 //   f_ver   W3 -> W2        first differing step in the second half of the table re-check
+//   f_acc   W3 -> W0        the finished episodes' accumulators and the running path error / return
+//                           are in LDS (W0's epilogue)
+//   n_tile  W0..W3 -> W1..W3  count of waves whose obs-tile rows are written: W1-W3 store the tile
+//                           once all four are, while W0 finishes the reward and its bookkeeping
+//                           (no workgroup barrier: the tile store does not wait for the reward sum)
 struct K1Shared {
     double cas[6][EPB];       // W1 -> W0, W2: CAStatic (d, os, oc, lpa, lca, rr)
     int scn[EPB];             // scenario index per env
@@ -297,7 +302,7 @@ struct K1Shared {
     uint32_t ep[EPB];         // W0 -> W1, W3: episode counter (the state's copy changes at a reset)
     double sina[EPB];         // W0 -> W2: sin of the post-step frame angle (AA reward)
     uint32_t w0t[EPB], w0fl[EPB];  // W0 -> W0: the step counter t and the flags, for after the joint sweep
-    uint32_t f_done, f_ca, f_gs, f_rp, f_ver, f_ver1;
+    uint32_t f_done, f_ca, f_gs, f_rp, f_ver, f_ver1, f_acc, n_tile;
     double pe[2][EPB];        // W3 -> W0: path_err, total_reward (prefetched for the epilogue)
     double acc[D2D_NSTATS][EPB];  // W3 -> W0: episode accumulators of envs that end (prefetched)
     union {
@@ -325,6 +330,15 @@ __device__ __forceinline__ void flag_raise(uint32_t& f) {
 }
 __device__ __forceinline__ void flag_wait(const uint32_t& f) {
     while (!flag_seen(f)) __builtin_amdgcn_s_sleep(1)  /* 64 cycles between polls */;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+// the obs-tile count: a wave's rows are written (release), and the wait for all `n` waves (acquire)
+__device__ __forceinline__ void tile_arrive(uint32_t& c) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if ((threadIdx.x & 63) == 0) atomicAdd(&c, 1u);
+}
+__device__ __forceinline__ void tile_wait(const uint32_t& c, uint32_t n) {
+    while (__builtin_amdgcn_readfirstlane(*(const volatile LdsU32*)&c) < n) __builtin_amdgcn_s_sleep(1);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
@@ -393,6 +407,8 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const SC* scns, const
         sh.f_rp = 0u;
         sh.f_ver = 0u;
         sh.f_ver1 = 0u;
+        sh.f_acc = 0u;
+        sh.n_tile = 0u;
     }
     __syncthreads();
     STAMP(1);
@@ -509,6 +525,7 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const SC* scns, const
                 trw[18] = (float)ov[18];
             }
         }
+        tile_arrive(sh.n_tile);
         // velocity part of the reward (speed, velocity angle, CA total), for W2
         flag_wait(sh.f_ca);
         STAMP(5);
@@ -618,6 +635,7 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const SC* scns, const
                 for (int k = 3; k < 17; ++k) orow[k] = row[k];
             }
         }
+        tile_arrive(sh.n_tile);
     } else if (wave == 2) {
         // ---------------------------------------------------------------- path search (critical)
         // the critical path, so it wins issue arbitration on its SIMD
@@ -686,6 +704,7 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const SC* scns, const
             sh.u.p.post[6][lane] = RP.reach;
         }
         flag_raise(sh.f_rp);
+        tile_arrive(sh.n_tile);
         STAMP(5);
     } else {
         // ---------------------------------------------------------------- auto-reset observation
@@ -724,6 +743,7 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const SC* scns, const
 #pragma unroll
             for (int k = 0; k < D2D_NSTATS; ++k) sh.acc[k][lane] = fld(a.acc, k, n, i);
         }
+        flag_raise(sh.f_acc);
         if (valid && done && auto_reset) {
             // the next episode: spawn state, reset observation (cached or computed), new state
             const uint32_t ep = sh.ep[lane];
@@ -777,34 +797,43 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const SC* scns, const
 #pragma unroll
             for (int k = 0; k < 8; ++k) orow[19 + k] = (float)po[k];
         }
+        tile_arrive(sh.n_tile);
     }
     STAMP(2);
-    __syncthreads();
-    STAMP(3);
 
     // ---------------------------------------------------------------- epilogue
-    // obs tile: rows [e0, e0+rows) are one contiguous span of global memory (grouped: one
-    // contiguous 108-byte row per env)
-    if (GRP) {
-        for (int k = qt; gvalid && k < EPB * D2D_OBS_DIM; k += K1_THREADS) {
-            const int r = k / D2D_OBS_DIM;
-            const int e = a.lane_env[e0 + r];
-            if (e >= 0) a.obs[(size_t)e * D2D_OBS_DIM + (k - r * D2D_OBS_DIM)] = sh.u.p.obs[k];
+    // W1-W3 store the obs tile once every wave's rows are in it; W0 meanwhile takes the reward sum
+    // (above) and writes the bookkeeping (below).  Rows [e0, e0+rows) are one contiguous span of
+    // global memory (grouped: one contiguous 108-byte row per env).
+    if (wave != 0) {
+        tile_wait(sh.n_tile, 4u);
+        STAMP(3);
+        constexpr int TT = K1_THREADS - 64;  // the storing threads
+        const int tq = qt - 64;
+        if (GRP) {
+            for (int k = tq; gvalid && k < EPB * D2D_OBS_DIM; k += TT) {
+                const int r = k / D2D_OBS_DIM;
+                const int e = a.lane_env[e0 + r];
+                if (e >= 0) a.obs[(size_t)e * D2D_OBS_DIM + (k - r * D2D_OBS_DIM)] = sh.u.p.obs[k];
+            }
+        } else {
+            const int rows = gvalid ? max(0, min(EPB, a.n - e0)) : 0;
+            const int words = rows * D2D_OBS_DIM;
+            float* dst = a.obs + (size_t)e0 * D2D_OBS_DIM;
+            // a full tile is 64 x 27 floats = 432 float4 at a 16-B aligned offset (e0 * 108 B, e0 % 64
+            // == 0; the caller's obs buffer is a torch allocation): 16-byte stores
+            int k0 = 0;
+            if (rows == EPB && ((uintptr_t)a.obs & 15u) == 0) {
+                float4* d4 = reinterpret_cast<float4*>(dst);
+                const float4* s4 = reinterpret_cast<const float4*>(sh.u.p.obs);
+                for (int k = tq; k < words / 4; k += TT) d4[k] = s4[k];
+                k0 = words;
+            }
+            for (int k = k0 + tq; k < words; k += TT) dst[k] = sh.u.p.obs[k];
         }
     } else {
-        const int rows = gvalid ? max(0, min(EPB, a.n - e0)) : 0;
-        const int words = rows * D2D_OBS_DIM;
-        float* dst = a.obs + (size_t)e0 * D2D_OBS_DIM;
-        // a full tile is 64 x 27 floats = 432 float4 at a 16-B aligned offset (e0 * 108 B, e0 % 64
-        // == 0; the caller's obs buffer is a torch allocation): 16-byte stores
-        int k0 = 0;
-        if (rows == EPB && ((uintptr_t)a.obs & 15u) == 0) {
-            float4* d4 = reinterpret_cast<float4*>(dst);
-            const float4* s4 = reinterpret_cast<const float4*>(sh.u.p.obs);
-            for (int k = qt; k < words / 4; k += K1_THREADS) d4[k] = s4[k];
-            k0 = words;
-        }
-        for (int k = k0 + qt; k < words; k += K1_THREADS) dst[k] = sh.u.p.obs[k];
+        flag_wait(sh.f_acc);
+        STAMP(3);
     }
     const int lne = lane_fresh(), ile = e0 + lne, iee = GRP ? ie : ile;
     const bool vle = gvalid && (GRP ? iee >= 0 : ile < a.n);
