@@ -54,10 +54,11 @@ def test_golden_teacher_forced(d2, which):
 
 
 @pytest.mark.parametrize("scn,n", [("corridor", 2048), ("S_corridor", 2048), ("large", 2048), ("mixed", 2048),
-                                   ("corridor_free", 4096)])
+                                   ("corridor_free", 4096), ("corridor", 1000)])
 def test_vs_oracle_teacher_forced(d2, scn, n):
     """HIP vs oracle with auto-reset, teacher-forced every step.  corridor_free at 4 096 envs is
-    BASELINE configs[1] (no obstacles: obs 8..16 = (1, 0, 0) x 3, CA = 0)."""
+    BASELINE configs[1] (no obstacles: obs 8..16 = (1, 0, 0) x 3, CA = 0); 1 000 envs end in a
+    40-env workgroup (the obs tile's partial store)."""
     scenarios = SCENARIOS if scn == "mixed" else [scn]
     venv, orc = make_pair(d2, n, scenarios, seed=99, kwargs=_cfgkw())
     rng = np.random.default_rng(1)
