@@ -12,12 +12,12 @@
 //   W1  sensor part (obs 3..16, CA inputs); for envs that end: the spawn-state sensor part
 //   W2  path role: Brent closest point through the golden-march tables (steps [1, bt_split) of the
 //       table re-check), obs 19..26, the position / path terms of the reward while the physics wave
-//       finishes, then the sum
+//       finishes (W0 takes the sum)
 //   W3  steps [bt_split, len) of W2's table re-check; then, for envs that end, the
 //       spawn state and the spawn-state path part
 //   (W1 and W3 take the spawn-state parts from the auto-reset observation cache when it is ready)
-//   epilogue (after the one barrier): the 64x27 f32 obs tile is stored as one contiguous span;
-//   W0 writes reward / flags / info / bookkeeping / auto-reset state.
+//   epilogue (no barrier: an LDS count of the waves whose rows are written): W1-W3 store the 64x27
+//   f32 obs tile as one contiguous span; W0 writes reward / flags / info / bookkeeping.
 //
 // W2's Brent search runs at the highest wave priority.  At 65 536 envs this is 1 024 workgroups = 4
 // per CU = 4 waves per SIMD, one of each role (VGPR <= 128, LDS <= 40 KB); every SIMD then issues
@@ -373,8 +373,8 @@ constexpr int K1_KN_BYTES = D2D_MAX_WPS * 64 * 8;
 // One env step for the 64 envs of group wg (slots [64 wg, 64 wg + 64)) by the calling wave in role `role` (0..3, wave-uniform); qt =
 // 64 role + lane, the thread's index among the group's 256.  scns / hots: the scenario and probe
 // tables indexed by global scenario id (LDS when staged: LDS / LTAB), s0 the group's scenario.
-// All 256 threads of the group call it once; the workgroup's barriers are block-wide, so every
-// wave of the block runs k1_body exactly once.
+// All 256 threads of the group call it once; the staging barrier is block-wide, so every wave of
+// the block runs k1_body exactly once.
 template <bool LDS, bool LTAB, bool GRP, bool S3, class SC>
 __device__ __forceinline__ void k1_body(const StepArgs& a, const SC* scns, const BtHot* hots, int s0, K1Shared& sh,
                                         int wg, int role, int qt) {
