@@ -540,6 +540,15 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const SC* scns, const
             RV = reward_vel(a.cfg, ov, C);
             dclose = C.d;
         }
+        // at full load: W3's prefetched path error / return (long ready) read before the wait on
+        // W2, so the epilogue after it starts from registers (corridor 26.68 -> 26.49 us per step;
+        // with one workgroup per CU, where W3 first takes a third of the table re-check, the
+        // epilogue reads them: 20.29 vs 20.73 us at 4 096 envs)
+        if (!S3) {
+            flag_wait(sh.f_acc);
+            path_err = sh.pe[0][lane_fresh()];
+            tot_rew = sh.pe[1][lane_fresh()];
+        }
         // the reward: W2's position / path terms (usually long ready: the physics chain ends last)
         flag_wait(sh.f_rp);
         if (vw) {
@@ -832,15 +841,17 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const SC* scns, const
             for (int k = k0 + tq; k < words; k += TT) dst[k] = sh.u.p.obs[k];
         }
     } else {
-        flag_wait(sh.f_acc);
+        if (S3) flag_wait(sh.f_acc);  // (at full load W0 waited for it before the reward)
         STAMP(3);
     }
     const int lne = lane_fresh(), ile = e0 + lne, iee = GRP ? ie : ile;
     const bool vle = gvalid && (GRP ? iee >= 0 : ile < a.n);
     if (wave == 0 && vle) {
         const int lane = lne, i = ile, ie = iee;
-        path_err = sh.pe[0][lane];
-        tot_rew = sh.pe[1][lane];
+        if (S3) {
+            path_err = sh.pe[0][lane];
+            tot_rew = sh.pe[1][lane];
+        }
         flags = (flags & ~D2D_FLAG_LA_LOCK) | sh.pflags[lane];
         const double reward = rew_sum;
         path_err += sh.u.p.post[3][lane];
