@@ -422,7 +422,8 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const SC* scns, const
     int t = 0, cause = 0;
     uint32_t flags = 0;
     RewardVel RV{};
-    double dclose = 0.0, rew_sum = 0.0, rew_pp = 0.0;
+    double dclose = 0.0, rew_sum = 0.0, rew_pp = 0.0, pdist = 0.0;
+    uint32_t plal = 0;                  // W2's LA-lock bit
     bool done = false;
     if (wave == 0) {
         // ---------------------------------------------------------------- physics
@@ -546,8 +547,9 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const SC* scns, const
         // epilogue reads them: 20.29 vs 20.73 us at 4 096 envs)
         if (!S3) {
             flag_wait(sh.f_acc);
-            path_err = sh.pe[0][lane_fresh()];
-            tot_rew = sh.pe[1][lane_fresh()];
+            const int lp = lane_fresh();
+            path_err = sh.pe[0][lp];
+            tot_rew = sh.pe[1][lp];
         }
         // the reward: W2's position / path terms (usually long ready: the physics chain ends last)
         flag_wait(sh.f_rp);
@@ -560,6 +562,10 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const SC* scns, const
             RQ.ls = sh.u.p.post[0][ln];
             RQ.lc = sh.u.p.post[1][ln];
             RQ.pa = sh.u.p.post[2][ln];
+            if (!GRP) {  // (read with the other terms; the grouped kernel measured 1.5 % slower so)
+                pdist = sh.u.p.post[3][ln];
+                plal = sh.pflags[ln];
+            }
             const RewardSum Q = reward_sum(a.cfg, RP, RV, RQ);
             rew_sum = Q.reward;
             rew_pp = Q.pp;
@@ -852,10 +858,11 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const SC* scns, const
             path_err = sh.pe[0][lane];
             tot_rew = sh.pe[1][lane];
         }
-        flags = (flags & ~D2D_FLAG_LA_LOCK) | sh.pflags[lane];
+        flags = (flags & ~D2D_FLAG_LA_LOCK) | (GRP ? sh.pflags[lane] : plal);
         const double reward = rew_sum;
-        path_err += sh.u.p.post[3][lane];
-        const double ape = path_err / (double)t;
+        path_err += GRP ? sh.u.p.post[3][lane] : pdist;
+        // (the grouped kernel divides here; the env-ordered one only for the envs that end)
+        const double ape_g = GRP ? path_err / (double)t : 0.0;
         tot_rew += reward;
         bool trunc = false, term = done;
         if (a.cfg.timeup_truncates && done && cause == D2D_END_TIMEUP) {
@@ -877,22 +884,25 @@ __device__ __forceinline__ void k1_body(const StepArgs& a, const SC* scns, const
             r[D2D_INFO_DCLOSE] = (float)dclose;
             r[D2D_INFO_STEPS] = (float)t;
             r[D2D_INFO_CAUSE] = (float)cause;
-            r[D2D_INFO_APE] = done ? (float)ape : 0.0f;
+            r[D2D_INFO_APE] = done ? (float)(GRP ? ape_g : path_err / (double)t) : 0.0f;
             r[D2D_INFO_TOTREW] = done ? (float)tot_rew : 0.0f;
             r[D2D_INFO_REWARD] = (float)reward;
         }
         if (done) {
             // finished-episode accumulators (info counters of drone_2d_env.py:593-613)
+            double pacc[D2D_NSTATS];
+#pragma unroll
+            for (int k = 0; k < D2D_NSTATS; ++k) pacc[k] = sh.acc[k][lane];
+            const double ape = GRP ? ape_g : path_err / (double)t;
             const bool c1 = cause & D2D_END_COLLISION, c2 = cause & D2D_END_REACH;
             const bool c4 = cause & D2D_END_TIMEUP, c5 = cause & D2D_END_AA;
-            fld(a.acc, D2D_ST_RETURN, n, i) = sh.acc[D2D_ST_RETURN][lane] + tot_rew;
-            fld(a.acc, D2D_ST_EPISODES, n, i) = sh.acc[D2D_ST_EPISODES][lane] + 1.0;
-            fld(a.acc, D2D_ST_SUCCESS, n, i) = sh.acc[D2D_ST_SUCCESS][lane] + (c2 ? 1.0 : 0.0);
-            fld(a.acc, D2D_ST_FAIL, n, i) = sh.acc[D2D_ST_FAIL][lane] + ((c1 || c4 || c5) ? 1.0 : 0.0);
-            fld(a.acc, D2D_ST_COLLISION, n, i) =
-                sh.acc[D2D_ST_COLLISION][lane] + ((c1 && !c2 && !c4 && !c5) ? 1.0 : 0.0);
-            fld(a.acc, D2D_ST_APE, n, i) = sh.acc[D2D_ST_APE][lane] + ape;
-            fld(a.acc, D2D_ST_LEN, n, i) = sh.acc[D2D_ST_LEN][lane] + (double)t;
+            fld(a.acc, D2D_ST_RETURN, n, i) = pacc[D2D_ST_RETURN] + tot_rew;
+            fld(a.acc, D2D_ST_EPISODES, n, i) = pacc[D2D_ST_EPISODES] + 1.0;
+            fld(a.acc, D2D_ST_SUCCESS, n, i) = pacc[D2D_ST_SUCCESS] + (c2 ? 1.0 : 0.0);
+            fld(a.acc, D2D_ST_FAIL, n, i) = pacc[D2D_ST_FAIL] + ((c1 || c4 || c5) ? 1.0 : 0.0);
+            fld(a.acc, D2D_ST_COLLISION, n, i) = pacc[D2D_ST_COLLISION] + ((c1 && !c2 && !c4 && !c5) ? 1.0 : 0.0);
+            fld(a.acc, D2D_ST_APE, n, i) = pacc[D2D_ST_APE] + ape;
+            fld(a.acc, D2D_ST_LEN, n, i) = pacc[D2D_ST_LEN] + (double)t;
         }
         if (!(done && auto_reset)) {
             fld(a.st, D2D_S_PATH_ERR, n, i) = path_err;
